@@ -1,0 +1,183 @@
+/*
+ * msl_hip.h — C-ABI of libmsl_hip.so, the MI355X (gfx950) kernels behind the
+ * DeepLabv2/ResNet-101 MaxSquare domain-adaptation training step.
+ *
+ * The reference (shiyutang/MaxSquareLoss) has no native code and no FFI: its
+ * boundary is the Python/nn.Module API.  Every entry point
+ * below replaces one implicit ATen/cuDNN op of that API; the reference site it
+ * stands in for is cited next to it (paths relative to the reference root).
+ *
+ * Conventions (all entry points):
+ *   - Tensors are fp32 NCHW with N = 1 (bs = 1 per GPU), i.e.
+ *     a [C][H][W] block; labels are int64 with -1 = ignore.
+ *   - All pointers are caller-owned device pointers (the PyTorch caching
+ *     allocator on the Python side).  The library allocates nothing and keeps
+ *     no per-call global state; scratch comes from the caller's workspace,
+ *     sized by the matching *_workspace() query.
+ *   - Work is enqueued on the given hipStream_t (passed as msl_stream_t) and
+ *     is stream-ordered; no entry point synchronises the host, so every call
+ *     is safe to capture in a hipGraph.
+ *   - Return value: 0 = MSL_OK, < 0 = argument / shape / workspace error
+ *     (see msl_status_string), > 0 = the hipError_t of a failed launch.
+ */
+#ifndef MSL_HIP_H
+#define MSL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* msl_stream_t; /* a hipStream_t */
+
+#define MSL_OK 0
+#define MSL_ERR_SHAPE (-1)
+#define MSL_ERR_WORKSPACE (-2)
+#define MSL_ERR_ARG (-3)
+
+int msl_abi_version(void);
+const char* msl_status_string(int status);
+
+/* ------------------------------------------------------------------------
+ * Dilated 3x3 convolution, stride 1, padding = dilation, as an FP32-MFMA
+ * implicit GEMM.  One call covers either a single conv (nbranch = 1:
+ * Bottleneck.conv2 of layer3 d=2 / layer4 d=4, deeplab_multi.py:17-18,82-83)
+ * or the live part of an ASPP head (nbranch = 2: conv_d6(x) + conv_d12(x) with
+ * biases, Classifier_Module.forward, deeplab_multi.py:62-66 incl. quirk Q1).
+ * Weights of branch b start at w + b*branch_stride, shape [cout][cin][3][3].
+ * ---------------------------------------------------------------------- */
+
+/* Elements of the packed operand produced by msl_dconv_pack (for_dgrad = 0:
+ * forward layout, 1: transposed + tap-flipped layout for the data gradient). */
+long long msl_dconv_packed_elems(int nbranch, int cin, int cout, int for_dgrad);
+int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin, int cout,
+                   int for_dgrad, float* packed, msl_stream_t stream);
+
+/* y[cout][h][w] = sum_b conv3x3(x, W_b, dil_b) (+ sum_b bias[b][cout] if bias)
+ * replaces nn.Conv2d.forward at deeplab_multi.py:35 (layer3/4) and :63-65 (ASPP). */
+size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w);
+int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
+                  int cin, int cout, int h, int w, int dil0, int dil1, void* ws, size_t ws_bytes,
+                  msl_stream_t stream);
+
+/* dx[cin][h][w] = sum_b conv3x3^T(dy, W_b, dil_b)   (autograd of the same sites) */
+size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w);
+int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
+                    int cout, int h, int w, int dil0, int dil1, void* ws, size_t ws_bytes,
+                    msl_stream_t stream);
+
+/* dw[b][cout][cin][3][3] (= or += when accumulate) and, if dbias != NULL,
+ * dbias[b][cout] = sum_px dy (identical for both branches). */
+size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w);
+int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
+                    int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                    size_t ws_bytes, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Bilinear upsample, align_corners=True (F.interpolate at deeplab_multi.py:124,
+ * :128).  The forward reproduces torch-CPU's rounding bit for bit.
+ * ---------------------------------------------------------------------- */
+int msl_upsample_fwd(const float* in, float* out, int c, int hi, int wi, int ho, int wo,
+                     msl_stream_t stream);
+size_t msl_upsample_bwd_workspace(int c, int hi, int wi, int ho, int wo);
+int msl_upsample_bwd(const float* gout, float* gin, int c, int hi, int wi, int ho, int wo,
+                     void* ws, size_t ws_bytes, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Fused losses on the *low-resolution* logits [c][hi][wi]: each kernel
+ * re-interpolates (bit-exact bilinear) to [c][ho][wo] on the fly, applies the
+ * softmax and the loss, and the backward returns the gradient w.r.t. the
+ * low-res logits directly (loss backward + softmax backward + upsample
+ * backward in one pass, deterministic gather form).  hi == ho, wi == wo is the
+ * identity interpolation, i.e. the plain hi-res loss.
+ *
+ * Every *_fwd writes a small device "stats" record consumed by *_bwd and the
+ * loss scalar to out[0]; gout is a device pointer to dL/d(loss).
+ * ---------------------------------------------------------------------- */
+size_t msl_loss_workspace(int c, int hi, int wi, int ho, int wo);
+int msl_loss_stats_elems(void); /* floats in a stats record */
+
+/* nn.CrossEntropyLoss(ignore_index=-1) (train_source.py:128, solve_gta5.py:226-231).
+ * out[0] = mean CE over valid pixels (nan if none, quirk Q8), stats = {sum, n_valid}. */
+int msl_ce_up_fwd(const float* logits, const int64_t* labels, int c, int hi, int wi, int ho,
+                  int wo, float* out, float* stats, void* ws, size_t ws_bytes,
+                  msl_stream_t stream);
+int msl_ce_up_bwd(const float* logits, const int64_t* labels, int c, int hi, int wi, int ho,
+                  int wo, const float* stats, const float* gout, float* dlogits, void* ws,
+                  size_t ws_bytes, msl_stream_t stream);
+
+/* MaxSquareloss (utils/loss.py:104-119): out[0] = -sum(p^2) / (2*C*H*W). */
+int msl_maxsquare_up_fwd(const float* logits, int c, int hi, int wi, int ho, int wo, float* out,
+                         float* stats, void* ws, size_t ws_bytes, msl_stream_t stream);
+int msl_maxsquare_up_bwd(const float* logits, int c, int hi, int wi, int ho, int wo,
+                         const float* stats, const float* gout, float* dlogits, void* ws,
+                         size_t ws_bytes, msl_stream_t stream);
+
+/* IW_MaxSquareloss (utils/loss.py:69-102): hist = per-class count of argmax p
+ * (int32, bit-exact), weights = 1/max(hist^r * (HW)^(1-r), 1),
+ * out[0] = -sum_px w[argmax] * sum_c p^2 / C.  hist/weights may be NULL. */
+int msl_iw_maxsquare_up_fwd(const float* logits, int c, int hi, int wi, int ho, int wo,
+                            float ratio, float* out, float* stats, int32_t* hist,
+                            float* weights, void* ws, size_t ws_bytes, msl_stream_t stream);
+int msl_iw_maxsquare_up_bwd(const float* logits, int c, int hi, int wi, int ho, int wo,
+                            const float* stats, const float* gout, float* dlogits, void* ws,
+                            size_t ws_bytes, msl_stream_t stream);
+
+/* Multi-level self-produced guidance (solve_gta5.py:206-213): P = softmax(up(x2)),
+ * P2 = softmax(up(x1)), label2 = (max P > thr | max P2 > thr) ? argmax((P+P2)/2) : -1,
+ * out[0] = CE(up(x1), label2) (mean over valid, nan if none).  The backward
+ * returns d/d x1 only (label2 is detached in the reference). */
+int msl_multi_ce_up_fwd(const float* logits1, const float* logits2, int c, int hi, int wi,
+                        int ho, int wo, float thr, float* out, float* stats, void* ws,
+                        size_t ws_bytes, msl_stream_t stream);
+int msl_multi_ce_up_bwd(const float* logits1, const float* logits2, int c, int hi, int wi,
+                        int ho, int wo, float thr, const float* stats, const float* gout,
+                        float* dlogits1, void* ws, size_t ws_bytes, msl_stream_t stream);
+
+/* Probability-input forms, for callers that hand the loss an explicit prob
+ * tensor exactly as the reference API does (loss.py:76, :110).
+ * prob is [c][hw]; label (nullable) is int64 [hw]. */
+int msl_maxsquare_prob_fwd(const float* prob, int c, int hw, float* out, void* ws,
+                           size_t ws_bytes, msl_stream_t stream);
+int msl_maxsquare_prob_bwd(const float* prob, int c, int hw, const float* gout, float* dprob,
+                           msl_stream_t stream);
+int msl_iw_maxsquare_prob_fwd(const float* prob, const int64_t* label, int c, int hw,
+                              float ratio, float* out, int32_t* hist, float* weights, void* ws,
+                              size_t ws_bytes, msl_stream_t stream);
+int msl_iw_maxsquare_prob_bwd(const float* prob, int c, int hw, const float* weights,
+                              const float* gout, float* dprob, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * SGD step with the reference's duplicated-parameter semantics (quirk Q2):
+ * torch.optim.SGD(momentum, weight_decay) single-tensor loop over the
+ * optim_parameters() groups (train_source.py:139-144, deeplab_multi.py:132-171),
+ * where a parameter listed k times receives k sequential updates sharing one
+ * momentum buffer.  One launch updates every entry.
+ * ---------------------------------------------------------------------- */
+typedef struct msl_sgd_entry {
+  float* param;       /* updated in place */
+  const float* grad;  /* read-only */
+  float* momentum;    /* momentum buffer, updated in place */
+  long long numel;
+  int mult;           /* occurrences of this parameter in its group (1, 3 or 4) */
+  int group;          /* 0: backbone (lr), 1: ASPP heads (10*lr) */
+  int has_buf;        /* 0 on the parameter's first step (buffer created = d) */
+  int pad_;
+} msl_sgd_entry;
+
+/* entries and block_entry live in device memory; block_entry[b] is the entry
+ * processed by block b (chunks of msl_sgd_block_elems() elements), built by
+ * msl_sgd_plan on the host. */
+int msl_sgd_block_elems(void);
+long long msl_sgd_plan(const long long* numels, int n_entries, int32_t* block_entry_host,
+                       long long* block_offset_host, long long max_blocks);
+int msl_sgd_step(const msl_sgd_entry* entries, const int32_t* block_entry,
+                 const long long* block_offset, long long n_blocks, float lr0, float lr1,
+                 float momentum, float weight_decay, float grad_scale, msl_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSL_HIP_H */

@@ -1,0 +1,570 @@
+// Dilated 3x3 convolution (stride 1, padding = dilation) as FP32-MFMA implicit
+// GEMMs on gfx950.  Replaces the cuDNN/oneDNN convolutions of
+//   - Bottleneck.conv2 in layer3 (d=2) and layer4 (d=4)   deeplab_multi.py:17-18, 82-83
+//   - the live ASPP branches conv_d6 + conv_d12 (+bias)    deeplab_multi.py:51-66, 84-85
+// forward, data gradient and weight gradient.
+//
+// Layout: activations are [C][P] fp32 with P = H*W (N = 1, NCHW).  The pixel
+// axis is tiled linearly (not in 2-D blocks): 65x129 maps do not tile in 2-D
+// without ~20 % waste, while 128-pixel linear tiles waste < 1 %.  A dilated tap
+// is then a constant shift of the linear pixel index plus a per-pixel validity
+// test (row wrap / image border), evaluated once per K-step per thread.
+//
+// GEMM mapping (MFMA v_mfma_f32_32x32x2_f32: exact f32 FMA chains):
+//   forward / dgrad:  C[m][p] = sum_k A[k][m] * B[k][p]
+//       k = ((branch*ncb + cb)*9 + tap)*16 + ci_local  (one tap, 16 channels per K-step)
+//       A = packed weights [Kp][lda] (m contiguous; dgrad: transposed + tap-flipped)
+//       B = image[cb*16 + ci_local][p + shift(tap)]  (zero outside the image)
+//   wgrad (one GEMM per tap, batched over grid.z):
+//       dW[m][n][tap] = sum_p dY[m][p] * X[n][p + shift(tap)]   (K = pixels)
+// Both operands are staged through LDS ([k][m] / [k][n], so every MFMA operand
+// read is a conflict-free ds_read_b32 of 32 consecutive floats), double
+// buffered, one barrier per K-step.  Small GEMMs are split along K into fp32
+// slabs that a reduce kernel sums deterministically (fixed order).
+#include "msl_internal.h"
+
+namespace msl {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kCB = 16;       // channels per forward K-step
+constexpr int kPackPad = 128; // packed-weight row padding (>= any BM)
+
+struct FwdArgs {
+  const float* A;     // packed weights [Kp][lda]
+  const float* B;     // image [cimg][P]
+  float* C;           // out [M][P] or slabs [S][M][P]
+  const float* bias;  // [nbias][M] or null (only used when S == 1)
+  int nbias;
+  int M, lda, H, W, P, cimg, ncb, dil0, dil1, ksteps, kps;
+  long long slab;
+};
+
+struct WgradArgs {
+  const float* dy;  // [M][P]
+  const float* x;   // [N][P]
+  float* C;         // dW [nbranch][M][N][9] or slabs of that
+  int M, N, H, W, P, dil0, dil1, ntap, ksteps, kps, accumulate;
+  long long slab, cbranch;
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
+  constexpr int BK = kCB;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  constexpr int LDA_S = BM + 4, LDB_S = BN + 4;
+  constexpr int A_STAGE = BK * LDA_S, STAGE = A_STAGE + BK * LDB_S;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int split = blockIdx.z;
+  const int s_begin = split * a.kps;
+  const int s_end = min(a.ksteps, s_begin + a.kps);
+
+  constexpr int BROWS = 256 / BN;
+  constexpr int BPASS = BK / BROWS;
+  const int bn = tid % BN, brow0 = tid / BN;
+  const int p = n0 + bn;
+  const int py = p / a.W, px = p - py * a.W;
+  const bool pin = p < a.P;
+
+  constexpr int A_F4_ROW = BM / 4;
+  constexpr int A_F4 = BK * A_F4_ROW;
+  constexpr int APASS = (A_F4 + 255) / 256;
+
+  float4 ra[APASS];
+  float rb[BPASS];
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int per_b = a.ncb * 9;
+  auto gload = [&](int s) {
+    const int b = s / per_b;
+    const int rem = s - b * per_b;
+    const int cb = rem / 9;
+    const int t = rem - cb * 9;
+    const int d = b ? a.dil1 : a.dil0;
+    const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
+    const bool v = pin && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
+    const int ci0 = cb * kCB + brow0;
+    const float* src = a.B + (long long)ci0 * a.P + (p + dh * a.W + dw);
+#pragma unroll
+    for (int j = 0; j < BPASS; ++j) {
+      const int ci = ci0 + j * BROWS;
+      rb[j] = (v && ci < a.cimg) ? src[(long long)(j * BROWS) * a.P] : 0.f;
+    }
+    const float* ab = a.A + (long long)s * BK * a.lda + m0;
+#pragma unroll
+    for (int i = 0; i < APASS; ++i) {
+      const int idx = tid + i * 256;
+      if (A_F4 % 256 == 0 || idx < A_F4) {
+        const int r = idx / A_F4_ROW, c4 = idx - r * A_F4_ROW;
+        ra[i] = *reinterpret_cast<const float4*>(ab + (long long)r * a.lda + c4 * 4);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    float* As = smem + buf * STAGE;
+    float* Bs = As + A_STAGE;
+#pragma unroll
+    for (int i = 0; i < APASS; ++i) {
+      const int idx = tid + i * 256;
+      if (A_F4 % 256 == 0 || idx < A_F4) {
+        const int r = idx / A_F4_ROW, c4 = idx - r * A_F4_ROW;
+        *reinterpret_cast<float4*>(As + r * LDA_S + c4 * 4) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BPASS; ++j) Bs[(brow0 + j * BROWS) * LDB_S + bn] = rb[j];
+  };
+  auto compute = [&](int buf) {
+    const float* As = smem + buf * STAGE;
+    const float* Bs = As + A_STAGE;
+    const int l32 = lane & 31, kh = lane >> 5;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const int kr = kk + kh;
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = As[kr * LDA_S + wm + i * 32 + l32];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = Bs[kr * LDB_S + wn + j * 32 + l32];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (s_begin < s_end) {
+    gload(s_begin);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int s = s_begin; s < s_end; ++s) {
+      const bool more = s + 1 < s_end;
+      if (more) gload(s + 1);
+      compute(cur);
+      if (more) sstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  float* C = a.C + (long long)split * a.slab;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + j * 32 + (lane & 31);
+        if (m < a.M && n < a.P) {
+          float v = acc[i][j][r];
+          if (a.bias) {
+            float bsum = a.bias[m];
+            for (int b = 1; b < a.nbias; ++b) bsum += a.bias[b * a.M + m];
+            v += bsum;
+          }
+          C[(long long)m * a.P + n] = v;
+        }
+      }
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) k_igemm_wgrad(WgradArgs a) {
+  constexpr int BK = 32;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  constexpr int LDA_S = BM + 1, LDB_S = BN + 1;  // odd strides: transposing writes are conflict-free
+  constexpr int A_STAGE = BK * LDA_S, STAGE = A_STAGE + BK * LDB_S;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int tapz = blockIdx.z % a.ntap;
+  const int split = blockIdx.z / a.ntap;
+  const int br = tapz / 9, t = tapz - br * 9;
+  const int d = br ? a.dil1 : a.dil0;
+  const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
+  const int s_begin = split * a.kps;
+  const int s_end = min(a.ksteps, s_begin + a.kps);
+
+  const int kl = tid & 31, r0 = tid >> 5;
+  constexpr int APASS = BM / 8, BPASS = BN / 8;
+  float ra[APASS], rb[BPASS];
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto gload = [&](int s) {
+    const int p = s * BK + kl;
+    const bool pv = p < a.P;
+    const int py = p / a.W, px = p - py * a.W;
+    const bool vb = pv && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
+    const int off = p + dh * a.W + dw;
+#pragma unroll
+    for (int j = 0; j < APASS; ++j) {
+      const int m = m0 + r0 + 8 * j;
+      ra[j] = (pv && m < a.M) ? a.dy[(long long)m * a.P + p] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < BPASS; ++j) {
+      const int n = n0 + r0 + 8 * j;
+      rb[j] = (vb && n < a.N) ? a.x[(long long)n * a.P + off] : 0.f;
+    }
+  };
+  auto sstore = [&](int buf) {
+    float* As = smem + buf * STAGE;
+    float* Bs = As + A_STAGE;
+#pragma unroll
+    for (int j = 0; j < APASS; ++j) As[kl * LDA_S + r0 + 8 * j] = ra[j];
+#pragma unroll
+    for (int j = 0; j < BPASS; ++j) Bs[kl * LDB_S + r0 + 8 * j] = rb[j];
+  };
+  auto compute = [&](int buf) {
+    const float* As = smem + buf * STAGE;
+    const float* Bs = As + A_STAGE;
+    const int l32 = lane & 31, kh = lane >> 5;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const int kr = kk + kh;
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = As[kr * LDA_S + wm + i * 32 + l32];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = Bs[kr * LDB_S + wn + j * 32 + l32];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (s_begin < s_end) {
+    gload(s_begin);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int s = s_begin; s < s_end; ++s) {
+      const bool more = s + 1 < s_end;
+      if (more) gload(s + 1);
+      compute(cur);
+      if (more) sstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  float* C = a.C + (long long)split * a.slab + (long long)br * a.cbranch;
+  const long long ldc = (long long)a.N * 9;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + j * 32 + (lane & 31);
+        if (m < a.M && n < a.N) {
+          const long long idx = (long long)m * ldc + (long long)n * 9 + t;
+          C[idx] = a.accumulate ? C[idx] + acc[i][j][r] : acc[i][j][r];
+        }
+      }
+}
+
+// out[i] = (acc ? out[i] : 0) + sum_s ws[s*n + i] (+ sum_b bias[b*M + i/bias_div])
+__global__ void __launch_bounds__(256) k_reduce_slabs(const float* __restrict__ ws, int S, long long n,
+                                                       float* __restrict__ out, int accumulate,
+                                                       const float* __restrict__ bias, int nbias,
+                                                       int bias_M, int bias_div) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float v = ws[i];
+    for (int s = 1; s < S; ++s) v += ws[(long long)s * n + i];
+    if (bias) {
+      const int m = (int)(i / bias_div);
+      float bsum = bias[m];
+      for (int b = 1; b < nbias; ++b) bsum += bias[b * bias_M + m];
+      v += bsum;
+    }
+    out[i] = accumulate ? out[i] + v : v;
+  }
+}
+
+// dbias[b][m] (=|+=) sum_p dy[m][p], same value for every branch b.
+__global__ void __launch_bounds__(256) k_bias_grad(const float* __restrict__ dy, int P,
+                                                    float* __restrict__ db, int M, int nbranch,
+                                                    int accumulate) {
+  const int m = blockIdx.x;
+  float s = 0.f;
+  for (int p = threadIdx.x; p < P; p += 256) s += dy[(long long)m * P + p];
+  s = wave_sum(s);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tot = (part[0] + part[1]) + (part[2] + part[3]);
+    for (int b = 0; b < nbranch; ++b) db[b * M + m] = accumulate ? db[b * M + m] + tot : tot;
+  }
+}
+
+// Packed operand for the forward-form GEMM.
+//   for_dgrad = 0: image = x (cin channels),  m = co: P[k][co] = W[co][ci][t]
+//   for_dgrad = 1: image = dy (cout channels), m = ci: P[k][ci] = W[co][ci][8 - t]
+// k = ((b*ncb + cb)*9 + t)*16 + c_local with c = cb*16 + c_local (image channel).
+__global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long long branch_stride,
+                                               int cin, int cout, int for_dgrad, int ncb, int lda,
+                                               long long total, float* __restrict__ out) {
+  const int cimg = for_dgrad ? cout : cin;
+  const int mreal = for_dgrad ? cin : cout;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int m = (int)(e % lda);
+    const long long k = e / lda;
+    const int cl = (int)(k % kCB);
+    const long long q = k / kCB;
+    const int t = (int)(q % 9);
+    const long long q2 = q / 9;
+    const int cb = (int)(q2 % ncb);
+    const int b = (int)(q2 / ncb);
+    const int c = cb * kCB + cl;
+    float v = 0.f;
+    if (c < cimg && m < mreal) {
+      const float* wb = w + (long long)b * branch_stride;
+      if (!for_dgrad)
+        v = wb[((long long)m * cin + c) * 9 + t];
+      else
+        v = wb[((long long)c * cin + m) * 9 + (8 - t)];
+    }
+    out[e] = v;
+  }
+}
+
+// ---------------------------------------------------------------- planning
+struct FwdPlan {
+  int bm, bn, tiles_m, tiles_n, ksteps, kps, S;
+};
+
+static int pad_to(int v, int a) { return (v + a - 1) / a * a; }
+
+static int choose_split(int tiles, int ksteps, int min_steps) {
+  const int target = 512;  // 256 CUs x 2 resident workgroups
+  if (tiles >= 384) return 1;
+  int S = (target + tiles - 1) / tiles;
+  S = std::max(1, std::min(S, ksteps / min_steps));
+  return S;
+}
+
+static FwdPlan plan_fwd(int nbranch, int cimg, int M, int P) {
+  FwdPlan pl;
+  pl.bm = 64;
+  pl.bn = 128;
+  pl.tiles_m = cdiv(M, pl.bm);
+  pl.tiles_n = cdiv(P, pl.bn);
+  pl.ksteps = nbranch * cdiv(cimg, kCB) * 9;
+  int S = choose_split(pl.tiles_m * pl.tiles_n, pl.ksteps, 8);
+  pl.kps = cdiv(pl.ksteps, S);
+  pl.S = cdiv(pl.ksteps, pl.kps);
+  return pl;
+}
+
+struct WgradPlan {
+  int bm, bn, tiles_m, tiles_n, ntap, ksteps, kps, S;
+};
+
+static WgradPlan plan_wgrad(int nbranch, int cin, int cout, int P) {
+  WgradPlan pl;
+  pl.bm = 64;
+  pl.bn = 128;
+  pl.tiles_m = cdiv(cout, pl.bm);
+  pl.tiles_n = cdiv(cin, pl.bn);
+  pl.ntap = nbranch * 9;
+  pl.ksteps = cdiv(P, 32);
+  int S = choose_split(pl.tiles_m * pl.tiles_n * pl.ntap, pl.ksteps, 8);
+  pl.kps = cdiv(pl.ksteps, S);
+  pl.S = cdiv(pl.ksteps, pl.kps);
+  return pl;
+}
+
+static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
+  return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
+}
+
+static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
+                           int nbias, float* out, int nbranch, int h, int w, int dil0, int dil1,
+                           void* ws, size_t ws_bytes, hipStream_t st) {
+  const int P = h * w;
+  FwdPlan pl = plan_fwd(nbranch, cimg, M, P);
+  if (ws_bytes < fwd_ws_bytes(pl, M, P)) return MSL_ERR_WORKSPACE;
+  FwdArgs a;
+  a.A = packed;
+  a.B = img;
+  a.C = pl.S > 1 ? (float*)ws : out;
+  a.bias = pl.S > 1 ? nullptr : bias;
+  a.nbias = nbias;
+  a.M = M;
+  a.lda = pad_to(M, kPackPad);
+  a.H = h;
+  a.W = w;
+  a.P = P;
+  a.cimg = cimg;
+  a.ncb = cdiv(cimg, kCB);
+  a.dil0 = dil0;
+  a.dil1 = dil1;
+  a.ksteps = pl.ksteps;
+  a.kps = pl.kps;
+  a.slab = (long long)M * P;
+  dim3 grid(pl.tiles_n, pl.tiles_m, pl.S);
+  hipLaunchKernelGGL((k_igemm_fwd<64, 128, 2, 2>), grid, dim3(256), 0, st, a);
+  MSL_CHECK_LAUNCH();
+  if (pl.S > 1) {
+    const long long n = (long long)M * P;
+    const int blocks = (int)std::min<long long>(cdiv(n, 256), 4096);
+    hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, (const float*)ws, pl.S, n,
+                       out, 0, bias, nbias, M, P);
+    MSL_CHECK_LAUNCH();
+  }
+  return MSL_OK;
+}
+
+static bool bad_dims(int nbranch, int cin, int cout, int h, int w) {
+  return nbranch < 1 || nbranch > 2 || cin < 1 || cout < 1 || h < 1 || w < 1 ||
+         (long long)h * w > (1LL << 30);
+}
+
+}  // namespace msl
+
+using namespace msl;
+
+extern "C" {
+
+int msl_abi_version(void) { return MSL_ABI_VERSION; }
+
+const char* msl_status_string(int status) {
+  switch (status) {
+    case MSL_OK: return "ok";
+    case MSL_ERR_SHAPE: return "invalid shape";
+    case MSL_ERR_WORKSPACE: return "workspace too small";
+    case MSL_ERR_ARG: return "invalid argument";
+    default: return status > 0 ? hipGetErrorString((hipError_t)status) : "unknown error";
+  }
+}
+
+long long msl_dconv_packed_elems(int nbranch, int cin, int cout, int for_dgrad) {
+  const int cimg = for_dgrad ? cout : cin;
+  const int m = for_dgrad ? cin : cout;
+  return (long long)nbranch * cdiv(cimg, kCB) * 9 * kCB * pad_to(m, kPackPad);
+}
+
+int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin, int cout,
+                   int for_dgrad, float* packed, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, 1, 1) || !w || !packed) return MSL_ERR_ARG;
+  const int cimg = for_dgrad ? cout : cin;
+  const int m = for_dgrad ? cin : cout;
+  const long long total = msl_dconv_packed_elems(nbranch, cin, cout, for_dgrad);
+  const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
+  hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, as_stream(stream), w, branch_stride, cin,
+                     cout, for_dgrad, cdiv(cimg, kCB), pad_to(m, kPackPad), total, packed);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w) {
+  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
+  FwdPlan pl = plan_fwd(nbranch, cin, cout, h * w);
+  return fwd_ws_bytes(pl, cout, h * w);
+}
+
+int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
+                  int cin, int cout, int h, int w, int dil0, int dil1, void* ws, size_t ws_bytes,
+                  msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_fwd_form(x, cin, packed, cout, bias, nbranch, y, nbranch, h, w, dil0, dil1, ws,
+                         ws_bytes, as_stream(stream));
+}
+
+size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
+  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
+  FwdPlan pl = plan_fwd(nbranch, cout, cin, h * w);
+  return fwd_ws_bytes(pl, cin, h * w);
+}
+
+int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
+                    int cout, int h, int w, int dil0, int dil1, void* ws, size_t ws_bytes,
+                    msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_fwd_form(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, h, w, dil0, dil1,
+                         ws, ws_bytes, as_stream(stream));
+}
+
+size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
+  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
+  WgradPlan pl = plan_wgrad(nbranch, cin, cout, h * w);
+  return pl.S > 1 ? (size_t)pl.S * nbranch * cout * cin * 9 * sizeof(float) : 0;
+}
+
+int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
+                    int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                    size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  hipStream_t st = as_stream(stream);
+  const int P = h * w;
+  WgradPlan pl = plan_wgrad(nbranch, cin, cout, P);
+  const long long nout = (long long)nbranch * cout * cin * 9;
+  if (pl.S > 1 && ws_bytes < (size_t)pl.S * nout * sizeof(float)) return MSL_ERR_WORKSPACE;
+  WgradArgs a;
+  a.dy = dy;
+  a.x = x;
+  a.C = pl.S > 1 ? (float*)ws : dw;
+  a.M = cout;
+  a.N = cin;
+  a.H = h;
+  a.W = w;
+  a.P = P;
+  a.dil0 = dil0;
+  a.dil1 = dil1;
+  a.ntap = pl.ntap;
+  a.ksteps = pl.ksteps;
+  a.kps = pl.kps;
+  a.accumulate = pl.S > 1 ? 0 : accumulate;
+  a.slab = nout;
+  a.cbranch = (long long)cout * cin * 9;
+  dim3 grid(pl.tiles_n, pl.tiles_m, pl.S * pl.ntap);
+  hipLaunchKernelGGL((k_igemm_wgrad<64, 128, 2, 2>), grid, dim3(256), 0, st, a);
+  MSL_CHECK_LAUNCH();
+  if (pl.S > 1) {
+    const int blocks = (int)std::min<long long>(cdiv(nout, 256), 4096);
+    hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, (const float*)ws, pl.S, nout,
+                       dw, accumulate, (const float*)nullptr, 0, 1, 1);
+    MSL_CHECK_LAUNCH();
+  }
+  if (dbias) {
+    hipLaunchKernelGGL(k_bias_grad, dim3(cout), dim3(256), 0, st, dy, P, dbias, cout, nbranch,
+                       accumulate);
+    MSL_CHECK_LAUNCH();
+  }
+  return MSL_OK;
+}
+
+}  // extern "C"

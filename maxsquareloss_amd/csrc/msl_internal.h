@@ -1,0 +1,37 @@
+// Internal helpers shared by the libmsl_hip.so translation units (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+#include "../../include/msl_hip.h"
+
+#define MSL_ABI_VERSION 1
+
+#define MSL_CHECK_LAUNCH()                         \
+  do {                                             \
+    hipError_t e_ = hipGetLastError();             \
+    if (e_ != hipSuccess) return (int)e_;          \
+  } while (0)
+
+namespace msl {
+
+static inline hipStream_t as_stream(msl_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// 64-lane wave reductions (CDNA wave = 64).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace msl

@@ -1,0 +1,187 @@
+"""DeepLabv2 / ResNet-101 "multi" model with the MI355X hot path.
+
+Drop-in for graphs/models/deeplab_multi.py of the reference:
+  - same constructor `DeeplabMulti(num_classes=21, pretrained=True)` (:174),
+  - same module tree and state_dict keys (`layer3.5.conv2.weight`,
+    `layer6.conv2d_list.1.bias`, ...),
+  - same `forward(x) -> (x2, x1)` (layer6 head, layer5 head) (:113-130),
+  - same `optim_parameters(args)` groups, duplicates included (:132-171, Q2).
+
+What runs where:
+  - every stride-1 3x3 Bottleneck.conv2 (dilation 2 in layer3, 4 in layer4, and
+    1 in layers 1-2) -> `DilatedConv3x3`, HIP implicit-GEMM kernels (fwd, dgrad,
+    wgrad) on FP32 MFMA;
+  - the ASPP heads (live branches d=6 and d=12 only, quirk Q1) -> one fused
+    two-branch HIP conv with both biases;
+  - bilinear upsampling (align_corners=True) -> HIP kernel; the result keeps a
+    handle on the low-res logits for the fused losses;
+  - stem, 1x1 convs, BatchNorm (train mode, per replica, Q9), ReLU, maxpool ->
+    PyTorch-ROCm (MIOpen), SURVEY.md §8a row a13.
+"""
+import torch
+import torch.nn as nn
+
+from ... import ops
+
+affine_par = True
+
+
+class DilatedConv3x3(nn.Conv2d):
+    """nn.Conv2d(c, c, 3, stride=1, padding=d, dilation=d, bias=False) on the HIP kernels."""
+
+    def __init__(self, in_channels, out_channels, dilation=1):
+        super().__init__(in_channels, out_channels, kernel_size=3, stride=1, padding=dilation,
+                         dilation=dilation, bias=False)
+        self._pack = ops.PackCache()
+
+    def forward(self, x):
+        return ops.dconv3x3(x, self.weight, self.dilation[0], self._pack)
+
+
+class Bottleneck(nn.Module):
+    """deeplab_multi.py:8-48 (Caffe-style: the stride sits on conv1)."""
+
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, dilation=1, downsample=None, bn_momentum=0.1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, kernel_size=1, stride=stride, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes, affine=affine_par)
+        self.conv2 = DilatedConv3x3(planes, planes, dilation=dilation)
+        self.bn2 = nn.BatchNorm2d(planes, affine=affine_par)
+        self.conv3 = nn.Conv2d(planes, planes * 4, kernel_size=1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4, affine=affine_par)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        residual = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            residual = self.downsample(x)
+        out += residual
+        return self.relu(out)
+
+
+class Classifier_Module(nn.Module):
+    """ASPP head (deeplab_multi.py:51-66).
+
+    The reference returns inside its loop, so only conv2d_list[0] (d=6) and
+    conv2d_list[1] (d=12) ever run (quirk Q1); branches 2 and 3 exist for
+    state_dict compatibility and never receive gradients.
+    """
+
+    def __init__(self, inplanes, dilation_series, padding_series, num_classes):
+        super().__init__()
+        self.conv2d_list = nn.ModuleList()
+        for dilation, padding in zip(dilation_series, padding_series):
+            self.conv2d_list.append(nn.Conv2d(inplanes, num_classes, kernel_size=3, stride=1,
+                                              padding=padding, dilation=dilation, bias=True))
+        for m in self.conv2d_list:
+            m.weight.data.normal_(0, 0.01)
+        self._pack = ops.PackCache()
+
+    def forward(self, x):
+        c0, c1 = self.conv2d_list[0], self.conv2d_list[1]
+        return ops.aspp2(x, c0.weight, c0.bias, c1.weight, c1.bias, c0.dilation[0], c1.dilation[0],
+                         self._pack)
+
+
+class ResNetMulti(nn.Module):
+    """deeplab_multi.py:69-171."""
+
+    def __init__(self, block, layers, num_classes):
+        self.inplanes = 64
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64, affine=affine_par)
+        for i in self.bn1.parameters():
+            i.requires_grad = False
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1, ceil_mode=True)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=1, dilation=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=1, dilation=4)
+        self.layer5 = self._make_pred_layer(Classifier_Module, 1024, [6, 12, 18, 24], [6, 12, 18, 24], num_classes)
+        self.layer6 = self._make_pred_layer(Classifier_Module, 2048, [6, 12, 18, 24], [6, 12, 18, 24], num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                m.weight.data.normal_(0, 0.01)
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.data.fill_(1)
+                m.bias.data.zero_()
+
+    def _make_layer(self, block, planes, blocks, stride=1, dilation=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion or dilation == 2 or dilation == 4:
+            downsample = nn.Sequential(
+                nn.Conv2d(self.inplanes, planes * block.expansion, kernel_size=1, stride=stride, bias=False),
+                nn.BatchNorm2d(planes * block.expansion, affine=affine_par))
+        layers = [block(self.inplanes, planes, stride, dilation=dilation, downsample=downsample)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes, dilation=dilation))
+        return nn.Sequential(*layers)
+
+    def _make_pred_layer(self, block, inplanes, dilation_series, padding_series, num_classes):
+        return block(inplanes, dilation_series, padding_series, num_classes)
+
+    def forward(self, x):
+        input_size = x.size()[2:]
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer1(x)
+        x = self.layer2(x)
+        x = self.layer3(x)
+        x1 = self.layer5(x)
+        x1 = ops.upsample_bilinear(x1, input_size)
+        x2 = self.layer4(x)
+        x2 = self.layer6(x2)
+        x2 = ops.upsample_bilinear(x2, input_size)
+        return x2, x1
+
+    def get_1x_lr_params_NOscale(self):
+        """Backbone parameters, each yielded once per enclosing module (quirk Q2)."""
+        b = [self.conv1, self.bn1, self.layer1, self.layer2, self.layer3, self.layer4]
+        for i in range(len(b)):
+            for j in b[i].modules():
+                for k in j.parameters():
+                    if k.requires_grad:
+                        yield k
+
+    def get_10x_lr_params(self):
+        b = [self.layer5.parameters(), self.layer6.parameters()]
+        for j in range(len(b)):
+            for i in b[j]:
+                yield i
+
+    def optim_parameters(self, args):
+        return [{'params': self.get_1x_lr_params_NOscale(), 'lr': args.lr},
+                {'params': self.get_10x_lr_params(), 'lr': 10 * args.lr}]
+
+
+def DeeplabMulti(num_classes=21, pretrained=True):
+    """deeplab_multi.py:174-187.  `pretrained=True` needs the reference's ImageNet
+    checkpoint (an absent /data path); load it with `load_pretrained`."""
+    model = ResNetMulti(Bottleneck, [3, 4, 23, 3], num_classes)
+    if pretrained:
+        raise FileNotFoundError(
+            "DeeplabMulti(pretrained=True): the reference's ImageNet init checkpoint "
+            "(DeepLab_resnet_pretrained_init-f81d91e8.pth) is not available offline; pass "
+            "pretrained=False or call load_pretrained(model, path)")
+    return model
+
+
+def load_pretrained(model, restore_from):
+    """Load the reference's init checkpoint, skipping layer5 like deeplab_multi.py:177-186."""
+    saved_state_dict = torch.load(restore_from, map_location="cpu", weights_only=True)
+    new_params = model.state_dict().copy()
+    for i in saved_state_dict:
+        i_parts = i.split('.')
+        if not i_parts[1] == 'layer5':
+            new_params['.'.join(i_parts[1:])] = saved_state_dict[i]
+    model.load_state_dict(new_params)
+    return model

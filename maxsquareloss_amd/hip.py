@@ -1,0 +1,97 @@
+"""ctypes binding of libmsl_hip.so (the C-ABI declared in include/msl_hip.h).
+
+This is the only place the product path reaches native code.  There is no
+fallback: if the library is missing or no GPU is visible, every compute call
+raises.  `import torch` happens before the library is loaded so that its
+libamdhip64.so.7 dependency resolves to the HIP runtime torch already mapped
+(one runtime per process, so torch's hipStream_t handles are valid here).
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmsl_hip.so")
+
+c_int, c_ll, c_sz, c_f, c_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p
+
+# name -> (restype, argtypes); must match include/msl_hip.h exactly.
+SIGNATURES = {
+    "msl_abi_version": (c_int, []),
+    "msl_status_string": (ctypes.c_char_p, [c_int]),
+    "msl_dconv_packed_elems": (c_ll, [c_int, c_int, c_int, c_int]),
+    "msl_dconv_pack": (c_int, [c_p, c_ll, c_int, c_int, c_int, c_int, c_p, c_p]),
+    "msl_dconv_fwd_workspace": (c_sz, [c_int] * 5),
+    "msl_dconv_fwd": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_sz, c_p]),
+    "msl_dconv_dgrad_workspace": (c_sz, [c_int] * 5),
+    "msl_dconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_sz, c_p]),
+    "msl_dconv_wgrad_workspace": (c_sz, [c_int] * 5),
+    "msl_dconv_wgrad": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p]),
+    "msl_upsample_fwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p]),
+    "msl_upsample_bwd_workspace": (c_sz, [c_int] * 5),
+    "msl_upsample_bwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p, c_sz, c_p]),
+    "msl_loss_workspace": (c_sz, [c_int] * 5),
+    "msl_loss_stats_elems": (c_int, []),
+    "msl_ce_up_fwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p, c_p, c_p, c_sz, c_p]),
+    "msl_ce_up_bwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "msl_maxsquare_up_fwd": (c_int, [c_p] + [c_int] * 5 + [c_p, c_p, c_p, c_sz, c_p]),
+    "msl_maxsquare_up_bwd": (c_int, [c_p] + [c_int] * 5 + [c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "msl_iw_maxsquare_up_fwd": (c_int, [c_p] + [c_int] * 5 + [c_f, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "msl_iw_maxsquare_up_bwd": (c_int, [c_p] + [c_int] * 5 + [c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "msl_multi_ce_up_fwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_f, c_p, c_p, c_p, c_sz, c_p]),
+    "msl_multi_ce_up_bwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_f, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "msl_maxsquare_prob_fwd": (c_int, [c_p, c_int, c_int, c_p, c_p, c_sz, c_p]),
+    "msl_maxsquare_prob_bwd": (c_int, [c_p, c_int, c_int, c_p, c_p, c_p]),
+    "msl_iw_maxsquare_prob_fwd": (c_int, [c_p, c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "msl_iw_maxsquare_prob_bwd": (c_int, [c_p, c_int, c_int, c_p, c_p, c_p, c_p]),
+    "msl_sgd_block_elems": (c_int, []),
+    "msl_sgd_plan": (c_ll, [c_p, c_int, c_p, c_p, c_ll]),
+    "msl_sgd_step": (c_int, [c_p, c_p, c_p, c_ll, c_f, c_f, c_f, c_f, c_f, c_p]),
+}
+
+ABI_VERSION = 1
+_lib = None
+
+
+class MSLError(RuntimeError):
+    pass
+
+
+def load(require_gpu=True):
+    """Load libmsl_hip.so and declare every C-ABI symbol.  Raises if absent."""
+    global _lib
+    if require_gpu and not torch.cuda.is_available():
+        raise MSLError("maxsquareloss_amd: no GPU visible; the HIP path has no CPU fallback")
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MSLError(f"maxsquareloss_amd: {LIB_PATH} is missing; run __graft_entry__.build() "
+                       "(make -C maxsquareloss_amd/csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.msl_abi_version() != ABI_VERSION:
+        raise MSLError("libmsl_hip.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = load(require_gpu=False).msl_status_string(status).decode()
+        raise MSLError(f"{what} failed: {msg} (status {status})")
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def workspace(nbytes, device):
+    """Scratch from the caching allocator (stream-ordered reuse, no sync)."""
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)

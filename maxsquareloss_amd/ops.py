@@ -1,0 +1,390 @@
+"""torch.autograd wrappers over the HIP kernels of libmsl_hip.so.
+
+Each Function is a thin shim: shape checks on the host, then one or two C-ABI
+calls on torch's current HIP stream.  Tensors are bs=1 NCHW fp32 (the
+reference only runs bs=1: IW_MaxSquareloss broadcasts (N,H,W) weights against
+(N,C,H,W) probabilities, which only works for N=1 - SURVEY.md quirk Q3).
+"""
+import torch
+from torch.autograd import Function
+
+from . import hip
+
+_f32 = torch.float32
+
+
+def _check_act(x, name):
+    if not x.is_cuda or x.dtype != _f32 or x.dim() != 4 or x.size(0) != 1:
+        raise hip.MSLError(f"{name}: expected a CUDA fp32 tensor of shape (1,C,H,W), got "
+                           f"{tuple(x.shape)} {x.dtype} {x.device}")
+    return x.contiguous()
+
+
+# --------------------------------------------------------------------------- packing cache
+class PackCache:
+    """Packed copies of a conv's weights, rebuilt when any weight changes.
+
+    The forward GEMM wants W as [k = (tap, 16-channel block)][cout] and the
+    data gradient wants the transposed, tap-flipped layout; both are derived
+    from the parameters once per optimizer step (keyed on the tensors'
+    in-place version counters), not once per call.
+    """
+
+    def __init__(self):
+        self.key = {0: None, 1: None}
+        self.buf = {0: None, 1: None}
+
+    def get(self, weights, cin, cout, for_dgrad):
+        key = tuple((w.data_ptr(), w._version) for w in weights)
+        if self.key[for_dgrad] != key:
+            lib = hip.load()
+            nb = len(weights)
+            total = lib.msl_dconv_packed_elems(nb, cin, cout, for_dgrad)
+            per_branch = total // nb
+            buf = self.buf[for_dgrad]
+            if buf is None or buf.numel() != total or buf.device != weights[0].device:
+                buf = torch.empty(total, dtype=_f32, device=weights[0].device)
+            s = hip.stream_ptr()
+            for b, w in enumerate(weights):
+                wc = w.detach().contiguous()
+                hip.check(lib.msl_dconv_pack(wc.data_ptr(), 0, 1, cin, cout, for_dgrad,
+                                             buf.data_ptr() + 4 * b * per_branch, s),
+                          "msl_dconv_pack")
+            self.buf[for_dgrad] = buf
+            self.key[for_dgrad] = key
+        return self.buf[for_dgrad]
+
+
+# --------------------------------------------------------------------------- dilated conv
+class _DConv3x3(Function):
+    """sum_b conv3x3(x, W_b, dilation d_b) (+ sum_b bias_b); nbranch in {1, 2}."""
+
+    @staticmethod
+    def forward(ctx, x, w0, w1, b0, b1, dil0, dil1, cache):
+        x = _check_act(x, "dconv3x3")
+        weights = [w0] if w1 is None else [w0, w1]
+        nb = len(weights)
+        cout, cin = w0.shape[0], w0.shape[1]
+        if w0.shape[2:] != (3, 3) or x.size(1) != cin:
+            raise hip.MSLError(f"dconv3x3: weight {tuple(w0.shape)} does not match input {tuple(x.shape)}")
+        h, w = x.shape[2], x.shape[3]
+        lib = hip.load()
+        packed = cache.get(weights, cin, cout, 0)
+        bias = None
+        if b0 is not None:
+            bias = torch.stack([b0] if nb == 1 else [b0, b1]).contiguous()
+        y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
+        wsb = lib.msl_dconv_fwd_workspace(nb, cin, cout, h, w)
+        ws = hip.workspace(wsb, x.device)
+        hip.check(lib.msl_dconv_fwd(x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb,
+                                    cin, cout, h, w, dil0, dil1 if nb > 1 else 0, ws.data_ptr(), wsb,
+                                    hip.stream_ptr()), "msl_dconv_fwd")
+        ctx.save_for_backward(x, *weights)
+        ctx.meta = (nb, cin, cout, h, w, dil0, dil1, b0 is not None, cache)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, *weights = ctx.saved_tensors
+        nb, cin, cout, h, w, dil0, dil1, has_bias, cache = ctx.meta
+        gy = gy.contiguous()
+        lib = hip.load()
+        s = hip.stream_ptr()
+        d1 = dil1 if nb > 1 else 0
+        dx = None
+        if ctx.needs_input_grad[0]:
+            packed_d = cache.get(weights, cin, cout, 1)
+            dx = torch.empty_like(x)
+            wsb = lib.msl_dconv_dgrad_workspace(nb, cin, cout, h, w)
+            ws = hip.workspace(wsb, x.device)
+            hip.check(lib.msl_dconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin,
+                                          cout, h, w, dil0, d1, ws.data_ptr(), wsb, s), "msl_dconv_dgrad")
+        dw_all = torch.empty((nb, cout, cin, 3, 3), dtype=_f32, device=x.device)
+        db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
+        wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w)
+        ws = hip.workspace(wsb, x.device)
+        hip.check(lib.msl_dconv_wgrad(x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb,
+                                      cin, cout, h, w, dil0, d1, 0, ws.data_ptr(), wsb, s), "msl_dconv_wgrad")
+        dw0 = dw_all[0]
+        dw1 = dw_all[1] if nb > 1 else None
+        db0 = db_all[0] if has_bias else None
+        db1 = db_all[1] if (has_bias and nb > 1) else None
+        return dx, dw0, dw1, db0, db1, None, None, None
+
+
+def dconv3x3(x, weight, dilation, cache):
+    """Stride-1, padding=dilation, bias-free 3x3 conv (Bottleneck.conv2, deeplab_multi.py:17-18)."""
+    return _DConv3x3.apply(x, weight, None, None, None, int(dilation), 0, cache)
+
+
+def aspp2(x, w0, b0, w1, b1, dil0, dil1, cache):
+    """conv_d6(x) + conv_d12(x) with biases: the live part of Classifier_Module (deeplab_multi.py:62-66)."""
+    return _DConv3x3.apply(x, w0, w1, b0, b1, int(dil0), int(dil1), cache)
+
+
+# --------------------------------------------------------------------------- upsample
+class _Upsample(Function):
+    @staticmethod
+    def forward(ctx, x, ho, wo):
+        x = _check_act(x, "upsample")
+        c, hi, wi = x.shape[1:]
+        y = torch.empty((1, c, ho, wo), dtype=_f32, device=x.device)
+        hip.check(hip.load().msl_upsample_fwd(x.data_ptr(), y.data_ptr(), c, hi, wi, ho, wo,
+                                              hip.stream_ptr()), "msl_upsample_fwd")
+        ctx.meta = (c, hi, wi, ho, wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        c, hi, wi, ho, wo = ctx.meta
+        gy = gy.contiguous()
+        lib = hip.load()
+        gx = torch.empty((1, c, hi, wi), dtype=_f32, device=gy.device)
+        wsb = lib.msl_upsample_bwd_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, gy.device)
+        hip.check(lib.msl_upsample_bwd(gy.data_ptr(), gx.data_ptr(), c, hi, wi, ho, wo, ws.data_ptr(),
+                                       wsb, hip.stream_ptr()), "msl_upsample_bwd")
+        return gx, None, None
+
+
+def upsample_bilinear(x, size):
+    """F.interpolate(x, size, mode='bilinear', align_corners=True) (deeplab_multi.py:124,128).
+
+    The result carries `_msl_low` = x so the fused losses below can work from
+    the low-resolution logits instead of re-reading the upsampled tensor.
+    """
+    y = _Upsample.apply(x, int(size[0]), int(size[1]))
+    y._msl_low = x
+    return y
+
+
+# --------------------------------------------------------------------------- fused losses
+def _stats(device):
+    return torch.empty(hip.load().msl_loss_stats_elems(), dtype=_f32, device=device)
+
+
+def _geom(low, out_hw):
+    c, hi, wi = low.shape[1:]
+    return c, hi, wi, int(out_hw[0]), int(out_hw[1])
+
+
+class _CEUp(Function):
+    @staticmethod
+    def forward(ctx, low, labels, ho, wo):
+        low = _check_act(low, "ce_up")
+        labels = labels.contiguous()
+        c, hi, wi, ho, wo = _geom(low, (ho, wo))
+        if labels.dtype != torch.int64 or labels.numel() != ho * wo:
+            raise hip.MSLError(f"ce_up: labels must be int64 with {ho*wo} elements")
+        lib = hip.load()
+        out = torch.empty((), dtype=_f32, device=low.device)
+        st = _stats(low.device)
+        wsb = lib.msl_loss_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, low.device)
+        hip.check(lib.msl_ce_up_fwd(low.data_ptr(), labels.data_ptr(), c, hi, wi, ho, wo, out.data_ptr(),
+                                    st.data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()), "msl_ce_up_fwd")
+        ctx.save_for_backward(low, labels, st)
+        ctx.geo = (c, hi, wi, ho, wo)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        low, labels, st = ctx.saved_tensors
+        c, hi, wi, ho, wo = ctx.geo
+        lib = hip.load()
+        g = g.to(_f32).contiguous()
+        d = torch.empty_like(low)
+        wsb = lib.msl_loss_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, low.device)
+        hip.check(lib.msl_ce_up_bwd(low.data_ptr(), labels.data_ptr(), c, hi, wi, ho, wo, st.data_ptr(),
+                                    g.data_ptr(), d.data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()),
+                  "msl_ce_up_bwd")
+        return d, None, None, None
+
+
+class _MaxSquareUp(Function):
+    @staticmethod
+    def forward(ctx, low, ho, wo):
+        low = _check_act(low, "maxsquare_up")
+        c, hi, wi, ho, wo = _geom(low, (ho, wo))
+        lib = hip.load()
+        out = torch.empty((), dtype=_f32, device=low.device)
+        st = _stats(low.device)
+        wsb = lib.msl_loss_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, low.device)
+        hip.check(lib.msl_maxsquare_up_fwd(low.data_ptr(), c, hi, wi, ho, wo, out.data_ptr(), st.data_ptr(),
+                                           ws.data_ptr(), wsb, hip.stream_ptr()), "msl_maxsquare_up_fwd")
+        ctx.save_for_backward(low, st)
+        ctx.geo = (c, hi, wi, ho, wo)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        low, st = ctx.saved_tensors
+        c, hi, wi, ho, wo = ctx.geo
+        lib = hip.load()
+        g = g.to(_f32).contiguous()
+        d = torch.empty_like(low)
+        wsb = lib.msl_loss_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, low.device)
+        hip.check(lib.msl_maxsquare_up_bwd(low.data_ptr(), c, hi, wi, ho, wo, st.data_ptr(), g.data_ptr(),
+                                           d.data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()),
+                  "msl_maxsquare_up_bwd")
+        return d, None, None
+
+
+class _IWMaxSquareUp(Function):
+    @staticmethod
+    def forward(ctx, low, ho, wo, ratio):
+        low = _check_act(low, "iw_maxsquare_up")
+        c, hi, wi, ho, wo = _geom(low, (ho, wo))
+        lib = hip.load()
+        out = torch.empty((), dtype=_f32, device=low.device)
+        st = _stats(low.device)
+        hist = torch.empty(c, dtype=torch.int32, device=low.device)
+        weights = torch.empty(c, dtype=_f32, device=low.device)
+        wsb = lib.msl_loss_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, low.device)
+        hip.check(lib.msl_iw_maxsquare_up_fwd(low.data_ptr(), c, hi, wi, ho, wo, float(ratio), out.data_ptr(),
+                                              st.data_ptr(), hist.data_ptr(), weights.data_ptr(), ws.data_ptr(),
+                                              wsb, hip.stream_ptr()), "msl_iw_maxsquare_up_fwd")
+        ctx.save_for_backward(low, st)
+        ctx.geo = (c, hi, wi, ho, wo)
+        ctx.mark_non_differentiable(hist, weights)
+        return out, hist, weights
+
+    @staticmethod
+    def backward(ctx, g, _gh, _gw):
+        low, st = ctx.saved_tensors
+        c, hi, wi, ho, wo = ctx.geo
+        lib = hip.load()
+        g = g.to(_f32).contiguous()
+        d = torch.empty_like(low)
+        wsb = lib.msl_loss_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, low.device)
+        hip.check(lib.msl_iw_maxsquare_up_bwd(low.data_ptr(), c, hi, wi, ho, wo, st.data_ptr(), g.data_ptr(),
+                                              d.data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()),
+                  "msl_iw_maxsquare_up_bwd")
+        return d, None, None, None
+
+
+class _MultiCEUp(Function):
+    @staticmethod
+    def forward(ctx, low1, low2, ho, wo, thr):
+        low1 = _check_act(low1, "multi_ce_up")
+        low2 = _check_act(low2.detach(), "multi_ce_up")
+        c, hi, wi, ho, wo = _geom(low1, (ho, wo))
+        lib = hip.load()
+        out = torch.empty((), dtype=_f32, device=low1.device)
+        st = _stats(low1.device)
+        wsb = lib.msl_loss_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, low1.device)
+        hip.check(lib.msl_multi_ce_up_fwd(low1.data_ptr(), low2.data_ptr(), c, hi, wi, ho, wo, float(thr),
+                                          out.data_ptr(), st.data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()),
+                  "msl_multi_ce_up_fwd")
+        ctx.save_for_backward(low1, low2, st)
+        ctx.geo = (c, hi, wi, ho, wo, float(thr))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        low1, low2, st = ctx.saved_tensors
+        c, hi, wi, ho, wo, thr = ctx.geo
+        lib = hip.load()
+        g = g.to(_f32).contiguous()
+        d = torch.empty_like(low1)
+        wsb = lib.msl_loss_workspace(c, hi, wi, ho, wo)
+        ws = hip.workspace(wsb, low1.device)
+        hip.check(lib.msl_multi_ce_up_bwd(low1.data_ptr(), low2.data_ptr(), c, hi, wi, ho, wo, thr, st.data_ptr(),
+                                          g.data_ptr(), d.data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()),
+                  "msl_multi_ce_up_bwd")
+        return d, None, None, None, None
+
+
+def low_of(pred):
+    """The low-resolution logits behind an upsampled prediction, or None."""
+    return getattr(pred, "_msl_low", None)
+
+
+def ce_up(low, labels, out_hw):
+    return _CEUp.apply(low, labels, int(out_hw[0]), int(out_hw[1]))
+
+
+def maxsquare_up(low, out_hw):
+    return _MaxSquareUp.apply(low, int(out_hw[0]), int(out_hw[1]))
+
+
+def iw_maxsquare_up(low, out_hw, ratio):
+    """Returns (loss, hist int32[C], weights fp32[C])."""
+    return _IWMaxSquareUp.apply(low, int(out_hw[0]), int(out_hw[1]), float(ratio))
+
+
+def multi_ce_up(low1, low2, out_hw, thr):
+    return _MultiCEUp.apply(low1, low2, int(out_hw[0]), int(out_hw[1]), float(thr))
+
+
+# --------------------------------------------------------------------------- prob-input losses
+class _MaxSquareProb(Function):
+    @staticmethod
+    def forward(ctx, prob):
+        prob = _check_act(prob, "maxsquare_prob")
+        c, hw = prob.size(1), prob.size(2) * prob.size(3)
+        lib = hip.load()
+        out = torch.empty((), dtype=_f32, device=prob.device)
+        wsb = lib.msl_loss_workspace(c, 1, 1, 1, hw)
+        ws = hip.workspace(wsb, prob.device)
+        hip.check(lib.msl_maxsquare_prob_fwd(prob.data_ptr(), c, hw, out.data_ptr(), ws.data_ptr(), wsb,
+                                             hip.stream_ptr()), "msl_maxsquare_prob_fwd")
+        ctx.save_for_backward(prob)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (prob,) = ctx.saved_tensors
+        c, hw = prob.size(1), prob.size(2) * prob.size(3)
+        g = g.to(_f32).contiguous()
+        d = torch.empty_like(prob)
+        hip.check(hip.load().msl_maxsquare_prob_bwd(prob.data_ptr(), c, hw, g.data_ptr(), d.data_ptr(),
+                                                    hip.stream_ptr()), "msl_maxsquare_prob_bwd")
+        return d
+
+
+class _IWMaxSquareProb(Function):
+    @staticmethod
+    def forward(ctx, prob, label, ratio):
+        prob = _check_act(prob, "iw_maxsquare_prob")
+        c, hw = prob.size(1), prob.size(2) * prob.size(3)
+        if label is not None:
+            label = label.contiguous()
+            if label.dtype != torch.int64 or label.numel() != hw:
+                raise hip.MSLError("iw_maxsquare_prob: label must be int64 (N,H,W) with N=1")
+        lib = hip.load()
+        out = torch.empty((), dtype=_f32, device=prob.device)
+        hist = torch.empty(c, dtype=torch.int32, device=prob.device)
+        weights = torch.empty(c, dtype=_f32, device=prob.device)
+        wsb = lib.msl_loss_workspace(c, 1, 1, 1, hw)
+        ws = hip.workspace(wsb, prob.device)
+        hip.check(lib.msl_iw_maxsquare_prob_fwd(prob.data_ptr(), hip.ptr(label), c, hw, float(ratio),
+                                                out.data_ptr(), hist.data_ptr(), weights.data_ptr(),
+                                                ws.data_ptr(), wsb, hip.stream_ptr()), "msl_iw_maxsquare_prob_fwd")
+        ctx.save_for_backward(prob, weights)
+        ctx.mark_non_differentiable(hist, weights)
+        return out, hist, weights
+
+    @staticmethod
+    def backward(ctx, g, _gh, _gw):
+        prob, weights = ctx.saved_tensors
+        c, hw = prob.size(1), prob.size(2) * prob.size(3)
+        g = g.to(_f32).contiguous()
+        d = torch.empty_like(prob)
+        hip.check(hip.load().msl_iw_maxsquare_prob_bwd(prob.data_ptr(), c, hw, weights.data_ptr(), g.data_ptr(),
+                                                       d.data_ptr(), hip.stream_ptr()), "msl_iw_maxsquare_prob_bwd")
+        return d, None, None
+
+
+def maxsquare_prob(prob):
+    return _MaxSquareProb.apply(prob)
+
+
+def iw_maxsquare_prob(prob, label, ratio):
+    return _IWMaxSquareProb.apply(prob, label, float(ratio))

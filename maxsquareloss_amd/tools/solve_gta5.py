@@ -1,0 +1,157 @@
+"""GTA5/SYNTHIA -> Cityscapes UDA trainer (tools/solve_gta5.py of the reference), MI355X path.
+
+One iteration (solve_gta5.py:335-387), with the same method names:
+    poly_lr_scheduler
+    pred = model(x_src);  train_source(pred, y)   # CE(x2,y) [+ lambda_seg*CE(x1,y)]; backward
+    pred = model(x_tgt);  train_target(pred)      # lambda_t*MaxSquare|IW-MaxSquare(x2)
+                                                  # [+ lambda_seg*lambda_t*CE(x1, label_2)]; backward
+    optimizer.step(); optimizer.zero_grad()
+Gradients of the two backward passes accumulate; with WORLD_SIZE > 1 the
+bucketed RCCL all-reduce is armed for the target backward and overlaps it.
+
+The losses run fused from the low-resolution logits (utils/loss.py), so the
+two softmax tensors of the reference (:182-183) are never materialised.
+Style-transfer augmentation (exp_tag source_aug/target_aug) and the
+validation/eval path are out of scope.
+"""
+import argparse
+
+import torch
+
+from ..utils.loss import IW_MaxSquareloss, MaxSquareloss, multi_level_guidance_ce
+from ..utils.synthetic import SyntheticDomain
+from .train_source import Trainer, add_train_args, init_args
+
+
+class UDATrainer(Trainer):
+    def __init__(self, args, cuda=None, train_id="None", logger=None):
+        super().__init__(args, cuda, train_id, logger)
+        h, w = self.args.crop_size[1], self.args.crop_size[0]
+        th, tw = self.args.target_crop_size[1], self.args.target_crop_size[0]
+        self.source_dataloader = SyntheticDomain(h, w, self.args.num_classes, self.args.synthetic_images,
+                                                 rank=self.rank)
+        self.target_dataloader = SyntheticDomain(th, tw, self.args.num_classes, self.args.synthetic_images,
+                                                 rank=self.rank, offset=500)
+        self.ignore_index = -1
+        mode = self.args.target_mode
+        if mode == "maxsquare":
+            self.target_loss = MaxSquareloss(ignore_index=-1, num_class=self.args.num_classes)
+        elif mode == "IW_maxsquare":
+            self.target_loss = IW_MaxSquareloss(ignore_index=-1, num_class=self.args.num_classes,
+                                                ratio=self.args.IW_ratio)
+        else:
+            raise NotImplementedError(f"target_mode {mode!r} is outside the MI355X hot path "
+                                      "(maxsquare, IW_maxsquare)")
+        self.current_round = self.args.init_round
+        self.round_num = self.args.round_num
+        self.threshold = self.args.threshold
+        self.iter_num = 1
+        self._reset_meters()
+
+    def _reset_meters(self):
+        z = lambda: torch.zeros((), device=self.device)  # noqa: E731
+        self.loss_seg_value, self.loss_seg_value_2 = z(), z()
+        self.loss_target_value, self.loss_target_value_2 = z(), z()
+
+    # ---------------------------------------------------------------- the two halves
+    def train_source(self, pred, y):
+        """solve_gta5.py:220-235."""
+        if isinstance(pred, tuple):
+            pred_2 = pred[1]
+            pred = pred[0]
+        y = torch.squeeze(y, 1)
+        self.loss_val = self.loss(pred, y)
+        loss_ = self.loss_val
+        if self.args.multi:
+            loss_2 = self.args.lambda_seg * self.loss(pred_2, y)
+            loss_ = loss_ + loss_2
+            self.loss_seg_value_2 += loss_2.detach() / self.iter_num
+        loss_.backward()
+        self.loss_seg_value += self.loss_val.detach() / self.iter_num
+
+    def train_target(self, pred):
+        """solve_gta5.py:178-218 (maxsquare / IW_maxsquare target modes)."""
+        pred_2 = None
+        if isinstance(pred, tuple):
+            pred_2 = pred[1]
+            pred = pred[0]
+        self.loss_target = self.args.lambda_target * self.target_loss(pred)
+        loss_target_ = self.loss_target
+        if self.args.multi:
+            self.loss_target_2 = (self.args.lambda_seg * self.args.lambda_target *
+                                  multi_level_guidance_ce(pred, pred_2, self.threshold))
+            loss_target_ = loss_target_ + self.loss_target_2
+            self.loss_target_value_2 += self.loss_target_2.detach() / self.iter_num
+        if self.reducer:
+            self.reducer.prepare_for_backward()
+        loss_target_.backward()
+        self.loss_target_value += self.loss_target.detach() / self.iter_num
+
+    def uda_step(self, x_s, y_s, x_t):
+        """One iteration of the hot loop (solve_gta5.py:336-383), inputs already on the device."""
+        self.poly_lr_scheduler(optimizer=self.optimizer, init_lr=self.args.lr)
+        pred = self.model(x_s)
+        self.train_source(pred, y_s)
+        pred = self.model(x_t)
+        self.train_target(pred)
+        if self.reducer:
+            self.reducer.finish()
+        self.optimizer.step()
+        self.optimizer.zero_grad()
+        self.current_iter += 1
+
+    # ---------------------------------------------------------------- loop
+    def main(self):
+        self.args.iter_max = self.current_iter + self.dataloader.num_iterations * \
+            self.args.epoch_each_round * self.round_num
+        self.optimizer.zero_grad()
+        for _ in range(self.current_round, self.round_num):
+            self.epoch_num = self.current_epoch + (self.current_round + 1) * self.args.epoch_each_round
+            self.train()
+            self.current_round += 1
+
+    def train(self):
+        for epoch in range(self.current_epoch, self.epoch_num):
+            self.train_one_epoch(epoch)
+            self.current_epoch += 1
+        self.save_checkpoint(self.train_id + "final.pth")
+
+    def train_one_epoch(self, epoch=0):
+        self.model.eval() if self.args.freeze_bn else self.model.train()
+        self.iter_num = self.dataloader.num_iterations
+        self._reset_meters()
+        for i in range(self.iter_num):
+            x_s, y_s, _ = self.source_dataloader[i % len(self.source_dataloader)]
+            x_t, _, _ = self.target_dataloader[i % len(self.target_dataloader)]
+            self.uda_step(x_s.to(self.device), y_s.to(self.device, dtype=torch.long), x_t.to(self.device))
+        self.logger.info("epoch %d: source loss %.6f target loss %.6f", self.current_epoch,
+                         float(self.loss_seg_value), float(self.loss_target_value))
+
+
+def add_UDA_train_args(arg_parser):
+    """solve_gta5.py:407-432."""
+    a = arg_parser.add_argument
+    a("--source_dataset", default="gta5", type=str, choices=["gta5", "synthia"])
+    a("--source_split", default="train", type=str)
+    a("--init_round", type=int, default=0)
+    a("--round_num", type=int, default=1)
+    a("--epoch_each_round", type=int, default=2)
+    a("--target_mode", type=str, default="maxsquare",
+      choices=["maxsquare", "IW_maxsquare", "entropy", "IW_entropy", "hard"])
+    a("--lambda_target", type=float, default=1)
+    a("--gamma", type=float, default=0)
+    a("--IW_ratio", type=float, default=0.2)
+    a("--threshold", type=float, default=0.95)
+    a("--target_solo_epoch", type=int, default=0)
+    return arg_parser
+
+
+def build_parser():
+    return add_UDA_train_args(add_train_args(argparse.ArgumentParser()))
+
+
+if __name__ == "__main__":
+    args, train_id, logger = init_args(build_parser().parse_args())
+    args.target_dataset = args.dataset
+    train_id = str(args.source_dataset) + "2" + str(args.target_dataset) + "_" + args.target_mode
+    UDATrainer(args=args, cuda=True, train_id=train_id, logger=logger).main()

@@ -1,0 +1,252 @@
+"""Source-only trainer (tools/train_source.py of the reference), MI355X path.
+
+Same flags (add_train_args, :726-829), same `init_args` parsing (:832-883),
+same `Trainer` surface (`train()`, `train_one_epoch()`, `poly_lr_scheduler`,
+`save_checkpoint` / `load_checkpoint` dict format).  Differences, all outside
+the training arithmetic:
+  - data is synthetic (the GTA5/Cityscapes/SYNTHIA files are not available):
+    utils/synthetic.py reproduces the reference preprocessing on generated
+    uint8 images; the dataset flags are accepted and only set shapes/classes;
+  - one process per GPU: under torchrun (WORLD_SIZE > 1) the model is
+    replicated and gradients are all-reduced over RCCL (utils/dist.py);
+  - loss scalars stay on the device (no per-iteration .cpu().item() sync);
+    the NaN check of :277-278 runs on the accumulated value at epoch end;
+  - the per-iteration D2H argmax + Eval confusion matrix (:280-283) and
+    tensorboard logging are out of scope.
+"""
+import argparse
+import logging
+import os
+import random
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..utils.dist import GradReducer
+from ..utils.loss import CrossEntropyLoss
+from ..utils.optim import SGD
+from ..utils.synthetic import SyntheticDomain, init_weights
+from ..utils.train_helper import get_model
+
+ITER_MAX = 5000
+
+
+def str2bool(v):
+    if isinstance(v, bool):
+        return v
+    if v.lower() in ("yes", "true", "t", "y", "1"):
+        return True
+    if v.lower() in ("no", "false", "f", "n", "0"):
+        return False
+    raise argparse.ArgumentTypeError("Unsupported value encountered.")
+
+
+def dist_env():
+    """(rank, world, local_rank) from torchrun's environment, (0, 1, 0) otherwise."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+class Trainer:
+    def __init__(self, args, cuda=None, train_id="None", logger=None):
+        self.args = args
+        self.rank, self.world, self.local_rank = dist_env()
+        self.cuda = bool(cuda) and torch.cuda.is_available()
+        if not self.cuda:
+            raise RuntimeError("the MI355X trainer needs a GPU (no CPU fallback)")
+        torch.cuda.set_device(self.local_rank)
+        self.device = torch.device("cuda", self.local_rank)
+        if self.world > 1 and not dist.is_initialized():
+            dist.init_process_group("nccl", device_id=self.device)
+        self.train_id = train_id
+        self.logger = logger or logging.getLogger(__name__)
+        self.current_MIoU = self.best_MIou = self.best_FWIou = self.best_source_MIou = 0
+        self.current_epoch = 0
+        self.current_iter = 0
+
+        self.loss = CrossEntropyLoss(weight=None, ignore_index=-1)
+
+        self.model, self.params = get_model(self.args)
+        init_weights(self.model, seed=self.args.seed)
+        self.model.to(self.device)
+
+        if self.args.optim != "SGD":
+            raise NotImplementedError("only --optim SGD (the reference default) is on the MI355X path")
+        self.optimizer = SGD(lr=self.args.lr, params=self.params, momentum=self.args.momentum,
+                             weight_decay=self.args.weight_decay)
+        self.reducer = GradReducer(self.optimizer) if self.world > 1 else None
+
+        h, w = self.args.crop_size[1], self.args.crop_size[0]
+        self.dataloader = SyntheticDomain(h, w, self.args.num_classes, self.args.synthetic_images,
+                                          rank=self.rank)
+        self.dataloader.num_iterations = min(len(self.dataloader), ITER_MAX)
+        iters = self.args.iter_stop if self.args.iter_stop is not None else self.args.iter_max
+        self.epoch_num = -(-iters // self.dataloader.num_iterations)
+
+    # ------------------------------------------------------------------ loop
+    def main(self):
+        if self.args.continue_training and self.args.checkpoint_dir:
+            self.load_checkpoint(self.args.checkpoint_dir)
+        self.train()
+
+    def train(self):
+        for epoch in range(self.current_epoch, self.epoch_num):
+            self.train_one_epoch(epoch)
+            self.current_epoch += 1
+        self.save_checkpoint(self.train_id + "final.pth")
+
+    def train_one_epoch(self, epoch=None):
+        self.model.train()
+        iter_num = self.dataloader.num_iterations
+        loss_sum = torch.zeros((), device=self.device)
+        for i in range(iter_num):
+            x, y, _ = self.dataloader[i]
+            self.poly_lr_scheduler(self.optimizer, init_lr=self.args.lr, iter=self.current_iter,
+                                   max_iter=self.args.iter_max, power=self.args.poly_power)
+            x = x.to(self.device, non_blocking=True)
+            y = y.to(self.device, dtype=torch.long, non_blocking=True)
+            loss_sum += self.source_step(x, y).detach()
+            self.current_iter += 1
+        mean = float(loss_sum) / max(iter_num, 1)
+        if np.isnan(mean):
+            raise ValueError("Loss is nan during training...")
+        self.logger.info("The average loss of train epoch-%d-:%f", self.current_epoch, mean)
+
+    def source_step(self, x, y):
+        """train_source.py:248-264: CE(x2,y) + lambda_seg*CE(x1,y); zero_grad; backward; step."""
+        pred = self.model(x)
+        pred, pred_2 = pred if isinstance(pred, tuple) else (pred, None)
+        cur_loss = self.loss(pred, y)
+        if self.args.multi:
+            cur_loss = cur_loss + self.args.lambda_seg * self.loss(pred_2, y)
+        self.optimizer.zero_grad()
+        if self.reducer:
+            self.reducer.prepare_for_backward()
+        cur_loss.backward()
+        if self.reducer:
+            self.reducer.finish()
+        self.optimizer.step()
+        return cur_loss
+
+    # ------------------------------------------------------------------ checkpoints
+    def save_checkpoint(self, filename=None):
+        if self.rank != 0 or not self.args.save_dir:
+            return
+        os.makedirs(self.args.save_dir, exist_ok=True)
+        filename = os.path.join(self.args.save_dir, filename)
+        state = {"epoch": self.current_epoch + 1, "iteration": self.current_iter,
+                 "state_dict": self.model.state_dict(), "optimizer": self.optimizer.state_dict(),
+                 "best_MIou": self.best_MIou}
+        torch.save(state, filename)
+
+    def load_checkpoint(self, filename):
+        try:
+            checkpoint = torch.load(filename, map_location=self.device, weights_only=True)
+        except OSError:
+            self.logger.info("No checkpoint exists from '%s'. Skipping...", filename)
+            return
+        sd = checkpoint["state_dict"]
+        sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}  # DataParallel prefix
+        self.model.load_state_dict(sd)
+        if "optimizer" in checkpoint:
+            self.optimizer.load_state_dict(checkpoint["optimizer"])
+            self.current_epoch = checkpoint["epoch"]
+            self.current_iter = checkpoint["iteration"]
+            self.best_MIou = checkpoint["best_MIou"]
+
+    # ------------------------------------------------------------------ LR
+    def poly_lr_scheduler(self, optimizer, init_lr=None, iter=None, max_iter=None, power=None):
+        """train_source.py:706-717."""
+        init_lr = self.args.lr if init_lr is None else init_lr
+        iter = self.current_iter if iter is None else iter
+        max_iter = self.args.iter_max if max_iter is None else max_iter
+        power = self.args.poly_power if power is None else power
+        new_lr = init_lr * (1 - float(iter) / max_iter) ** power
+        optimizer.param_groups[0]["lr"] = new_lr
+        if len(optimizer.param_groups) == 2:
+            optimizer.param_groups[1]["lr"] = 10 * new_lr
+        if len(optimizer.param_groups) == 3:
+            optimizer.param_groups[2]["lr"] = new_lr
+
+
+def add_train_args(arg_parser):
+    """The reference's flags (train_source.py:726-829) plus --synthetic_images."""
+    a = arg_parser.add_argument
+    a("--data_root_path", type=str, default=None)
+    a("--list_path", type=str, default=None)
+    a("--checkpoint_dir", default=None)
+    a("--save_dir", default="./log/train")
+    a("--backbone", default="deeplabv2_multi")
+    a("--bn_momentum", type=float, default=0.1)
+    a("--imagenet_pretrained", type=str2bool, default=True)
+    a("--pretrained_ckpt_file", type=str, default=None)
+    a("--continue_training", type=str2bool, default=False)
+    a("--show_num_images", type=int, default=2)
+    a("--seed", default=12345, type=int)
+    a("--gpu", type=str, default="0")
+    a("--batch_size", default=1, type=int)
+    a("--exp_tag", type=str, default="test")
+    a("--dataset", default="Cityscapes", type=str)
+    a("--base_size", default="1856,928", type=str)
+    a("--crop_size", default="928,464", type=str)
+    a("--target_base_size", default="1856,928", type=str)
+    a("--target_crop_size", default="928,464", type=str)
+    a("--seg_size", default=(1280, 640))
+    a("--num_classes", default=19, type=int)
+    a("--data_loader_workers", default=0, type=int)
+    a("--pin_memory", default=2, type=int)
+    a("--split", type=str, default="train")
+    a("--random_mirror", default=True, type=str2bool)
+    a("--random_crop", default=False, type=str2bool)
+    a("--resize", default=True, type=str2bool)
+    a("--gaussian_blur", default=False, type=str2bool)
+    a("--numpy_transform", default=True, type=str2bool)
+    a("--freeze_bn", type=str2bool, default=False)
+    a("--optim", default="SGD", type=str)
+    a("--momentum", type=float, default=0.9)
+    a("--weight_decay", type=float, default=5e-4)
+    a("--lr", type=float, default=2.5e-4)
+    a("--iter_max", type=int, default=200000)
+    a("--iter_stop", type=int, default=80000)
+    a("--poly_power", type=float, default=0.9)
+    a("--rectification", type=bool, default=False)
+    a("--crop_trans", type=bool, default=False)
+    a("--client", type=bool, default=False)
+    a("--DA", type=bool, default=False)
+    a("--multi", default=True, type=str2bool)
+    a("--lambda_seg", type=float, default=0.1)
+    a("--synthetic_images", type=int, default=4, help="synthetic items per domain (no datasets offline)")
+    return arg_parser
+
+
+def init_args(args):
+    """train_source.py:832-883 without the log-file handler."""
+    train_id = args.exp_tag
+
+    def pair(s):
+        parts = str(s).split(",")
+        return int(parts[0]) if len(parts) == 1 else (int(parts[0]), int(parts[1]))
+
+    args.crop_size, args.base_size = pair(args.crop_size), pair(args.base_size)
+    args.target_crop_size, args.target_base_size = pair(args.target_crop_size), pair(args.target_base_size)
+    if isinstance(args.crop_size, int):
+        args.crop_size = (args.crop_size, args.crop_size)
+    if isinstance(args.target_crop_size, int):
+        args.target_crop_size = (args.target_crop_size, args.target_crop_size)
+    args.class_16 = args.num_classes == 16
+    args.class_13 = args.num_classes == 13
+    logger = logging.getLogger()
+    logger.setLevel(logging.INFO)
+    random.seed(args.seed)
+    np.random.seed(args.seed)
+    torch.random.manual_seed(args.seed)
+    return args, train_id, logger
+
+
+if __name__ == "__main__":
+    parser = add_train_args(argparse.ArgumentParser())
+    args, train_id, logger = init_args(parser.parse_args())
+    Trainer(args=args, cuda=True, train_id=train_id, logger=logger).main()

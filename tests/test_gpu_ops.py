@@ -1,0 +1,214 @@
+"""Kernel-level parity of the HIP path against fp64 / torch-CPU references (GPU only).
+
+Tolerances: conv outputs and gradients within 1e-5 of max|ref|
+against an fp64 CPU conv (the kernels are exact fp32 FMA chains, only the
+summation order differs); upsample forward bit-exact vs torch-CPU; losses
+1e-5 relative; class histograms bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from maxsquareloss_amd import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+def _conv_ref(x, w, d, bias=None):
+    return F.conv2d(x.double(), w.double(), None if bias is None else bias.double(), padding=d, dilation=d)
+
+
+@pytest.mark.parametrize("cin,cout,h,w,d", [
+    (256, 256, 17, 33, 2), (512, 512, 17, 33, 4), (64, 64, 33, 65, 1), (32, 48, 9, 13, 2),
+    (256, 256, 65, 129, 2)])
+def test_dconv_fwd_bwd(cin, cout, h, w, d):
+    g = torch.Generator().manual_seed(cin * 7 + h)
+    x = torch.randn(1, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.05
+    gy = torch.randn(1, cout, h, w, generator=g)
+    xr, wr = x.double().requires_grad_(), wt.double().requires_grad_()
+    yr = F.conv2d(xr, wr, padding=d, dilation=d)
+    yr.backward(gy.double())
+    xg = x.to(DEV).requires_grad_()
+    wg = wt.to(DEV).requires_grad_()
+    cache = ops.PackCache()
+    y = ops.dconv3x3(xg, wg, d, cache)
+    y.backward(gy.to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 1e-5
+    assert _rel(xg.grad, xr.grad) < 1e-5
+    assert _rel(wg.grad, wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("cin,c,h,w", [(1024, 19, 17, 33), (2048, 19, 33, 65), (96, 16, 9, 17), (64, 13, 65, 129)])
+def test_aspp2_fwd_bwd(cin, c, h, w):
+    g = torch.Generator().manual_seed(cin + c)
+    x = torch.randn(1, cin, h, w, generator=g)
+    w0 = torch.randn(c, cin, 3, 3, generator=g) * 0.01
+    w1 = torch.randn(c, cin, 3, 3, generator=g) * 0.01
+    b0 = torch.randn(c, generator=g) * 0.01
+    b1 = torch.randn(c, generator=g) * 0.01
+    gy = torch.randn(1, c, h, w, generator=g)
+    ref = [t.double().requires_grad_() for t in (x, w0, b0, w1, b1)]
+    yr = F.conv2d(ref[0], ref[1], ref[2], padding=6, dilation=6) + F.conv2d(ref[0], ref[3], ref[4], padding=12, dilation=12)
+    yr.backward(gy.double())
+    dev = [t.to(DEV).requires_grad_() for t in (x, w0, b0, w1, b1)]
+    y = ops.aspp2(dev[0], dev[1], dev[2], dev[3], dev[4], 6, 12, ops.PackCache())
+    y.backward(gy.to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 1e-5
+    for a, b in zip(dev, ref):
+        assert _rel(a.grad, b.grad) < 1e-5
+
+
+@pytest.mark.parametrize("c,hi,wi,ho,wo", [(19, 65, 129, 512, 1024), (19, 33, 65, 256, 512), (16, 81, 161, 640, 1280), (3, 5, 7, 11, 13)])
+def test_upsample(c, hi, wi, ho, wo):
+    g = torch.Generator().manual_seed(hi)
+    x = torch.randn(1, c, hi, wi, generator=g) * 3
+    yr = F.interpolate(x, size=(ho, wo), mode="bilinear", align_corners=True)
+    xg = x.to(DEV).requires_grad_()
+    y = ops.upsample_bilinear(xg, (ho, wo))
+    if wo % 16 == 0:  # torch-CPU's vectorised path (the model's shapes): bit-exact
+        assert torch.equal(y.cpu(), yr), "upsample forward must be bit-exact vs torch CPU"
+    else:  # torch's scalar tail rounds differently; within an ulp
+        assert _rel(y, yr) < 1e-6
+    gy = torch.randn(1, c, ho, wo, generator=g)
+    xr = x.double().requires_grad_()
+    F.interpolate(xr, size=(ho, wo), mode="bilinear", align_corners=True).backward(gy.double())
+    y.backward(gy.to(DEV))
+    assert _rel(xg.grad, xr.grad) < 1e-5
+
+
+def _softmax_ref(low, hw):
+    up = F.interpolate(low, size=hw, mode="bilinear", align_corners=True)
+    return up, F.softmax(up, dim=1)
+
+
+@pytest.mark.parametrize("c,hi,wi,ho,wo", [(19, 33, 65, 256, 512), (16, 17, 33, 128, 256), (13, 9, 17, 64, 128)])
+def test_fused_losses(c, hi, wi, ho, wo):
+    g = torch.Generator().manual_seed(c)
+    low = torch.randn(1, c, hi, wi, generator=g) * 4
+    low2 = torch.randn(1, c, hi, wi, generator=g) * 4
+    y = torch.randint(-1, c, (1, ho, wo), generator=g)
+    lowg = low.to(DEV).requires_grad_()
+    # --- CE
+    lr = low.clone().requires_grad_()
+    up, _ = _softmax_ref(lr, (ho, wo))
+    ref = F.cross_entropy(up, y, ignore_index=-1)
+    ref.backward()
+    out = ops.ce_up(lowg, y.to(DEV).reshape(-1), (ho, wo))
+    out.backward()
+    assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    assert _rel(lowg.grad, lr.grad) < 1e-5
+    # --- MaxSquare
+    lowg.grad = None
+    lr = low.clone().requires_grad_()
+    _, P = _softmax_ref(lr, (ho, wo))
+    ref = -torch.mean(P ** 2) / 2
+    ref.backward()
+    out = ops.maxsquare_up(lowg, (ho, wo))
+    out.backward()
+    assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    assert _rel(lowg.grad, lr.grad) < 1e-5
+    # --- IW MaxSquare
+    lowg.grad = None
+    lr = low.clone().requires_grad_()
+    _, P = _softmax_ref(lr, (ho, wo))
+    maxpred, arg = torch.max(P, 1)
+    hist = torch.histc(arg.float(), bins=c + 1, min=-1, max=c - 1)[1:]
+    wts = 1 / torch.max(torch.pow(hist, 0.2) * torch.pow(hist.sum(), 0.8), torch.ones(1))
+    ref = -torch.sum(P ** 2 * wts[arg].detach()) / c
+    ref.backward()
+    out, h, wv = ops.iw_maxsquare_up(lowg, (ho, wo), 0.2)
+    out.backward()
+    assert torch.equal(h.cpu().long(), hist.long()), "IW class histogram must be bit-exact"
+    assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    assert _rel(lowg.grad, lr.grad) < 1e-5
+    # --- multi-level guidance CE (gradient w.r.t. the x1 head only)
+    lowg.grad = None
+    lr = low.clone().requires_grad_()
+    up1, P2 = _softmax_ref(lr, (ho, wo))
+    _, P = _softmax_ref(low2, (ho, wo))
+    m1, _ = P.max(1)
+    m2, _ = P2.detach().max(1)
+    pc = (P + P2.detach()) / 2
+    _, ac = pc.max(1)
+    lab = torch.where((m1 > 0.5) | (m2 > 0.5), ac, torch.full_like(ac, -1))
+    ref = F.cross_entropy(up1, lab, ignore_index=-1)
+    ref.backward()
+    out = ops.multi_ce_up(lowg, low2.to(DEV), (ho, wo), 0.5)
+    out.backward()
+    assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    assert _rel(lowg.grad, lr.grad) < 1e-5
+
+
+def test_ce_all_ignored_is_nan():
+    low = torch.randn(1, 19, 9, 17, device=DEV, requires_grad=True)
+    y = torch.full((64 * 128,), -1, dtype=torch.int64, device=DEV)
+    out = ops.ce_up(low, y, (64, 128))
+    assert torch.isnan(out).item()
+
+
+def test_prob_losses():
+    g = torch.Generator().manual_seed(3)
+    P = torch.softmax(torch.randn(1, 19, 64, 128, generator=g) * 3, 1)
+    Pr = P.clone().requires_grad_()
+    ref = -torch.mean(Pr ** 2) / 2
+    ref.backward()
+    Pg = P.to(DEV).requires_grad_()
+    out = ops.maxsquare_prob(Pg)
+    out.backward()
+    assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    assert _rel(Pg.grad, Pr.grad) < 1e-5
+    lab = torch.randint(-1, 19, (1, 64, 128), generator=g)
+    Pr = P.clone().requires_grad_()
+    _, arg = torch.max(Pr, 1)
+    hist = torch.histc(lab.float(), bins=20, min=-1, max=18)[1:]
+    wts = 1 / torch.max(torch.pow(hist, 0.2) * torch.pow(hist.sum(), 0.8), torch.ones(1))
+    ref = -torch.sum(Pr ** 2 * wts[arg]) / 19
+    ref.backward()
+    Pg = P.to(DEV).requires_grad_()
+    out, h, _ = ops.iw_maxsquare_prob(Pg, lab.to(DEV), 0.2)
+    out.backward()
+    assert torch.equal(h.cpu().long(), hist.long())
+    assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    assert _rel(Pg.grad, Pr.grad) < 1e-5
+
+
+def test_sgd_multiplicity_matches_torch_cpu():
+    from maxsquareloss_amd.utils.optim import SGD
+    g = torch.Generator().manual_seed(5)
+    shapes = [(64, 3, 7, 7), (256,), (19, 64, 3, 3), (10,)]
+    init = [torch.randn(s, generator=g) for s in shapes]
+    grads = [[torch.randn(s, generator=g) for s in shapes] for _ in range(3)]
+    mult = [1, 3, 4, 1]
+    # torch CPU reference: duplicated entries in group 0, last param in group 1 (10x lr)
+    ref = [t.clone().requires_grad_() for t in init]
+    g0 = [p for p, k in zip(ref[:3], mult[:3]) for _ in range(k)]
+    opt = torch.optim.SGD([{"params": g0, "lr": 0.01}, {"params": [ref[3]], "lr": 0.1}], lr=0.01, momentum=0.9,
+                          weight_decay=5e-4, foreach=False)
+    mine = [t.clone().to(DEV).requires_grad_() for t in init]
+    m0 = [p for p, k in zip(mine[:3], mult[:3]) for _ in range(k)]
+    myopt = SGD([{"params": m0, "lr": 0.01}, {"params": [mine[3]], "lr": 0.1}], lr=0.01, momentum=0.9,
+                weight_decay=5e-4)
+    for step in range(3):
+        for p, gr in zip(ref, grads[step]):
+            p.grad = gr.clone()
+        opt.step()
+        myopt.zero_grad()
+        for p, gr in zip(mine, grads[step]):
+            # accumulate through autograd so the used-parameter hooks fire
+            (p * gr.to(DEV)).sum().backward()
+        myopt.step()
+    torch.cuda.synchronize()
+    for a, b in zip(mine, ref):
+        assert _rel(a, b) < 1e-6
