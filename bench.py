@@ -1,0 +1,180 @@
+"""bench.py - training images/s of the MI355X DeepLabv2/ResNet-101 MaxSquare UDA step.
+
+    python bench.py --gpus N --steps K --warmup W          (N > 1: launched by torchrun)
+
+A "step" is one iteration of tools/solve_gta5.py:335-387: one source image
+(fwd, CE, bwd) + one target image (fwd, MaxSquare, bwd) + the gradient
+all-reduce (N > 1) + the SGD step, i.e. 2 images per rank per step.  Workload =
+BASELINE.json configs[1]: GTA5->Cityscapes MaxSquare, 1024x512, bs=1/GPU,
+random-init (counter generator) weights, synthetic inputs already in HBM,
+--multi False, lambda_target 0.1, fp32.  Scaling is weak (bs=1 per GPU).
+
+Printed (rank 0, one JSON line): value = total images/s over all ranks, the
+roofline of the dominant kernel (layer3's dilated 3x3 forward, timed live with
+HIP events on its stream during the timed steps), the CPU baseline (the oracle's
+PyTorch-CPU restatement of the same step, a bounded sample on this host), and
+the relative loss delta of the first iteration vs that CPU reference.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from maxsquareloss_amd import ops  # noqa: E402
+from maxsquareloss_amd.tools.solve_gta5 import UDATrainer, build_parser  # noqa: E402
+from maxsquareloss_amd.tools.train_source import init_args  # noqa: E402
+from maxsquareloss_amd.utils.synthetic import synthetic_image, synthetic_labels  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def feat_hw(n):
+    """Spatial size of layer3/4 for an input side n: stem 7x7/2, maxpool 3/2 ceil_mode, layer2 1x1/2."""
+    n = (n - 1) // 2 + 1
+    m = -(-(n + 2 - 3) // 2) + 1
+    if (m - 1) * 2 >= n + 1:
+        m -= 1
+    return (m - 1) // 2 + 1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--target-mode", default="maxsquare", choices=["maxsquare", "IW_maxsquare"])
+    ap.add_argument("--multi", default="False")
+    ap.add_argument("--lambda-target", type=float, default=0.1)
+    ap.add_argument("--num-classes", type=int, default=19)
+    ap.add_argument("--cpu-baseline-iters", type=int, default=2, help="0 disables the CPU baseline")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="PMC-derived HBM traffic per launch of the dominant kernel (from a rocprofv3 --pmc run)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
+    argv = ["--crop_size", f"{a.width},{a.height}", "--target_crop_size", f"{a.width},{a.height}",
+            "--imagenet_pretrained", "False", "--save_dir", "", "--num_classes", str(a.num_classes),
+            "--target_mode", a.target_mode, "--multi", a.multi, "--lambda_target", str(a.lambda_target),
+            "--iter_max", "200000"]
+    args, _, _ = init_args(build_parser().parse_args(argv))
+    tr = UDATrainer(args, cuda=True)
+    rank, dev = tr.rank, tr.device
+    init_state = {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()} if rank == 0 else None
+
+    # inputs resident in HBM before timing: two (source, label, target) triples per rank
+    H, W, C = a.height, a.width, a.num_classes
+    batches = []
+    for i in range(2):
+        seed = 1000 * rank + i
+        batches.append((synthetic_image(H, W, seed).to(dev), synthetic_labels(H, W, C, seed).to(dev),
+                        synthetic_image(H, W, 500 + seed).to(dev)))
+    torch.cuda.synchronize()
+
+    first_losses = None
+    for i in range(a.warmup):
+        tr.uda_step(*batches[i % 2])
+        if i == 0:
+            first_losses = {"loss_seg": tr.loss_val.detach().clone(), "loss_target": tr.loss_target.detach().clone()}
+    torch.cuda.synchronize()
+
+    h3, w3 = feat_hw(H), feat_hw(W)
+    key = (1, 256, 256, h3, w3, 2)
+    ops.PROBE[key] = []
+
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        tr.uda_step(*batches[i % 2])
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    probes = ops.PROBE.pop(key)
+    kern_ms = sum(s.elapsed_time(e) for s, e in probes) / max(len(probes), 1)
+
+    el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if dist.is_initialized():
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = el.item()
+    images = 2 * a.steps * world
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    flops = 2.0 * 256 * 256 * 9 * h3 * w3
+    achieved = flops / (kern_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(a.pmc):
+        try:
+            traffic = json.load(open(a.pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "kernel": "dconv3x3 fwd layer3 d=2 (k_igemm_fwd + split-K reduce)",
+                "kernel_ms": round(kern_ms, 4), "launches": len(probes),
+                "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
+
+    cpu = None
+    loss_delta = None
+    if world == 1 and a.cpu_baseline_iters > 0:
+        from oracle import msl_oracle as orc
+        nthreads = torch.get_num_threads()
+        model = orc.Model(init_state, C)
+        opt = orc.SGDMult(model.params, model.names, args.lr)
+        cfg = dict(lr=args.lr, iter_max=args.iter_max, lambda_seg=args.lambda_seg, IW_ratio=args.IW_ratio,
+                   threshold=args.threshold, target_mode=args.target_mode, multi=args.multi,
+                   lambda_target=args.lambda_target)
+        xs, ys, xt = (t.cpu() for t in batches[0])
+        times = []
+        for it in range(1 + a.cpu_baseline_iters):
+            t1 = time.perf_counter()
+            out = orc.uda_step(model, opt, xs, ys, xt, cfg, it)
+            times.append(time.perf_counter() - t1)
+            if it == 0 and first_losses is not None:
+                loss_delta = {k: abs(first_losses[k].item() - out[k]) / max(abs(out[k]), 1e-30)
+                              for k in ("loss_seg", "loss_target")}
+        s_per_iter = sorted(times[1:])[len(times[1:]) // 2]
+        cpu = {"value": round(2.0 / s_per_iter, 4), "unit": "images/s", "cores": nthreads, "kind": "port",
+               "sample": f"oracle/msl_oracle.py uda_step at {W}x{H} ({args.target_mode}, multi={args.multi}), "
+                         f"median of {a.cpu_baseline_iters} iterations after 1 warm-up, torch-CPU {nthreads} threads",
+               "s_per_iter": round(s_per_iter, 3)}
+
+    ms_per_step = elapsed / a.steps * 1e3
+    line = {
+        "metric": METRIC, "value": round(images / elapsed, 3), "unit": "images/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (counter-generated uint8 images -> BGR-mean, uniform labels; random-init weights)",
+        "config": {"workload": f"GTA5->Cityscapes {args.target_mode} UDA step (solve_gta5.py), {W}x{H}, bs=1/GPU",
+                   "target_mode": args.target_mode, "multi": args.multi, "lambda_target": args.lambda_target,
+                   "num_classes": C, "global_batch": 2 * world, "parallelism": f"dp{world}"},
+        "roofline": roofline, "cpu_baseline": cpu,
+        "loss_delta_vs_cpu": None if loss_delta is None else {k: float(f"{v:.3g}") for k, v in loss_delta.items()},
+        "iterations_per_s": round(a.steps * 1.0 / elapsed, 4),
+    }
+    print(json.dumps(line), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -394,17 +394,17 @@ __global__ void __launch_bounds__(256) k_bwd_rows(const float* __restrict__ L1,
     const int c = e / g.Wi, ix = e - c * g.Wi;
     const int beg = bnd[ix > 0 ? ix - 1 : 0], end = bnd[ix + 1 <= g.Wi ? ix + 1 : g.Wi];
     const float* Gc = G + c * g.Wo;
-    float s = 0.f;
+    double s = 0.0;  // ~2*Wo/Wi terms; fp64 keeps the gather at fp32-rounding accuracy
     for (int ox = beg; ox < end; ++ox) {
       const int i0 = ix0[ox];
       const int i1 = i0 + (i0 < g.Wi - 1 ? 1 : 0);
       float w = 0.f;
       if (i0 == ix) w += wx0[ox];
       if (i1 == ix) w += wx1[ox];
-      s = __fmaf_rn(w, Gc[ox], s);
+      s += (double)w * (double)Gc[ox];
     }
     // ox == Wo-1 may have i0 == Wi-1 == ix with bnd[Wi] == Wo: covered since end <= Wo.
-    T[c * plane + (long long)oy * g.Wi + ix] = s;
+    T[c * plane + (long long)oy * g.Wi + ix] = (float)s;
   }
 }
 
@@ -429,15 +429,15 @@ __global__ void __launch_bounds__(256) k_bwd_cols(const float* __restrict__ T, G
     };
     const int beg = lb(iy > 0 ? iy - 1 : 0), end = lb(iy + 1);
     const float* Tc = T + (long long)c * g.Ho * g.Wi + ix;
-    float s = 0.f;
+    double s = 0.0;
     for (int oy = beg; oy < end; ++oy) {
       const Lin ly = lin(oy, g.sh, g.Hi);
       float w = 0.f;
       if (ly.i0 == iy) w += ly.w0;
       if (ly.i1 == iy) w += ly.w1;
-      s = __fmaf_rn(w, Tc[(long long)oy * g.Wi], s);
+      s += (double)w * (double)Tc[(long long)oy * g.Wi];
     }
-    dlow[e] = s;
+    dlow[e] = (float)s;
   }
 }
 

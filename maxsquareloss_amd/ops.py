@@ -56,6 +56,11 @@ class PackCache:
 
 
 # --------------------------------------------------------------------------- dilated conv
+# Live kernel timing for bench.py: PROBE[(nbranch, cin, cout, h, w, dil0)] = [] collects
+# (start, end) HIP events recorded on the launching stream around each matching forward.
+PROBE = {}
+
+
 class _DConv3x3(Function):
     """sum_b conv3x3(x, W_b, dilation d_b) (+ sum_b bias_b); nbranch in {1, 2}."""
 
@@ -76,9 +81,17 @@ class _DConv3x3(Function):
         y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
         wsb = lib.msl_dconv_fwd_workspace(nb, cin, cout, h, w)
         ws = hip.workspace(wsb, x.device)
+        probe = PROBE.get((nb, cin, cout, h, w, dil0)) if PROBE else None
+        if probe is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         hip.check(lib.msl_dconv_fwd(x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb,
                                     cin, cout, h, w, dil0, dil1 if nb > 1 else 0, ws.data_ptr(), wsb,
                                     hip.stream_ptr()), "msl_dconv_fwd")
+        if probe is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            probe.append((ev0, ev1))
         ctx.save_for_backward(x, *weights)
         ctx.meta = (nb, cin, cout, h, w, dil0, dil1, b0 is not None, cache)
         return y

@@ -1,0 +1,332 @@
+"""ORACLE - test infrastructure only (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
+
+A CPU restatement of the reference's hot path in plain PyTorch-CPU ops, written
+from the reference's behaviour (cited file:line, paths relative to the
+reference root) - it shares no code with the HIP product path and nothing in
+maxsquareloss_amd/ may import it.
+
+  forward()            graphs/models/deeplab_multi.py:8-130 (Bottleneck, ASPP with the
+                       early return of :63-66 (Q1), bilinear align_corners upsample)
+  ce()                 nn.CrossEntropyLoss(ignore_index=-1), train_source.py:128
+  maxsquare()          utils/loss.py:104-119
+  iw_maxsquare()       utils/loss.py:69-102 (histc on the host, :92-96)
+  multi_guidance_ce()  tools/solve_gta5.py:206-213
+  SGDMult              torch.optim.SGD single-tensor loop over optim_parameters()
+                       (train_source.py:139-144; deeplab_multi.py:132-171; quirk Q2)
+  uda_step()           tools/solve_gta5.py:335-387
+  source_step()        tools/train_source.py:233-264
+
+Pinned against the real reference: tests/golden/*.npz are produced by
+oracle/gen_golden.py, which imports the reference's own deeplab_multi.py and
+loss.py by path in the survey container (and its SGD semantics through
+torch.optim.SGD(foreach=False)); tests/test_oracle_golden.py checks this module
+against them.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+LAYERS = [3, 4, 23, 3]
+PLANES = [64, 128, 256, 512]
+STRIDES = [1, 2, 1, 1]
+DILATIONS = [1, 1, 2, 4]
+ASPP_DIL = [6, 12, 18, 24]
+
+
+# --------------------------------------------------------------------------- parameters
+def param_specs(num_classes):
+    """[(name, shape, kind)] in the reference's registration order (named_parameters())."""
+    specs = [("conv1.weight", (64, 3, 7, 7), "conv"), ("bn1.weight", (64,), "bnw"), ("bn1.bias", (64,), "bnb")]
+    inplanes = 64
+    for li, (planes, n, stride, dil) in enumerate(zip(PLANES, LAYERS, STRIDES, DILATIONS)):
+        for b in range(n):
+            pre = f"layer{li + 1}.{b}."
+            cin = inplanes if b == 0 else planes * 4
+            specs += [(pre + "conv1.weight", (planes, cin, 1, 1), "conv"), (pre + "bn1.weight", (planes,), "bnw"),
+                      (pre + "bn1.bias", (planes,), "bnb"), (pre + "conv2.weight", (planes, planes, 3, 3), "conv"),
+                      (pre + "bn2.weight", (planes,), "bnw"), (pre + "bn2.bias", (planes,), "bnb"),
+                      (pre + "conv3.weight", (planes * 4, planes, 1, 1), "conv"),
+                      (pre + "bn3.weight", (planes * 4,), "bnw"), (pre + "bn3.bias", (planes * 4,), "bnb")]
+            if b == 0:
+                specs += [(pre + "downsample.0.weight", (planes * 4, cin, 1, 1), "conv"),
+                          (pre + "downsample.1.weight", (planes * 4,), "bnw"),
+                          (pre + "downsample.1.bias", (planes * 4,), "bnb")]
+        inplanes = planes * 4
+    for head, cin in (("layer5", 1024), ("layer6", 2048)):
+        for i in range(4):
+            specs += [(f"{head}.conv2d_list.{i}.weight", (num_classes, cin, 3, 3), "conv"),
+                      (f"{head}.conv2d_list.{i}.bias", (num_classes,), "aspp_bias")]
+    return specs
+
+
+def bn_names(num_classes):
+    return [n[:-len(".weight")] for n, _, k in param_specs(num_classes) if k == "bnw"]
+
+
+def multiplicity(name):
+    """Occurrences of a parameter in optim_parameters() (deeplab_multi.py:139-171, Q2).
+    Returns (group, k); bn1 (requires_grad=False, :76-77) -> (0, 0)."""
+    if name.startswith("bn1."):
+        return 0, 0
+    if name == "conv1.weight":
+        return 0, 1
+    if name.startswith("layer5.") or name.startswith("layer6."):
+        return 1, 1
+    return 0, 4 if ".downsample." in name else 3
+
+
+def optim_param_lists(names):
+    """The two group lists with duplicates, in the reference's generator order."""
+    g0 = []
+    order = ["conv1", "bn1", "layer1", "layer2", "layer3", "layer4"]
+    by_prefix = {p: [n for n in names if n.split(".")[0] == p] for p in order}
+    # b[i].modules() walks the module tree depth-first, each module yielding ALL its (recursive) params
+    for top in order:
+        pn = by_prefix[top]
+        if top in ("conv1", "bn1"):
+            g0 += [n for n in pn if multiplicity(n)[1] > 0]
+            continue
+        g0 += pn  # the Sequential itself
+        blocks = sorted({int(n.split(".")[1]) for n in pn})
+        for b in blocks:
+            bp = [n for n in pn if n.split(".")[1] == str(b)]
+            g0 += bp  # the Bottleneck
+            subs = []
+            for n in bp:
+                sub = n.split(".")[2]
+                if sub not in subs:
+                    subs.append(sub)
+            for sub in subs:
+                sp = [n for n in bp if n.split(".")[2] == sub]
+                if sub == "downsample":
+                    g0 += sp  # the downsample Sequential
+                    for leaf in ("0", "1"):
+                        g0 += [n for n in sp if n.split(".")[3] == leaf]
+                else:
+                    g0 += sp
+    g1 = [n for n in names if n.startswith("layer5.") or n.startswith("layer6.")]
+    return g0, g1
+
+
+# --------------------------------------------------------------------------- forward
+def _bn(x, params, buffers, name, training):
+    return F.batch_norm(x, buffers[name + ".running_mean"], buffers[name + ".running_var"],
+                        params[name + ".weight"], params[name + ".bias"], training, 0.1, 1e-5)
+
+
+def _bottleneck(x, params, buffers, pre, stride, dil, has_down, training):
+    out = F.conv2d(x, params[pre + "conv1.weight"], stride=stride)
+    out = F.relu(_bn(out, params, buffers, pre + "bn1", training))
+    out = F.conv2d(out, params[pre + "conv2.weight"], padding=dil, dilation=dil)
+    out = F.relu(_bn(out, params, buffers, pre + "bn2", training))
+    out = F.conv2d(out, params[pre + "conv3.weight"])
+    out = _bn(out, params, buffers, pre + "bn3", training)
+    res = x
+    if has_down:
+        res = F.conv2d(x, params[pre + "downsample.0.weight"], stride=stride)
+        res = _bn(res, params, buffers, pre + "downsample.1", training)
+    return F.relu(out + res)
+
+
+def _aspp(x, params, head):
+    # Classifier_Module.forward returns after the first loop iteration (deeplab_multi.py:63-66)
+    out = F.conv2d(x, params[f"{head}.conv2d_list.0.weight"], params[f"{head}.conv2d_list.0.bias"],
+                   padding=ASPP_DIL[0], dilation=ASPP_DIL[0])
+    return out + F.conv2d(x, params[f"{head}.conv2d_list.1.weight"], params[f"{head}.conv2d_list.1.bias"],
+                          padding=ASPP_DIL[1], dilation=ASPP_DIL[1])
+
+
+def features(params, buffers, x, training=True):
+    x = F.conv2d(x, params["conv1.weight"], stride=2, padding=3)
+    x = F.relu(_bn(x, params, buffers, "bn1", training))
+    x = F.max_pool2d(x, 3, 2, 1, ceil_mode=True)
+    low = {}
+    for li, (n, stride, dil) in enumerate(zip(LAYERS, STRIDES, DILATIONS)):
+        for b in range(n):
+            x = _bottleneck(x, params, buffers, f"layer{li + 1}.{b}.", stride if b == 0 else 1, dil, b == 0, training)
+        low[li + 1] = x
+    return low
+
+
+def forward_low(params, buffers, x, training=True):
+    """(x2_low, x1_low): the ASPP outputs before upsampling."""
+    x = F.conv2d(x, params["conv1.weight"], stride=2, padding=3)
+    x = F.relu(_bn(x, params, buffers, "bn1", training))
+    x = F.max_pool2d(x, 3, 2, 1, ceil_mode=True)
+    for li in range(3):
+        for b in range(LAYERS[li]):
+            x = _bottleneck(x, params, buffers, f"layer{li + 1}.{b}.", STRIDES[li] if b == 0 else 1,
+                            DILATIONS[li], b == 0, training)
+    x1 = _aspp(x, params, "layer5")
+    for b in range(LAYERS[3]):
+        x = _bottleneck(x, params, buffers, f"layer4.{b}.", 1, DILATIONS[3], b == 0, training)
+    x2 = _aspp(x, params, "layer6")
+    return x2, x1
+
+
+def forward(params, buffers, x, training=True):
+    """ResNetMulti.forward (deeplab_multi.py:113-130) -> (x2, x1) upsampled to the input size."""
+    hw = x.shape[2:]
+    x2, x1 = forward_low(params, buffers, x, training)
+    up = lambda t: F.interpolate(t, size=hw, mode="bilinear", align_corners=True)  # noqa: E731
+    return up(x2), up(x1)
+
+
+# --------------------------------------------------------------------------- losses
+def ce(pred, y):
+    return F.cross_entropy(pred, y, ignore_index=-1)
+
+
+def maxsquare(prob):
+    mask = prob != -1  # always true (Q5)
+    return -torch.mean(torch.pow(prob, 2)[mask]) / 2
+
+
+def iw_hist_weights(prob, ratio, num_class, label=None):
+    maxpred, argpred = torch.max(prob, 1)
+    if label is None:
+        label = argpred
+    hist = torch.histc(label[0].detach().cpu().float(), bins=num_class + 1, min=-1, max=num_class - 1)[1:]
+    w = 1 / torch.max(torch.pow(hist, ratio) * torch.pow(hist.sum(), 1 - ratio), torch.ones(1))
+    return hist, w, argpred
+
+
+def iw_maxsquare(prob, ratio, num_class, label=None):
+    hist, w, argpred = iw_hist_weights(prob, ratio, num_class, label)
+    weights = w[argpred[0]].detach().unsqueeze(0)
+    n = prob.size(0)
+    return -torch.sum(torch.pow(prob, 2) * weights) / (n * num_class), hist
+
+
+def multi_guidance_label(P, P2, threshold):
+    maxpred, _ = torch.max(P.detach(), dim=1)
+    maxpred_2, _ = torch.max(P2.detach(), dim=1)
+    pred_c = (P + P2) / 2
+    _, argpred_c = torch.max(pred_c, dim=1)
+    mask = (maxpred > threshold) | (maxpred_2 > threshold)
+    return torch.where(mask, argpred_c, torch.full_like(argpred_c, -1))
+
+
+def multi_guidance_ce(pred, pred_2, threshold):
+    P = F.softmax(pred, dim=1)
+    P2 = F.softmax(pred_2, dim=1)
+    return ce(pred_2, multi_guidance_label(P, P2, threshold))
+
+
+# --------------------------------------------------------------------------- SGD
+class SGDMult:
+    """torch.optim.SGD(momentum, weight_decay) single-tensor semantics over the duplicated
+    group lists: k sequential updates, one shared buffer, fresh buffer per occurrence on the
+    first step (the last kept).  Parameters whose grad is None are skipped."""
+
+    def __init__(self, params, names, lr, momentum=0.9, weight_decay=5e-4):
+        self.params = params
+        g0, g1 = optim_param_lists(names)
+        self.groups = [{"names": g0, "lr": lr}, {"names": g1, "lr": 10 * lr}]
+        self.momentum, self.wd = momentum, weight_decay
+        self.buf = {}
+
+    @torch.no_grad()
+    def step(self):
+        for g in self.groups:
+            lr = g["lr"]
+            bufs = [self.buf.get(n) for n in g["names"]]
+            for i, n in enumerate(g["names"]):
+                p = self.params[n]
+                if p.grad is None:
+                    continue
+                d = p.grad.add(p, alpha=self.wd)
+                if self.momentum != 0:
+                    b = bufs[i]
+                    if b is None:
+                        b = torch.clone(d).detach()
+                        bufs[i] = b
+                    else:
+                        b.mul_(self.momentum).add_(d)
+                    d = b
+                p.add_(d, alpha=-lr)
+            for n, b in zip(g["names"], bufs):
+                if b is not None:
+                    self.buf[n] = b
+
+    def zero_grad(self):
+        for p in self.params.values():
+            p.grad = None
+
+
+# --------------------------------------------------------------------------- steps
+class Model:
+    """Parameters + BN buffers as plain tensors (state_dict naming of DeeplabMulti)."""
+
+    def __init__(self, state_dict, num_classes=19):
+        self.num_classes = num_classes
+        names = [n for n, _, _ in param_specs(num_classes)]
+        self.names = names
+        self.params = {n: state_dict[n].detach().clone().float() for n in names}
+        for n in names:
+            self.params[n].requires_grad_(multiplicity(n)[1] > 0)
+        self.buffers = {k: v.detach().clone() for k, v in state_dict.items() if k not in self.params}
+
+    def __call__(self, x, training=True):
+        return forward(self.params, self.buffers, x, training)
+
+    def state_dict(self):
+        sd = {n: p.detach() for n, p in self.params.items()}
+        sd.update(self.buffers)
+        return sd
+
+
+def poly_lr(init_lr, it, max_iter, power=0.9):
+    """train_source.py:706-717."""
+    return init_lr * (1 - float(it) / max_iter) ** power
+
+
+def uda_step(model, opt, xs, ys, xt, cfg, it):
+    """One iteration of solve_gta5.py:335-387.  cfg keys: lr, iter_max, target_mode
+    ('maxsquare'|'IW_maxsquare'), multi, lambda_seg, lambda_target, IW_ratio, threshold."""
+    lr = poly_lr(cfg["lr"], it, cfg["iter_max"])
+    opt.groups[0]["lr"], opt.groups[1]["lr"] = lr, 10 * lr
+    out = {}
+    pred, pred_2 = model(xs)
+    loss_s = ce(pred, ys)
+    loss_ = loss_s
+    if cfg["multi"]:
+        loss_2 = cfg["lambda_seg"] * ce(pred_2, ys)
+        loss_ = loss_ + loss_2
+        out["loss_seg_2"] = loss_2.item()
+    loss_.backward()
+    out["loss_seg"] = loss_s.item()
+    pred, pred_2 = model(xt)
+    P = F.softmax(pred, dim=1)
+    if cfg["target_mode"] == "maxsquare":
+        lt = maxsquare(P)
+    elif cfg["target_mode"] == "IW_maxsquare":
+        lt, hist = iw_maxsquare(P, cfg["IW_ratio"], model.num_classes)
+        out["hist"] = hist.numpy().astype(np.int64)
+    else:
+        raise ValueError(cfg["target_mode"])
+    loss_t = cfg["lambda_target"] * lt
+    total = loss_t
+    if cfg["multi"]:
+        lt2 = cfg["lambda_seg"] * cfg["lambda_target"] * multi_guidance_ce(pred, pred_2, cfg["threshold"])
+        total = total + lt2
+        out["loss_target_2"] = lt2.item()
+    total.backward()
+    out["loss_target"] = loss_t.item()
+    opt.step()
+    opt.zero_grad()
+    return out
+
+
+def source_step(model, opt, x, y, cfg, it):
+    """train_source.py:233-264 (one iteration of the source-only trainer)."""
+    lr = poly_lr(cfg["lr"], it, cfg["iter_max"])
+    opt.groups[0]["lr"], opt.groups[1]["lr"] = lr, 10 * lr
+    pred, pred_2 = model(x)
+    cur = ce(pred, y)
+    if cfg["multi"]:
+        cur = cur + cfg["lambda_seg"] * ce(pred_2, y)
+    opt.zero_grad()
+    cur.backward()
+    opt.step()
+    return {"loss": cur.item()}
