@@ -150,6 +150,28 @@ int msl_iw_maxsquare_prob_bwd(const float* prob, int c, int hw, const float* wei
                               const float* gout, float* dprob, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * BatchNorm2d fused with the Bottleneck's ReLU / residual add (deeplab_multi.py:31-46,
+ * :115-117): y = act(bn(x) [+ residual]), act = ReLU if relu else identity.
+ * training = 1: batch statistics over the p = H*W pixels of each of the c channels
+ * (bs = 1, quirk Q9), accumulated in fp64; running stats updated with momentum and
+ * the unbiased variance when update_running; num_batches_tracked (nullable) += 1.
+ * training = 0: running statistics (model.eval() / --freeze_bn).
+ * save_mean / save_invstd [c] are outputs consumed by msl_bn_bwd.
+ * ---------------------------------------------------------------------- */
+size_t msl_bn_workspace(int c, int p);
+int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const float* residual,
+               float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
+               float* save_mean, float* save_invstd, int c, int p, int training,
+               int update_running, float momentum, float eps, int relu, void* ws,
+               size_t ws_bytes, msl_stream_t stream);
+/* dx (nullable), dres = d residual (nullable), dgamma / dbeta (nullable); y is the
+ * forward output (needed when relu). */
+int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gamma,
+               const float* save_mean, const float* save_invstd, float* dx, float* dres,
+               float* dgamma, float* dbeta, int c, int p, int training, int relu, void* ws,
+               size_t ws_bytes, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * SGD step with the reference's duplicated-parameter semantics (quirk Q2):
  * torch.optim.SGD(momentum, weight_decay) single-tensor loop over the
  * optim_parameters() groups (train_source.py:139-144, deeplab_multi.py:132-171),

@@ -19,7 +19,7 @@ static inline hipStream_t as_stream(msl_stream_t s) { return reinterpret_cast<hi
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // 64-lane wave reductions (CDNA wave = 64).
 __device__ __forceinline__ float wave_sum(float v) {

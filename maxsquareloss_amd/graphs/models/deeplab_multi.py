@@ -15,8 +15,10 @@ What runs where:
     two-branch HIP conv with both biases;
   - bilinear upsampling (align_corners=True) -> HIP kernel; the result keeps a
     handle on the low-res logits for the fused losses;
-  - stem, 1x1 convs, BatchNorm (train mode, per replica, Q9), ReLU, maxpool ->
-    PyTorch-ROCm (MIOpen), SURVEY.md §8a row a13.
+  - every BatchNorm (train mode, batch statistics of the one image, Q9) fused with the
+    following ReLU and, for bn3, the residual add -> HIP kernels with fp64-accumulated
+    statistics (MIOpen's single-pass variance is not accurate enough at bs=1);
+  - stem 7x7 conv, 1x1 convs, maxpool -> PyTorch-ROCm (MIOpen), SURVEY.md §8a row a13.
 """
 import torch
 import torch.nn as nn
@@ -56,14 +58,13 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        out = ops.bn_act(self.bn1, self.conv1(x), relu=True)
+        out = ops.bn_act(self.bn2, self.conv2(out), relu=True)
         residual = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
         if self.downsample is not None:
-            residual = self.downsample(x)
-        out += residual
-        return self.relu(out)
+            residual = ops.bn_act(self.downsample[1], self.downsample[0](x))
+        # bn3 + residual add + ReLU in one kernel (deeplab_multi.py:38-46)
+        return ops.bn_act(self.bn3, self.conv3(out), residual=residual, relu=True)
 
 
 class Classifier_Module(nn.Module):
@@ -132,7 +133,7 @@ class ResNetMulti(nn.Module):
 
     def forward(self, x):
         input_size = x.size()[2:]
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(ops.bn_act(self.bn1, self.conv1(x), relu=True))
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -401,3 +401,57 @@ def maxsquare_prob(prob):
 
 def iw_maxsquare_prob(prob, label, ratio):
     return _IWMaxSquareProb.apply(prob, label, float(ratio))
+
+
+# --------------------------------------------------------------------------- batch norm (+ReLU, +residual)
+class _BNAct(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, training, momentum,
+                eps, relu):
+        x = _check_act(x, "bn_act")
+        c, p = x.size(1), x.size(2) * x.size(3)
+        if residual is not None:
+            residual = residual.contiguous()
+            if residual.shape != x.shape:
+                raise hip.MSLError("bn_act: residual shape mismatch")
+        lib = hip.load()
+        y = torch.empty_like(x)
+        save_mean = torch.empty(c, dtype=_f32, device=x.device)
+        save_invstd = torch.empty(c, dtype=_f32, device=x.device)
+        wsb = lib.msl_bn_workspace(c, p)
+        ws = hip.workspace(wsb, x.device)
+        update = bool(training) and running_mean is not None
+        hip.check(lib.msl_bn_fwd(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
+                                 hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
+                                 save_mean.data_ptr(), save_invstd.data_ptr(), c, p, int(bool(training)), int(update),
+                                 float(momentum), float(eps), int(bool(relu)), ws.data_ptr(), wsb, hip.stream_ptr()),
+                  "msl_bn_fwd")
+        ctx.save_for_backward(x, weight, y if relu else None, save_mean, save_invstd)
+        ctx.meta = (c, p, bool(training), bool(relu))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y, save_mean, save_invstd = ctx.saved_tensors
+        c, p, training, relu = ctx.meta
+        gy = gy.contiguous()
+        lib = hip.load()
+        nig = ctx.needs_input_grad
+        dx = torch.empty_like(x) if nig[0] else None
+        dgamma = torch.empty(c, dtype=_f32, device=x.device) if nig[1] else None
+        dbeta = torch.empty(c, dtype=_f32, device=x.device) if nig[2] else None
+        dres = torch.empty_like(x) if nig[3] else None
+        wsb = lib.msl_bn_workspace(c, p)
+        ws = hip.workspace(wsb, x.device)
+        hip.check(lib.msl_bn_bwd(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight), save_mean.data_ptr(),
+                                 save_invstd.data_ptr(), hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta),
+                                 c, p, int(training), int(relu), ws.data_ptr(), wsb, hip.stream_ptr()), "msl_bn_bwd")
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+
+
+def bn_act(bn, x, residual=None, relu=False):
+    """act(bn(x) [+ residual]) for an nn.BatchNorm2d `bn` (train mode: batch statistics, bs = 1)."""
+    training = bn.training or not bn.track_running_stats
+    momentum = 0.1 if bn.momentum is None else bn.momentum
+    return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
+                        bn.num_batches_tracked if training else None, training, momentum, bn.eps, relu)

@@ -212,3 +212,44 @@ def test_sgd_multiplicity_matches_torch_cpu():
     torch.cuda.synchronize()
     for a, b in zip(mine, ref):
         assert _rel(a, b) < 1e-6
+
+
+@pytest.mark.parametrize("c,h,w,res,relu,train", [(64, 129, 257, False, True, True), (256, 65, 129, True, True, True),
+                                                  (1024, 33, 65, False, False, True), (64, 17, 33, True, True, False)])
+def test_bn_act(c, h, w, res, relu, train):
+    g = torch.Generator().manual_seed(c + h)
+    x = torch.randn(1, c, h, w, generator=g) * 3 + 40.0  # large mean: the cancellation case
+    r = torch.randn(1, c, h, w, generator=g) if res else None
+    gamma = torch.rand(c, generator=g) + 0.5
+    beta = torch.randn(c, generator=g)
+    rm, rv = torch.randn(c, generator=g), torch.rand(c, generator=g) + 0.5
+    gy = torch.randn(1, c, h, w, generator=g)
+    bn = torch.nn.BatchNorm2d(c).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+        bn.running_mean.copy_(rm)
+        bn.running_var.copy_(rv)
+    bn.train(train)
+    xr = x.double().requires_grad_()
+    gr, br = gamma.double().requires_grad_(), beta.double().requires_grad_()
+    rmr, rvr = rm.double(), rv.double()
+    rr = r.double().requires_grad_() if res else None
+    yr = torch.nn.functional.batch_norm(xr, rmr, rvr, gr, br, train, 0.1, 1e-5)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    yr.backward(gy.double())
+    xg = x.to(DEV).requires_grad_()
+    rg = r.to(DEV).requires_grad_() if res else None
+    y = ops.bn_act(bn, xg, residual=rg, relu=relu)
+    y.backward(gy.to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 1e-5
+    assert _rel(xg.grad, xr.grad) < 1e-4
+    assert _rel(bn.weight.grad, gr.grad) < 1e-5
+    assert _rel(bn.bias.grad, br.grad) < 1e-5
+    if res:
+        assert _rel(rg.grad, rr.grad) < 1e-6
+    assert _rel(bn.running_mean, rmr) < 1e-5 and _rel(bn.running_var, rvr) < 1e-5
