@@ -258,17 +258,19 @@ class SGDMult:
 class Model:
     """Parameters + BN buffers as plain tensors (state_dict naming of DeeplabMulti)."""
 
-    def __init__(self, state_dict, num_classes=19):
+    def __init__(self, state_dict, num_classes=19, dtype=torch.float32):
         self.num_classes = num_classes
+        self.dtype = dtype
         names = [n for n, _, _ in param_specs(num_classes)]
         self.names = names
-        self.params = {n: state_dict[n].detach().clone().float() for n in names}
+        self.params = {n: state_dict[n].detach().clone().to(dtype) for n in names}
         for n in names:
             self.params[n].requires_grad_(multiplicity(n)[1] > 0)
-        self.buffers = {k: v.detach().clone() for k, v in state_dict.items() if k not in self.params}
+        self.buffers = {k: (v.detach().clone().to(dtype) if v.is_floating_point() else v.detach().clone())
+                        for k, v in state_dict.items() if k not in self.params}
 
     def __call__(self, x, training=True):
-        return forward(self.params, self.buffers, x, training)
+        return forward(self.params, self.buffers, x.to(self.dtype), training)
 
     def state_dict(self):
         sd = {n: p.detach() for n, p in self.params.items()}
