@@ -1,0 +1,211 @@
+"""CPU tests of the host side: the C-ABI library, the model/optimizer plumbing and DP exchange."""
+import json
+import os
+import re
+import socket
+import subprocess
+import sys
+from collections import Counter
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "msl_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(msl_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from maxsquareloss_amd import hip
+    lib = hip.load(require_gpu=False)
+    syms = _header_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(hip.SIGNATURES) == set(syms), "ctypes signatures out of sync with include/msl_hip.h"
+    out = subprocess.run(["nm", "-D", "--defined-only", hip.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (msl_\w+)", out))
+    assert set(syms) <= exported
+
+
+def test_library_is_gfx950_code_object():
+    from maxsquareloss_amd import hip
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", hip.LIB_PATH],
+                         capture_output=True, text=True, cwd="/tmp")
+    assert "gfx950" in (out.stdout + out.stderr)
+
+
+def test_pure_host_entry_points():
+    from maxsquareloss_amd import hip
+    lib = hip.load(require_gpu=False)
+    assert lib.msl_abi_version() == hip.ABI_VERSION
+    assert lib.msl_status_string(-2) == b"workspace too small"
+    # packed-weight sizes: [nbranch][ceil(cimg/16)][9][16] rows x round_up(m, 128)
+    assert lib.msl_dconv_packed_elems(1, 256, 256, 0) == 16 * 9 * 16 * 256
+    assert lib.msl_dconv_packed_elems(2, 2048, 19, 0) == 2 * 128 * 9 * 16 * 128
+    assert lib.msl_dconv_packed_elems(2, 2048, 19, 1) == 2 * 2 * 9 * 16 * 2048
+    assert lib.msl_dconv_fwd_workspace(1, 256, 256, 65, 129) > 0  # split-K slabs at this size
+    assert lib.msl_loss_stats_elems() == 64
+    be = lib.msl_sgd_block_elems()
+    numels = np.array([10, be, be + 1, 0], dtype=np.int64)
+    assert lib.msl_sgd_plan(numels.ctypes.data, 4, None, None, 0) == 1 + 1 + 2
+    ent = np.zeros(8, np.int32)
+    off = np.zeros(8, np.int64)
+    n = lib.msl_sgd_plan(numels.ctypes.data, 4, ent.ctypes.data, off.ctypes.data, 8)
+    assert n == 4 and list(ent[:4]) == [0, 1, 2, 2] and list(off[:4]) == [0, 0, 0, be]
+
+
+def test_compute_calls_fail_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from maxsquareloss_amd import hip, ops
+    with pytest.raises(hip.MSLError):
+        ops.dconv3x3(torch.zeros(1, 4, 5, 5), torch.zeros(4, 4, 3, 3), 2, ops.PackCache())
+    with pytest.raises(hip.MSLError):
+        hip.load(require_gpu=True)
+
+
+def test_model_matches_reference_structure():
+    from oracle import msl_oracle as orc
+    from maxsquareloss_amd.graphs.models.deeplab_multi import DeeplabMulti
+    m = DeeplabMulti(19, pretrained=False)
+    specs = orc.param_specs(19)
+    assert [n for n, _ in m.named_parameters()] == [n for n, _, _ in specs]
+    assert [tuple(p.shape) for _, p in m.named_parameters()] == [s for _, s, _ in specs]
+    assert sum(p.numel() for p in m.parameters()) == 44601560
+    assert not m.bn1.weight.requires_grad
+    with pytest.raises(FileNotFoundError):
+        DeeplabMulti(19, pretrained=True)
+
+
+def test_optim_parameters_duplicates_match_reference():
+    from maxsquareloss_amd.graphs.models.deeplab_multi import DeeplabMulti
+    from maxsquareloss_amd.utils.optim import unique_with_multiplicity
+    m = DeeplabMulti(19, pretrained=False)
+    names = {id(p): n for n, p in m.named_parameters()}
+
+    class A:
+        lr = 2.5e-4
+    groups = m.optim_parameters(A)
+    lists = [[names[id(p)] for p in g["params"]] for g in groups]
+    ref = json.load(open(os.path.join(GOLD, "optim_lists.json")))
+    assert lists[0] == ref["group0"] and lists[1] == ref["group1"]
+    groups = m.optim_parameters(A)
+    uniq = unique_with_multiplicity(list(groups[0]["params"]))
+    mult = Counter(k for _, k in uniq)
+    assert mult == Counter({3: 297, 4: 12, 1: 1})
+    live = sum(p.numel() for n, p in m.named_parameters()
+               if p.requires_grad and not any(f"conv2d_list.{i}" in n for i in (2, 3)))
+    assert live == 43550732  # the live fp32 gradient set exchanged per iteration
+
+
+def test_synthetic_generators_are_deterministic():
+    from maxsquareloss_amd.utils.synthetic import counter_normal, synthetic_image, synthetic_labels
+    a = counter_normal(1, "x", 1000, 0.01)
+    assert np.array_equal(a, counter_normal(1, "x", 1000, 0.01))
+    assert abs(a.std() - 0.01) < 0.001 and abs(a.mean()) < 0.002
+    img = synthetic_image(8, 16, 3)
+    assert img.shape == (1, 3, 8, 16) and img.dtype == torch.float32
+    assert img.min() >= -123 and img.max() <= 256 - 104
+    lab = synthetic_labels(8, 16, 19, 3)
+    assert lab.dtype == torch.int64 and lab.min() >= -1 and lab.max() <= 18
+
+
+def test_bench_feature_geometry():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.feat_hw(512) == 65 and bench.feat_hw(1024) == 129
+    assert bench.feat_hw(640) == 81 and bench.feat_hw(760) == 96 and bench.feat_hw(1280) == 161
+
+
+def test_poly_lr_matches_reference_formula():
+    from maxsquareloss_amd.tools.train_source import Trainer
+
+    class O:
+        param_groups = [{"lr": 0}, {"lr": 0}]
+
+    class T:
+        args = type("a", (), {"lr": 2.5e-4, "iter_max": 1000, "poly_power": 0.9})()
+        current_iter = 100
+    Trainer.poly_lr_scheduler(T, O, init_lr=2.5e-4, iter=100, max_iter=1000, power=0.9)
+    assert O.param_groups[0]["lr"] == pytest.approx(2.5e-4 * 0.9 ** 0.9)
+    assert O.param_groups[1]["lr"] == pytest.approx(10 * O.param_groups[0]["lr"])
+
+
+# ---------------------------------------------------------------------------- DP (gloo, 2 ranks)
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    from maxsquareloss_amd.utils.dist import GradReducer
+    from maxsquareloss_amd.utils.optim import SGD
+    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4),
+                              torch.nn.Linear(4, 4))  # the last layer is never used: a "dead" param
+    dead = net[3]
+    plist = [p for p in net.parameters()]
+    opt = SGD([{"params": plist[:2] + plist[:2], "lr": 0.1}, {"params": plist[2:], "lr": 1.0}],
+              lr=0.1, momentum=0.9, weight_decay=5e-4)
+    red = GradReducer(opt, bucket_cap_mb=0.0002)  # ~50 floats per bucket -> several buckets
+    results = []
+    for it in range(3):
+        opt.zero_grad()
+        g = torch.Generator().manual_seed(100 * it + rank)
+        x1, x2 = torch.randn(5, 8, generator=g), torch.randn(3, 8, generator=g)
+        net[2](net[1](net[0](x1))).pow(2).sum().backward()      # "source" backward: local only
+        red.prepare_for_backward()
+        net[2](net[1](net[0](x2))).sum().backward()             # "target" backward: overlapped reduce
+        red.finish()
+        results.append([p.grad.detach().numpy().copy() for p in plist] + [opt.grads.used.copy()])
+        assert dead.weight.grad.abs().sum() == 0
+    q.put((rank, results, red.live.copy(), opt.grad_scale))
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_two_ranks_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (res, live, gs)) for r, res, live, gs in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # expected: the rank-sum of each rank's own (source + target) gradients
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4), torch.nn.Linear(4, 4))
+    plist = list(net.parameters())
+    for it in range(3):
+        total = [torch.zeros_like(p) for p in plist]
+        for r in range(world):
+            net.zero_grad()
+            g = torch.Generator().manual_seed(100 * it + r)
+            x1, x2 = torch.randn(5, 8, generator=g), torch.randn(3, 8, generator=g)
+            net[2](net[1](net[0](x1))).pow(2).sum().backward()
+            net[2](net[1](net[0](x2))).sum().backward()
+            for t, p in zip(total, plist):
+                if p.grad is not None:
+                    t += p.grad
+        for r in range(world):
+            res = got[r][0][it]
+            for a, b in zip(res[:-1], total):
+                np.testing.assert_allclose(a, b.numpy(), rtol=1e-5, atol=1e-6)
+    for r in range(world):
+        assert got[r][2] == pytest.approx(1.0 / world)
+        live = got[r][1]
+        assert live.sum() == 4  # the 2 Linear layers in use (weight, bias each); dead layer excluded
