@@ -21,273 +21,9 @@
 // read is a conflict-free ds_read_b32 of 32 consecutive floats), double
 // buffered, one barrier per K-step.  Small GEMMs are split along K into fp32
 // slabs that a reduce kernel sums deterministically (fixed order).
-#include "msl_internal.h"
+#include "dconv_kernels.h"
 
 namespace msl {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int kCB = 16;       // channels per forward K-step
-constexpr int kPackPad = 128; // packed-weight row padding (>= any BM)
-
-struct FwdArgs {
-  const float* A;     // packed weights [Kp][lda]
-  const float* B;     // image [cimg][P]
-  float* C;           // out [M][P] or slabs [S][M][P]
-  const float* bias;  // [nbias][M] or null (only used when S == 1)
-  int nbias;
-  int M, lda, H, W, P, cimg, ncb, dil0, dil1, ksteps, kps;
-  long long slab;
-};
-
-struct WgradArgs {
-  const float* dy;  // [M][P]
-  const float* x;   // [N][P]
-  float* C;         // dW [nbranch][M][N][9] or slabs of that
-  int M, N, H, W, P, dil0, dil1, ntap, ksteps, kps, accumulate;
-  long long slab, cbranch;
-};
-
-template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
-  constexpr int BK = kCB;
-  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
-  constexpr int LDA_S = BM + 4, LDB_S = BN + 4;
-  constexpr int A_STAGE = BK * LDA_S, STAGE = A_STAGE + BK * LDB_S;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int split = blockIdx.z;
-  const int s_begin = split * a.kps;
-  const int s_end = min(a.ksteps, s_begin + a.kps);
-
-  constexpr int BROWS = 256 / BN;
-  constexpr int BPASS = BK / BROWS;
-  const int bn = tid % BN, brow0 = tid / BN;
-  const int p = n0 + bn;
-  const int py = p / a.W, px = p - py * a.W;
-  const bool pin = p < a.P;
-
-  constexpr int A_F4_ROW = BM / 4;
-  constexpr int A_F4 = BK * A_F4_ROW;
-  constexpr int APASS = (A_F4 + 255) / 256;
-
-  float4 ra[APASS];
-  float rb[BPASS];
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int per_b = a.ncb * 9;
-  auto gload = [&](int s) {
-    const int b = s / per_b;
-    const int rem = s - b * per_b;
-    const int cb = rem / 9;
-    const int t = rem - cb * 9;
-    const int d = b ? a.dil1 : a.dil0;
-    const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
-    const bool v = pin && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
-    const int ci0 = cb * kCB + brow0;
-    const float* src = a.B + (long long)ci0 * a.P + (p + dh * a.W + dw);
-#pragma unroll
-    for (int j = 0; j < BPASS; ++j) {
-      const int ci = ci0 + j * BROWS;
-      rb[j] = (v && ci < a.cimg) ? src[(long long)(j * BROWS) * a.P] : 0.f;
-    }
-    const float* ab = a.A + (long long)s * BK * a.lda + m0;
-#pragma unroll
-    for (int i = 0; i < APASS; ++i) {
-      const int idx = tid + i * 256;
-      if (A_F4 % 256 == 0 || idx < A_F4) {
-        const int r = idx / A_F4_ROW, c4 = idx - r * A_F4_ROW;
-        ra[i] = *reinterpret_cast<const float4*>(ab + (long long)r * a.lda + c4 * 4);
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-    float* As = smem + buf * STAGE;
-    float* Bs = As + A_STAGE;
-#pragma unroll
-    for (int i = 0; i < APASS; ++i) {
-      const int idx = tid + i * 256;
-      if (A_F4 % 256 == 0 || idx < A_F4) {
-        const int r = idx / A_F4_ROW, c4 = idx - r * A_F4_ROW;
-        *reinterpret_cast<float4*>(As + r * LDA_S + c4 * 4) = ra[i];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < BPASS; ++j) Bs[(brow0 + j * BROWS) * LDB_S + bn] = rb[j];
-  };
-  auto compute = [&](int buf) {
-    const float* As = smem + buf * STAGE;
-    const float* Bs = As + A_STAGE;
-    const int l32 = lane & 31, kh = lane >> 5;
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const int kr = kk + kh;
-      float av[TM], bv[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = As[kr * LDA_S + wm + i * 32 + l32];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = Bs[kr * LDB_S + wn + j * 32 + l32];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  if (s_begin < s_end) {
-    gload(s_begin);
-    sstore(0);
-    __syncthreads();
-    int cur = 0;
-    for (int s = s_begin; s < s_end; ++s) {
-      const bool more = s + 1 < s_end;
-      if (more) gload(s + 1);
-      compute(cur);
-      if (more) sstore(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
-    }
-  }
-
-  float* C = a.C + (long long)split * a.slab;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int n = n0 + wn + j * 32 + (lane & 31);
-        if (m < a.M && n < a.P) {
-          float v = acc[i][j][r];
-          if (a.bias) {
-            float bsum = a.bias[m];
-            for (int b = 1; b < a.nbias; ++b) bsum += a.bias[b * a.M + m];
-            v += bsum;
-          }
-          C[(long long)m * a.P + n] = v;
-        }
-      }
-}
-
-template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256) k_igemm_wgrad(WgradArgs a) {
-  constexpr int BK = 32;
-  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
-  constexpr int LDA_S = BM + 1, LDB_S = BN + 1;  // odd strides: transposing writes are conflict-free
-  constexpr int A_STAGE = BK * LDA_S, STAGE = A_STAGE + BK * LDB_S;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int tapz = blockIdx.z % a.ntap;
-  const int split = blockIdx.z / a.ntap;
-  const int br = tapz / 9, t = tapz - br * 9;
-  const int d = br ? a.dil1 : a.dil0;
-  const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
-  const int s_begin = split * a.kps;
-  const int s_end = min(a.ksteps, s_begin + a.kps);
-
-  const int kl = tid & 31, r0 = tid >> 5;
-  constexpr int APASS = BM / 8, BPASS = BN / 8;
-  float ra[APASS], rb[BPASS];
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  auto gload = [&](int s) {
-    const int p = s * BK + kl;
-    const bool pv = p < a.P;
-    const int py = p / a.W, px = p - py * a.W;
-    const bool vb = pv && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
-    const int off = p + dh * a.W + dw;
-#pragma unroll
-    for (int j = 0; j < APASS; ++j) {
-      const int m = m0 + r0 + 8 * j;
-      ra[j] = (pv && m < a.M) ? a.dy[(long long)m * a.P + p] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < BPASS; ++j) {
-      const int n = n0 + r0 + 8 * j;
-      rb[j] = (vb && n < a.N) ? a.x[(long long)n * a.P + off] : 0.f;
-    }
-  };
-  auto sstore = [&](int buf) {
-    float* As = smem + buf * STAGE;
-    float* Bs = As + A_STAGE;
-#pragma unroll
-    for (int j = 0; j < APASS; ++j) As[kl * LDA_S + r0 + 8 * j] = ra[j];
-#pragma unroll
-    for (int j = 0; j < BPASS; ++j) Bs[kl * LDB_S + r0 + 8 * j] = rb[j];
-  };
-  auto compute = [&](int buf) {
-    const float* As = smem + buf * STAGE;
-    const float* Bs = As + A_STAGE;
-    const int l32 = lane & 31, kh = lane >> 5;
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const int kr = kk + kh;
-      float av[TM], bv[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = As[kr * LDA_S + wm + i * 32 + l32];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = Bs[kr * LDB_S + wn + j * 32 + l32];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  if (s_begin < s_end) {
-    gload(s_begin);
-    sstore(0);
-    __syncthreads();
-    int cur = 0;
-    for (int s = s_begin; s < s_end; ++s) {
-      const bool more = s + 1 < s_end;
-      if (more) gload(s + 1);
-      compute(cur);
-      if (more) sstore(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
-    }
-  }
-
-  float* C = a.C + (long long)split * a.slab + (long long)br * a.cbranch;
-  const long long ldc = (long long)a.N * 9;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int n = n0 + wn + j * 32 + (lane & 31);
-        if (m < a.M && n < a.N) {
-          const long long idx = (long long)m * ldc + (long long)n * 9 + t;
-          C[idx] = a.accumulate ? C[idx] + acc[i][j][r] : acc[i][j][r];
-        }
-      }
-}
 
 // out[i] = (acc ? out[i] : 0) + sum_s ws[s*n + i] (+ sum_b bias[b*M + i/bias_div])
 __global__ void __launch_bounds__(256) k_reduce_slabs(const float* __restrict__ ws, int S, long long n,
@@ -357,7 +93,7 @@ __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long 
 
 // ---------------------------------------------------------------- planning
 struct FwdPlan {
-  int bm, bn, tiles_m, tiles_n, ksteps, kps, S;
+  int bm, bn, bk, tiles_m, tiles_n, ksteps, kps, S;
 };
 
 static int pad_to(int v, int a) { return (v + a - 1) / a * a; }
@@ -374,27 +110,30 @@ static FwdPlan plan_fwd(int nbranch, int cimg, int M, int P) {
   FwdPlan pl;
   pl.bm = 64;
   pl.bn = 128;
+  const int groups = nbranch * cdiv(cimg, kCB) * 9;
+  pl.bk = groups % 2 == 0 ? 32 : 16;
   pl.tiles_m = cdiv(M, pl.bm);
   pl.tiles_n = cdiv(P, pl.bn);
-  pl.ksteps = nbranch * cdiv(cimg, kCB) * 9;
-  int S = choose_split(pl.tiles_m * pl.tiles_n, pl.ksteps, 8);
+  pl.ksteps = groups / (pl.bk / kCB);
+  int S = choose_split(pl.tiles_m * pl.tiles_n, pl.ksteps, 4);
   pl.kps = cdiv(pl.ksteps, S);
   pl.S = cdiv(pl.ksteps, pl.kps);
   return pl;
 }
 
 struct WgradPlan {
-  int bm, bn, tiles_m, tiles_n, ntap, ksteps, kps, S;
+  int bm, bn, bk, tiles_m, tiles_n, ntap, ksteps, kps, S;
 };
 
 static WgradPlan plan_wgrad(int nbranch, int cin, int cout, int P) {
   WgradPlan pl;
   pl.bm = 64;
   pl.bn = 128;
+  pl.bk = 32;
   pl.tiles_m = cdiv(cout, pl.bm);
   pl.tiles_n = cdiv(cin, pl.bn);
   pl.ntap = nbranch * 9;
-  pl.ksteps = cdiv(P, 32);
+  pl.ksteps = cdiv(P, pl.bk);
   int S = choose_split(pl.tiles_m * pl.tiles_n * pl.ntap, pl.ksteps, 8);
   pl.kps = cdiv(pl.ksteps, S);
   pl.S = cdiv(pl.ksteps, pl.kps);
@@ -430,7 +169,10 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   a.kps = pl.kps;
   a.slab = (long long)M * P;
   dim3 grid(pl.tiles_n, pl.tiles_m, pl.S);
-  hipLaunchKernelGGL((k_igemm_fwd<64, 128, 2, 2>), grid, dim3(256), 0, st, a);
+  if (pl.bk == 32)
+    hipLaunchKernelGGL((k_igemm_fwd<64, 128, 32, 2, 2>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_igemm_fwd<64, 128, 16, 2, 2>), grid, dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
   if (pl.S > 1) {
     const long long n = (long long)M * P;
@@ -551,7 +293,7 @@ int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, in
   a.slab = nout;
   a.cbranch = (long long)cout * cin * 9;
   dim3 grid(pl.tiles_n, pl.tiles_m, pl.S * pl.ntap);
-  hipLaunchKernelGGL((k_igemm_wgrad<64, 128, 2, 2>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((k_igemm_wgrad<64, 128, 32, 2, 2>), grid, dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
   if (pl.S > 1) {
     const int blocks = (int)std::min<long long>(cdiv(nout, 256), 4096);

@@ -1,0 +1,625 @@
+// Implicit-GEMM kernel templates for the dilated 3x3 conv (design notes in dconv.hip).
+// Shared by libmsl_hip.so (dconv.hip) and the standalone tuning harness (scripts/tune_dconv.hip).
+#pragma once
+#include "msl_internal.h"
+
+namespace msl {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kCB = 16;        // image channels per forward K-group (one tap, 16 channels)
+constexpr int kPackPad = 128;  // packed-weight row padding (>= any BM)
+
+struct FwdArgs {
+  const float* A;     // packed weights [Kp][lda]
+  const float* B;     // image [cimg][P]
+  float* C;           // out [M][P] or slabs [S][M][P]
+  const float* bias;  // [nbias][M] or null (only used when S == 1)
+  int nbias;
+  int M, lda, H, W, P, cimg, ncb, dil0, dil1, ksteps, kps;  // ksteps counts BK-deep steps
+  long long slab;
+};
+
+struct WgradArgs {
+  const float* dy;  // [M][P]
+  const float* x;   // [N][P]
+  float* C;         // dW [nbranch][M][N][9] or slabs of that
+  int M, N, H, W, P, dil0, dil1, ntap, ksteps, kps, accumulate;
+  long long slab, cbranch;
+};
+
+// acc[i][j] += A_tile(kk..kk+BK) x B_tile over one LDS stage; A at As[k][m], B at Bs[k][n].
+// All of the stage's operand reads are issued before the first MFMA, so the LDS latency of
+// k-pair kk+1.. overlaps the MFMAs of k-pair kk (the compiler emits counted lgkmcnt waits).
+template <int BK, int TM, int TN, int LDA_S, int LDB_S>
+__device__ __forceinline__ void mfma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
+                                           int wm, int wn, int lane, f32x16 (&acc)[TM][TN]) {
+  const int l32 = lane & 31, kh = lane >> 5;
+  constexpr int KP = BK / 2;
+  float av[KP][TM], bv[KP][TN];
+#pragma unroll
+  for (int kp = 0; kp < KP; ++kp) {
+    const int kr = 2 * kp + kh;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[kp][i] = As[kr * LDA_S + wm + i * 32 + l32];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[kp][j] = Bs[kr * LDB_S + wn + j * 32 + l32];
+  }
+#pragma unroll
+  for (int kp = 0; kp < KP; ++kp)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kp][i], bv[kp][j], acc[i][j], 0, 0, 0);
+}
+
+// Forward form: C[m][p] = sum_k A[k][m] * B[k][p], BK = G * 16 (G tap-groups per K-step).
+template <int BM, int BN, int BK, int WM, int WN>
+__global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
+  constexpr int G = BK / kCB;
+  static_assert(BK % kCB == 0, "BK multiple of 16");
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  constexpr int LDA_S = BM, LDB_S = BN;  // row reads are contiguous: no padding needed
+  constexpr int A_STAGE = BK * LDA_S, STAGE = A_STAGE + BK * LDB_S;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int split = blockIdx.z;
+  const int s_begin = split * a.kps;
+  const int s_end = min(a.ksteps, s_begin + a.kps);
+
+  constexpr int BROWS = 256 / BN;        // B rows per pass
+  constexpr int BPASS = kCB / BROWS;     // passes per tap-group
+  const int bn = tid % BN, brow0 = tid / BN;
+  const int p = n0 + bn;
+  const int py = p / a.W, px = p - py * a.W;
+  const bool pin = p < a.P;
+
+  constexpr int A_F4_ROW = BM / 4;
+  constexpr int A_F4 = BK * A_F4_ROW;
+  constexpr int APASS = (A_F4 + 255) / 256;
+
+  float4 ra[APASS];
+  float rb[G][BPASS];
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int per_b = a.ncb * 9;
+  auto gload = [&](int s) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int q = s * G + g;  // tap-group index
+      const int b = q / per_b;
+      const int rem = q - b * per_b;
+      const int cb = rem / 9;
+      const int t = rem - cb * 9;
+      const int d = b ? a.dil1 : a.dil0;
+      const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
+      const bool v = pin && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
+      const int ci0 = cb * kCB + brow0;
+      const float* src = a.B + (long long)ci0 * a.P + (p + dh * a.W + dw);
+#pragma unroll
+      for (int j = 0; j < BPASS; ++j) {
+        const int ci = ci0 + j * BROWS;
+        rb[g][j] = (v && ci < a.cimg) ? src[(long long)(j * BROWS) * a.P] : 0.f;
+      }
+    }
+    const float* ab = a.A + (long long)s * BK * a.lda + m0;
+#pragma unroll
+    for (int i = 0; i < APASS; ++i) {
+      const int idx = tid + i * 256;
+      if (A_F4 % 256 == 0 || idx < A_F4) {
+        const int r = idx / A_F4_ROW, c4 = idx - r * A_F4_ROW;
+        ra[i] = *reinterpret_cast<const float4*>(ab + (long long)r * a.lda + c4 * 4);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    float* As = smem + buf * STAGE;
+    float* Bs = As + A_STAGE;
+#pragma unroll
+    for (int i = 0; i < APASS; ++i) {
+      const int idx = tid + i * 256;
+      if (A_F4 % 256 == 0 || idx < A_F4) {
+        const int r = idx / A_F4_ROW, c4 = idx - r * A_F4_ROW;
+        *reinterpret_cast<float4*>(As + r * LDA_S + c4 * 4) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int j = 0; j < BPASS; ++j) Bs[(g * kCB + brow0 + j * BROWS) * LDB_S + bn] = rb[g][j];
+  };
+
+  if (s_begin < s_end) {
+    gload(s_begin);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int s = s_begin; s < s_end; ++s) {
+      const bool more = s + 1 < s_end;
+      if (more) gload(s + 1);
+      const float* As = smem + cur * STAGE;
+      mfma_stage<BK, TM, TN, LDA_S, LDB_S>(As, As + A_STAGE, wm, wn, lane, acc);
+      if (more) sstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  float* C = a.C + (long long)split * a.slab;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + j * 32 + (lane & 31);
+        if (m < a.M && n < a.P) {
+          float v = acc[i][j][r];
+          if (a.bias) {
+            float bsum = a.bias[m];
+            for (int b = 1; b < a.nbias; ++b) bsum += a.bias[b * a.M + m];
+            v += bsum;
+          }
+          C[(long long)m * a.P + n] = v;
+        }
+      }
+}
+
+// Weight gradient: dW[m][n][tap] = sum_p dY[m][p] * X[n][p + shift(tap)], BK pixels per K-step.
+template <int BM, int BN, int BK, int WM, int WN>
+__global__ void __launch_bounds__(256) k_igemm_wgrad(WgradArgs a) {
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  static_assert(BK == 32 || BK == 64, "BK");
+  constexpr int LDA_S = BM + 1, LDB_S = BN + 1;  // odd strides: transposing writes are conflict-free
+  constexpr int A_STAGE = BK * LDA_S, STAGE = A_STAGE + BK * LDB_S;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int tapz = blockIdx.z % a.ntap;
+  const int split = blockIdx.z / a.ntap;
+  const int br = tapz / 9, t = tapz - br * 9;
+  const int d = br ? a.dil1 : a.dil0;
+  const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
+  const int s_begin = split * a.kps;
+  const int s_end = min(a.ksteps, s_begin + a.kps);
+
+  constexpr int RSTEP = 256 / BK;  // rows covered per pass
+  const int kl = tid % BK, r0 = tid / BK;
+  constexpr int APASS = BM / RSTEP, BPASS = BN / RSTEP;
+  float ra[APASS], rb[BPASS];
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto gload = [&](int s) {
+    const int p = s * BK + kl;
+    const bool pv = p < a.P;
+    const int py = p / a.W, px = p - py * a.W;
+    const bool vb = pv && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
+    const int off = p + dh * a.W + dw;
+#pragma unroll
+    for (int j = 0; j < APASS; ++j) {
+      const int m = m0 + r0 + RSTEP * j;
+      ra[j] = (pv && m < a.M) ? a.dy[(long long)m * a.P + p] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < BPASS; ++j) {
+      const int n = n0 + r0 + RSTEP * j;
+      rb[j] = (vb && n < a.N) ? a.x[(long long)n * a.P + off] : 0.f;
+    }
+  };
+  auto sstore = [&](int buf) {
+    float* As = smem + buf * STAGE;
+    float* Bs = As + A_STAGE;
+#pragma unroll
+    for (int j = 0; j < APASS; ++j) As[kl * LDA_S + r0 + RSTEP * j] = ra[j];
+#pragma unroll
+    for (int j = 0; j < BPASS; ++j) Bs[kl * LDB_S + r0 + RSTEP * j] = rb[j];
+  };
+
+  if (s_begin < s_end) {
+    gload(s_begin);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int s = s_begin; s < s_end; ++s) {
+      const bool more = s + 1 < s_end;
+      if (more) gload(s + 1);
+      const float* As = smem + cur * STAGE;
+      mfma_stage<BK, TM, TN, LDA_S, LDB_S>(As, As + A_STAGE, wm, wn, lane, acc);
+      if (more) sstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  float* C = a.C + (long long)split * a.slab + (long long)br * a.cbranch;
+  const long long ldc = (long long)a.N * 9;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + j * 32 + (lane & 31);
+        if (m < a.M && n < a.N) {
+          const long long idx = (long long)m * ldc + (long long)n * 9 + t;
+          C[idx] = a.accumulate ? C[idx] + acc[i][j][r] : acc[i][j][r];
+        }
+      }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Forward form with an LDS-DMA ring (buffer_load ... lds): no register staging, STAGES-1 K-steps
+// in flight across raw barriers with counted vmcnt waits.  The dilated halo is zero-filled by
+// the buffer unit itself: a lane whose shifted pixel falls outside the image (or whose channel
+// is padding) gets an out-of-range offset, which loads 0.
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma_b32(__amdgpu_buffer_rsrc_t r, float* lds_row, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_row, 4, voff, 0, 0, 0);
+}
+__device__ __forceinline__ void dma_b128(__amdgpu_buffer_rsrc_t r, float* lds_row, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_row, 16, voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int STAGES, int WM, int WN>
+__global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
+  constexpr int BK = kCB;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  static_assert(BN % 64 == 0 && BM % 64 == 0, "tiles");
+  constexpr int A_STAGE = BK * BM, STAGE = A_STAGE + BK * BN;
+  // per wave and stage: A rows (16 B per lane: 64 lanes = 1024 floats = 1024/BM rows) + B rows
+  constexpr int A_ROWS_PER_INST = 256 / BM;                // rows of BM floats per dwordx4 instruction
+  constexpr int A_INST = BK / A_ROWS_PER_INST;             // per workgroup
+  constexpr int A_INST_W = (A_INST + 3) / 4;               // per wave
+  constexpr int B_INST = BK * (BN / 64);                   // per workgroup (one row-half each)
+  constexpr int B_INST_W = B_INST / 4;
+  constexpr int INST_W = A_INST_W + B_INST_W;
+  static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
+  __shared__ __attribute__((aligned(16))) float smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int split = blockIdx.z;
+  const int s_begin = split * a.kps;
+  const int s_end = min(a.ksteps, s_begin + a.kps);
+  const int nst = s_end - s_begin;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.A, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * BK * a.lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
+
+  // this lane's pixels: one per 64-wide half of the BN tile
+  constexpr int NH = BN / 64;
+  int py[NH], px[NH];
+  bool pin[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int p = n0 + h * 64 + lane;
+    pin[h] = p < a.P;
+    py[h] = p / a.W;
+    px[h] = p - py[h] * a.W;
+  }
+  const int per_b = a.ncb * 9;
+  constexpr unsigned OOB = 0x80000000u;
+
+  auto issue = [&](int s, int slot) {
+    float* As = smem + slot * STAGE;
+    float* Bs = As + A_STAGE;
+    const int b = s / per_b;
+    const int rem = s - b * per_b;
+    const int cb = rem / 9;
+    const int t = rem - cb * 9;
+    const int d = b ? a.dil1 : a.dil0;
+    const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
+    // A: wave wid loads instructions wid*A_INST_W .. ; each covers A_ROWS_PER_INST rows
+#pragma unroll
+    for (int i = 0; i < A_INST_W; ++i) {
+      const int inst = wid * A_INST_W + i;
+      const int row = inst * A_ROWS_PER_INST + lane / (BM / 4);
+      const int c4 = lane % (BM / 4);
+      const unsigned off = (unsigned)((((long long)s * BK + row) * a.lda + m0 + c4 * 4) * 4);
+      dma_b128(ra, As + inst * 256, off);  // 64 lanes x 16 B = 256 floats per instruction
+    }
+    // B: instruction j of this wave -> row r = (wid*B_INST_W + j) / NH, half h
+    const int cb16 = cb * kCB;
+#pragma unroll
+    for (int j = 0; j < B_INST_W; ++j) {
+      const int inst = wid * B_INST_W + j;
+      const int r = inst / NH, h = inst % NH;
+      const int ci = cb16 + r;
+      const bool v = pin[h] && ci < a.cimg && (unsigned)(py[h] + dh) < (unsigned)a.H &&
+                     (unsigned)(px[h] + dw) < (unsigned)a.W;
+      const long long e = (long long)ci * a.P + (n0 + h * 64 + lane) + dh * a.W + dw;
+      dma_b32(rb, Bs + r * BN + h * 64, v ? (unsigned)(e * 4) : OOB);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // prologue: STAGES-1 stages in flight
+#pragma unroll
+  for (int k = 0; k < STAGES - 1; ++k)
+    if (k < nst) issue(s_begin + k, k);
+  for (int i = 0; i < nst; ++i) {
+    // stage i must have landed: the younger in-flight stages may stay outstanding
+    const int younger = min(STAGES - 2, nst - 1 - i);
+    if (younger >= 2) wait_vmcnt<2 * INST_W>();
+    else if (younger == 1) wait_vmcnt<INST_W>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (i + STAGES - 1 < nst) issue(s_begin + i + STAGES - 1, (i + STAGES - 1) % STAGES);
+    const float* As = smem + (i % STAGES) * STAGE;
+    mfma_stage<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  float* C = a.C + (long long)split * a.slab;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + j * 32 + (lane & 31);
+        if (m < a.M && n < a.P) {
+          float v = acc[i][j][r];
+          if (a.bias) {
+            float bsum = a.bias[m];
+            for (int b = 1; b < a.nbias; ++b) bsum += a.bias[b * a.M + m];
+            v += bsum;
+          }
+          C[(long long)m * a.P + n] = v;
+        }
+      }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Stream-K forward form.  The (tile, K-step) iteration space of all output tiles is cut into NW
+// equal ranges, one per persistent workgroup (NW = CUs x resident workgroups per CU), so every
+// CU gets the same MFMA work whatever the tile count (65x129 maps give 132 or 264 tiles, which
+// split-K can only spread over 256 CUs unevenly).  A tile cut by range boundaries is finished by
+// its OWNER - the workgroup that computes its K-step 0, which is the last thing in the owner's
+// range - after the later pieces' workgroups (which did them first in their ranges) published
+// fp32 partials: plain stores, vmcnt(0), barrier, agent-scope release fence, relaxed agent
+// atomic add on the tile's counter; the owner polls the counter relaxed, then one agent-scope
+// acquire, then plain loads (MI355X_MICROARCH.md, inter-workgroup visibility).  All NW
+// workgroups are resident (NW <= capacity) and every spin is bounded.
+struct SkArgs {
+  float* part;     // [NW][kMaxSeg][BM*BN] partial accumulators (accumulator register order)
+  int* flags;      // [tiles] published-piece counters, zeroed before each launch
+  int* err;        // set to 1 if a spin timed out
+  int tiles_m, tiles_n, KS, NW;
+  int T;           // tiles * KS  (T * NW < 2^31, checked by the planner)
+};
+constexpr int kMaxSeg = 4;
+
+__device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
+__device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
+  return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
+}
+
+template <int BM, int BN, int STAGES, int WM, int WN>
+__global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
+  constexpr int BK = kCB;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  static_assert(BN % 64 == 0 && BM % 64 == 0, "tiles");
+  constexpr int A_STAGE = BK * BM, STAGE = A_STAGE + BK * BN;
+  constexpr int A_ROWS_PER_INST = 256 / BM;
+  constexpr int A_INST = BK / A_ROWS_PER_INST;
+  constexpr int A_INST_W = A_INST / 4;
+  constexpr int B_INST_W = BK * (BN / 64) / 4;
+  constexpr int INST_W = A_INST_W + B_INST_W;
+  constexpr int NH = BN / 64;
+  static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
+  __shared__ __attribute__((aligned(16))) float smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
+  // XCD-aware worker id: workgroups b, b+8, ... share an XCD and get consecutive ranges
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int w = (b % 8) * (nb / 8) + b / 8;
+  const int T = sk.T;
+  const int it_begin = sk_start(w, T, sk.NW), it_end = sk_start(w + 1, T, sk.NW);
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.A, (short)0, (int)min(0x7fffffffLL, (long long)sk.KS * BK * a.lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
+  const int per_b = a.ncb * 9;
+  constexpr unsigned OOB = 0x80000000u;
+
+  f32x16 acc[TM][TN];
+  int seg = 0;
+  for (int it = it_begin; it < it_end; ++seg) {
+    const int t = (unsigned)it / (unsigned)sk.KS;
+    const int k_a = it - t * sk.KS;
+    const int k_b = min(sk.KS, k_a + (it_end - it));
+    const int nst = k_b - k_a;
+    it += nst;
+    const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    int py[NH], px[NH];
+    bool pin[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int p = n0 + h * 64 + lane;
+      pin[h] = p < a.P;
+      py[h] = p / a.W;
+      px[h] = p - py[h] * a.W;
+    }
+    auto issue = [&](int s, int slot) {
+      float* As = smem + slot * STAGE;
+      float* Bs = As + A_STAGE;
+      const int br = s / per_b;
+      const int rem = s - br * per_b;
+      const int cb = rem / 9;
+      const int tp = rem - cb * 9;
+      const int d = br ? a.dil1 : a.dil0;
+      const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
+#pragma unroll
+      for (int i = 0; i < A_INST_W; ++i) {
+        const int inst = wid * A_INST_W + i;
+        const int row = inst * A_ROWS_PER_INST + lane / (BM / 4);
+        const int c4 = lane % (BM / 4);
+        const unsigned off = (unsigned)(((s * BK + row) * a.lda + m0 + c4 * 4) * 4);
+        dma_b128(ra, As + inst * 256, off);
+      }
+      const int cb16 = cb * kCB;
+      const int shift = dh * a.W + dw;
+#pragma unroll
+      for (int j = 0; j < B_INST_W; ++j) {
+        const int inst = wid * B_INST_W + j;
+        const int r = inst / NH, h = inst % NH;
+        const int ci = cb16 + r;
+        const bool v = pin[h] && ci < a.cimg && (unsigned)(py[h] + dh) < (unsigned)a.H &&
+                       (unsigned)(px[h] + dw) < (unsigned)a.W;
+        const unsigned e = (unsigned)(ci * a.P + (n0 + h * 64 + lane) + shift);
+        dma_b32(rb, Bs + r * BN + h * 64, v ? e * 4u : OOB);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    __builtin_amdgcn_s_barrier();  // the previous segment's LDS reads are complete in every wave
+#pragma unroll
+    for (int k = 0; k < STAGES - 1; ++k)
+      if (k < nst) issue(k_a + k, k);
+    for (int i = 0; i < nst; ++i) {
+      const int younger = min(STAGES - 2, nst - 1 - i);
+      if (younger >= 2) wait_vmcnt<2 * INST_W>();
+      else if (younger == 1) wait_vmcnt<INST_W>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (i + STAGES - 1 < nst) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
+      const float* As = smem + (i % STAGES) * STAGE;
+      mfma_stage<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    constexpr int PSZ = BM * BN;
+    if (k_a > 0) {
+      // contributor: publish this piece for the tile's owner
+      // lane-contiguous layout: [TM*TN][4 waves][64 lanes][16 floats] (4 x dwordx4 per lane)
+      float4* pp = reinterpret_cast<float4*>(sk.part + ((long long)w * kMaxSeg + seg) * PSZ) + (wid * 64 + lane) * 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            pp[(i * TN + j) * 1024 + q] = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1],
+                                                       acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(sk.flags + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    if (k_b < sk.KS) {
+      // owner of a split tile: wait for the later pieces, then add them in worker order
+      const int w_hi = sk_worker_of((t + 1) * sk.KS - 1, T, sk.NW);
+      const int expect = w_hi - w;
+      if (tid == 0) {
+        int n = 0;
+        for (unsigned spin = 0;; ++spin) {
+          n = __hip_atomic_load(sk.flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (n >= expect) break;
+          if (spin > (1u << 24)) {
+            __hip_atomic_store(sk.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+#pragma unroll 1
+      for (int wc = w + 1; wc <= w_hi; ++wc) {
+        const int first_it = sk_start(wc, T, sk.NW);
+        const int segc = t - (int)((unsigned)first_it / (unsigned)sk.KS);
+        const float4* pp = reinterpret_cast<const float4*>(sk.part + ((long long)wc * kMaxSeg + segc) * PSZ) +
+                           (wid * 64 + lane) * 4;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 v = pp[(i * TN + j) * 1024 + q];
+              acc[i][j][4 * q] += v.x;
+              acc[i][j][4 * q + 1] += v.y;
+              acc[i][j][4 * q + 2] += v.z;
+              acc[i][j][4 * q + 3] += v.w;
+            }
+      }
+    }
+    // owner (or sole worker of the tile): final output through a buffer resource - rows past M
+    // fall outside the descriptor and are dropped; columns past P get an out-of-range offset.
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn + j * 32 + (lane & 31);
+        const int mrow = m0 + wm + i * 32 + 4 * (lane >> 5);
+        const unsigned voff = n < a.P ? (unsigned)((mrow * a.P + n) * 4) : OOB;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int soff = ((r & 3) + 8 * (r >> 2)) * a.P * 4;
+          __builtin_amdgcn_raw_buffer_store_b32(acc[i][j][r], rc, voff, soff, 0);
+        }
+      }
+  }
+}
+
+}  // namespace msl

@@ -1,0 +1,186 @@
+// Standalone tuning harness for the dilated-conv implicit-GEMM kernels (not part of the library).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I maxsquareloss_amd/csrc scripts/tune_dconv.hip -o /tmp/tune
+// Times tile / depth / split variants at the layer3 (d=2) and layer4 (d=4) shapes in one process
+// and checks every variant against the first one.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "dconv_kernels.h"
+
+using namespace msl;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+__global__ void k_reduce(const float* ws, int S, long long n, float* out) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float v = ws[i];
+    for (int s = 1; s < S; ++s) v += ws[(long long)s * n + i];
+    out[i] = v;
+  }
+}
+
+static void fill(std::vector<float>& v, unsigned seed, float scale) {
+  unsigned s = seed;
+  for (auto& x : v) {
+    s = s * 1664525u + 1013904223u;
+    x = ((s >> 8) / 16777216.0f - 0.5f) * scale;
+  }
+}
+
+struct Shape { int cin, cout, h, w, dil; };
+
+template <int BM, int BN, int BK, int WM, int WN>
+float run_fwd(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int S, int iters, int lda) {
+  const int P = sh.h * sh.w;
+  FwdArgs a;
+  a.A = wp; a.B = x; a.C = S > 1 ? ws : y; a.bias = nullptr; a.nbias = 0;
+  a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
+  a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
+  const int groups = a.ncb * 9;
+  a.ksteps = groups / (BK / 16);
+  a.kps = (a.ksteps + S - 1) / S;
+  a.slab = (long long)sh.cout * P;
+  dim3 grid((P + BN - 1) / BN, (sh.cout + BM - 1) / BM, S);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_igemm_fwd<BM, BN, BK, WM, WN>), grid, dim3(256), 0, 0, a);
+    if (S > 1) hipLaunchKernelGGL(k_reduce, dim3(2048), dim3(256), 0, 0, (const float*)ws, S, a.slab, y);
+  }
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
+template <int BM, int BN, int STAGES, int WM, int WN>
+float run_fwd_dma(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int S, int iters, int lda) {
+  const int P = sh.h * sh.w;
+  FwdArgs a;
+  a.A = wp; a.B = x; a.C = S > 1 ? ws : y; a.bias = nullptr; a.nbias = 0;
+  a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
+  a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
+  a.ksteps = a.ncb * 9;
+  a.kps = (a.ksteps + S - 1) / S;
+  a.slab = (long long)sh.cout * P;
+  dim3 grid((P + BN - 1) / BN, (sh.cout + BM - 1) / BM, S);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_igemm_fwd_dma<BM, BN, STAGES, WM, WN>), grid, dim3(256), 0, 0, a);
+    if (S > 1) hipLaunchKernelGGL(k_reduce, dim3(2048), dim3(256), 0, 0, (const float*)ws, S, a.slab, y);
+  }
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
+template <int BM, int BN, int STAGES, int WM, int WN>
+float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda, int* flags) {
+  const int P = sh.h * sh.w;
+  FwdArgs a;
+  a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
+  a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
+  a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
+  a.ksteps = a.ncb * 9; a.kps = a.ksteps; a.slab = 0;
+  SkArgs sk;
+  sk.part = ws; sk.flags = flags + 64; sk.err = flags;
+  sk.tiles_m = (sh.cout + BM - 1) / BM; sk.tiles_n = (P + BN - 1) / BN; sk.KS = a.ksteps; sk.NW = NW;
+  sk.T = sk.tiles_m * sk.tiles_n * sk.KS;
+  const int tiles = sk.tiles_m * sk.tiles_n;
+  if (sk.T / NW > 2 * sk.KS) { printf("NW too small\n"); return 1e9f; }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipMemset(flags, 0, 256));
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) CK(hipEventRecord(e0));
+    CK(hipMemsetAsync(flags + 64, 0, tiles * 4, 0));
+    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, STAGES, WM, WN>), dim3(NW), dim3(256), 0, 0, a, sk);
+  }
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  int err; CK(hipMemcpy(&err, flags, 4, hipMemcpyDeviceToHost));
+  if (err) printf("SPIN TIMEOUT\n");
+  return ms / iters;
+}
+
+template <int BM, int BN, int BK, int WM, int WN>
+float run_wgrad(const Shape& sh, const float* x, const float* dy, float* dw, float* ws, int S, int iters) {
+  const int P = sh.h * sh.w;
+  WgradArgs a;
+  a.dy = dy; a.x = x; a.C = S > 1 ? ws : dw; a.M = sh.cout; a.N = sh.cin; a.H = sh.h; a.W = sh.w; a.P = P;
+  a.dil0 = sh.dil; a.dil1 = 0; a.ntap = 9; a.ksteps = (P + BK - 1) / BK; a.kps = (a.ksteps + S - 1) / S;
+  a.accumulate = 0; a.slab = (long long)sh.cout * sh.cin * 9; a.cbranch = a.slab;
+  dim3 grid((sh.cin + BN - 1) / BN, (sh.cout + BM - 1) / BM, S * 9);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_igemm_wgrad<BM, BN, BK, WM, WN>), grid, dim3(256), 0, 0, a);
+    if (S > 1) hipLaunchKernelGGL(k_reduce, dim3(2048), dim3(256), 0, 0, (const float*)ws, S, a.slab, dw);
+  }
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
+static double maxdiff(const float* a, const float* b, size_t n, double* scale) {
+  std::vector<float> ha(n), hb(n);
+  CK(hipMemcpy(ha.data(), a, n * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hb.data(), b, n * 4, hipMemcpyDeviceToHost));
+  double m = 0, s = 0;
+  for (size_t i = 0; i < n; ++i) { m = std::max(m, (double)std::fabs(ha[i] - hb[i])); s = std::max(s, (double)std::fabs(hb[i])); }
+  *scale = s;
+  return m;
+}
+
+int main(int argc, char** argv) {
+  const int iters = 20;
+  Shape shapes[] = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
+  for (const Shape& sh : shapes) {
+    const int P = sh.h * sh.w;
+    const int lda = (sh.cout + 127) / 128 * 128;
+    const long long kp = (long long)((sh.cin + 15) / 16) * 9 * 16;
+    std::vector<float> hx((size_t)sh.cin * P), hw((size_t)kp * lda), hdy((size_t)sh.cout * P);
+    fill(hx, 1, 2.f); fill(hw, 2, 0.02f); fill(hdy, 3, 2.f);
+    float *x, *wp, *dy, *y, *yref, *ws, *dw, *dwref;
+    int* flags; CK(hipMalloc(&flags, 1 << 20));
+    CK(hipMalloc(&x, hx.size() * 4)); CK(hipMalloc(&wp, hw.size() * 4)); CK(hipMalloc(&dy, hdy.size() * 4));
+    CK(hipMalloc(&y, (size_t)sh.cout * P * 4)); CK(hipMalloc(&yref, (size_t)sh.cout * P * 4));
+    CK(hipMalloc(&ws, std::max((size_t)16 * std::max((size_t)sh.cout * P, (size_t)sh.cout * sh.cin * 9) * 4, (size_t)1024 * 4 * 128 * 128 * 4)));
+    CK(hipMalloc(&dw, (size_t)sh.cout * sh.cin * 9 * 4)); CK(hipMalloc(&dwref, (size_t)sh.cout * sh.cin * 9 * 4));
+    CK(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(wp, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dy, hdy.data(), hdy.size() * 4, hipMemcpyHostToDevice));
+    const double gf = 2.0 * sh.cin * sh.cout * 9 * P / 1e9;
+    printf("=== shape cin %d cout %d %dx%d d=%d : %.2f GFLOP per conv\n", sh.cin, sh.cout, sh.h, sh.w, sh.dil, gf);
+    double sc;
+#define FWD(BM, BN, BK, WM, WN, S) { float ms = run_fwd<BM, BN, BK, WM, WN>(sh, x, wp, y, ws, S, iters, lda); \
+      double md = maxdiff(y, yref, (size_t)sh.cout * P, &sc); \
+      printf("fwd   BM %3d BN %3d BK %2d W %dx%d S %d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, BK, WM, WN, S, ms * 1e3, gf / ms, md, sc); }
+    run_fwd<64, 128, 16, 2, 2>(sh, x, wp, yref, ws, 1, 1, lda);
+    FWD(64, 128, 16, 2, 2, 1) FWD(64, 128, 16, 2, 2, 2)
+#define FDMA(BM, BN, ST, WM, WN, S) { float ms = run_fwd_dma<BM, BN, ST, WM, WN>(sh, x, wp, y, ws, S, iters, lda); \
+      double md = maxdiff(y, yref, (size_t)sh.cout * P, &sc); \
+      printf("fdma  BM %3d BN %3d ST %2d W %dx%d S %d grid %5d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, ST, WM, WN, S, \
+             ((P + BN - 1) / BN) * ((sh.cout + BM - 1) / BM) * S, ms * 1e3, gf / ms, md, sc); }
+#define FSK(BM, BN, ST, WM, WN, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); float ms = run_fwd_sk<BM, BN, ST, WM, WN>(sh, x, wp, y, ws, NW, iters, lda, flags); \
+      double md = maxdiff(y, yref, (size_t)sh.cout * P, &sc); \
+      printf("fsk   BM %3d BN %3d ST %2d W %dx%d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, ST, WM, WN, NW, ms * 1e3, gf / ms, md, sc); }
+    FSK(128, 128, 3, 2, 2, 256) FSK(128, 128, 3, 2, 2, 512) FSK(128, 128, 3, 2, 2, 768)
+    FSK(64, 128, 3, 2, 2, 512) FSK(64, 128, 3, 2, 2, 768) FSK(64, 128, 3, 2, 2, 1024)
+    FDMA(128, 128, 3, 2, 2, 1) FDMA(128, 128, 3, 2, 2, 2) FDMA(128, 128, 3, 2, 2, 3) FDMA(128, 128, 3, 2, 2, 4)
+    FDMA(128, 128, 3, 2, 2, 6) FDMA(128, 128, 3, 2, 2, 8)
+    FDMA(64, 128, 3, 2, 2, 1) FDMA(64, 128, 3, 2, 2, 2) FDMA(64, 128, 3, 2, 2, 3) FDMA(64, 128, 3, 2, 2, 4)
+    FDMA(64, 64, 3, 2, 2, 1) FDMA(64, 64, 3, 2, 2, 2) FDMA(64, 64, 3, 2, 2, 3)
+#define WGR(BM, BN, BK, WM, WN, S) { float ms = run_wgrad<BM, BN, BK, WM, WN>(sh, x, dy, dw, ws, S, iters); \
+      double md = maxdiff(dw, dwref, (size_t)sh.cout * sh.cin * 9, &sc); \
+      printf("wgrad BM %3d BN %3d BK %2d W %dx%d S %2d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, BK, WM, WN, S, ms * 1e3, gf / ms, md, sc); }
+    run_wgrad<64, 128, 32, 2, 2>(sh, x, dy, dwref, ws, 1, 1);
+    WGR(64, 128, 32, 2, 2, 8)
+    CK(hipFree(x)); CK(hipFree(wp)); CK(hipFree(dy)); CK(hipFree(y)); CK(hipFree(yref)); CK(hipFree(ws)); CK(hipFree(dw)); CK(hipFree(dwref));
+  }
+  return 0;
+}
