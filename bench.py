@@ -129,7 +129,7 @@ def main():
             traffic = None
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                "kernel": "dconv3x3 fwd layer3 d=2 (k_igemm_fwd + split-K reduce)",
+                "kernel": "dconv3x3 fwd layer3 d=2 (k_igemm_fwd_sk, stream-K)",
                 "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
 

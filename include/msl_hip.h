@@ -40,6 +40,12 @@ typedef void* msl_stream_t; /* a hipStream_t */
 int msl_abi_version(void);
 const char* msl_status_string(int status);
 
+/* Length (ints) of the arrival-counter array the conv forward / data-gradient calls take.
+ * The caller allocates it once per stream, zero-fills it once, and passes it to every call:
+ * each call finds it zero and leaves it zero (the stream-K kernel re-arms what it uses).
+ * Calls that may run concurrently need separate arrays. */
+int msl_counter_elems(void);
+
 /* ------------------------------------------------------------------------
  * Dilated 3x3 convolution, stride 1, padding = dilation, as an FP32-MFMA
  * implicit GEMM.  One call covers either a single conv (nbranch = 1:
@@ -59,14 +65,14 @@ int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin
  * replaces nn.Conv2d.forward at deeplab_multi.py:35 (layer3/4) and :63-65 (ASPP). */
 size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w);
 int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                  int cin, int cout, int h, int w, int dil0, int dil1, void* ws, size_t ws_bytes,
-                  msl_stream_t stream);
+                  int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                  size_t ws_bytes, msl_stream_t stream);
 
 /* dx[cin][h][w] = sum_b conv3x3^T(dy, W_b, dil_b)   (autograd of the same sites) */
 size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w);
 int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, void* ws, size_t ws_bytes,
-                    msl_stream_t stream);
+                    int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                    size_t ws_bytes, msl_stream_t stream);
 
 /* dw[b][cout][cin][3][3] (= or += when accumulate) and, if dbias != NULL,
  * dbias[b][cout] = sum_px dy (identical for both branches). */
@@ -74,6 +80,33 @@ size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w);
 int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
                     int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
                     size_t ws_bytes, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Pointwise (1x1, stride 1, no bias) convolution: the same FP32-MFMA GEMM
+ * kernels with one unshifted tap over the flat pixel axis p = h*w.  Replaces
+ * Bottleneck.conv1 / conv3 (deeplab_multi.py:13, 20) and the downsample conv
+ * (deeplab_multi.py:96-99)
+ * wherever their stride is 1 (layer1, layer3, layer4 and layer2 blocks 2-4).
+ * Weights [cout][cin] (= [cout][cin][1][1]).
+ * ---------------------------------------------------------------------- */
+long long msl_pconv_packed_elems(int cin, int cout, int for_dgrad);
+int msl_pconv_pack(const float* w, int cin, int cout, int for_dgrad, float* packed,
+                   msl_stream_t stream);
+
+/* y[cout][p] = sum_ci W[cout][ci] x[ci][p] */
+size_t msl_pconv_fwd_workspace(int cin, int cout, int p);
+int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
+                  int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+
+/* dx[cin][p] = sum_co W[co][cin] dy[co][p] */
+size_t msl_pconv_dgrad_workspace(int cin, int cout, int p);
+int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                    int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+
+/* dw[cout][cin] (= or += when accumulate) = sum_p dy[cout][p] x[cin][p] */
+size_t msl_pconv_wgrad_workspace(int cin, int cout, int p);
+int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,
+                    int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Bilinear upsample, align_corners=True (F.interpolate at deeplab_multi.py:124,

@@ -63,10 +63,11 @@ __global__ void __launch_bounds__(256) k_bias_grad(const float* __restrict__ dy,
 // Packed operand for the forward-form GEMM.
 //   for_dgrad = 0: image = x (cin channels),  m = co: P[k][co] = W[co][ci][t]
 //   for_dgrad = 1: image = dy (cout channels), m = ci: P[k][ci] = W[co][ci][8 - t]
-// k = ((b*ncb + cb)*9 + t)*16 + c_local with c = cb*16 + c_local (image channel).
+// k = ((b*ncb + cb)*taps + t)*16 + c_local with c = cb*16 + c_local (image channel); taps = 9
+// for the 3x3 convs, 1 for the pointwise ones.
 __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long long branch_stride,
                                                int cin, int cout, int for_dgrad, int ncb, int lda,
-                                               long long total, float* __restrict__ out) {
+                                               int taps, long long total, float* __restrict__ out) {
   const int cimg = for_dgrad ? cout : cin;
   const int mreal = for_dgrad ? cin : cout;
   for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
@@ -74,8 +75,8 @@ __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long 
     const long long k = e / lda;
     const int cl = (int)(k % kCB);
     const long long q = k / kCB;
-    const int t = (int)(q % 9);
-    const long long q2 = q / 9;
+    const int t = (int)(q % taps);
+    const long long q2 = q / taps;
     const int cb = (int)(q2 % ncb);
     const int b = (int)(q2 / ncb);
     const int c = cb * kCB + cl;
@@ -83,16 +84,25 @@ __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long 
     if (c < cimg && m < mreal) {
       const float* wb = w + (long long)b * branch_stride;
       if (!for_dgrad)
-        v = wb[((long long)m * cin + c) * 9 + t];
+        v = wb[((long long)m * cin + c) * taps + t];
       else
-        v = wb[((long long)c * cin + m) * 9 + (8 - t)];
+        v = wb[((long long)c * cin + m) * taps + (taps - 1 - t)];
     }
     out[e] = v;
   }
 }
 
 // ---------------------------------------------------------------- planning
+// Forward form (fwd and dgrad).  Unbiased GEMMs with M >= 128 run stream-K (k_igemm_fwd_sk,
+// 128x128 tiles, two K-steps per LDS stage, 512 persistent workgroups = 2 per CU): every CU
+// gets the same number of MFMA stages whatever the tile count.  The ASPP forward (M = 19
+// classes, bias) keeps the split-K tile kernel with 64-row tiles.
+constexpr int kSkBM = 128, kSkBN = 128, kSkNW = 512;
+constexpr int kMaxCounters = 65536;  // stream-K arrival counters (one per output tile)
+
 struct FwdPlan {
+  bool sk;
+  int G;  // stream-K: K-steps per stage
   int bm, bn, bk, tiles_m, tiles_n, ksteps, kps, S;
 };
 
@@ -106,15 +116,29 @@ static int choose_split(int tiles, int ksteps, int min_steps) {
   return S;
 }
 
-static FwdPlan plan_fwd(int nbranch, int cimg, int M, int P) {
+static FwdPlan plan_fwd(int nbranch, int taps, int cimg, int M, int P, bool has_bias) {
   FwdPlan pl;
+  const int groups = nbranch * cdiv(cimg, kCB) * taps;
+  pl.sk = M >= kSkBM && !has_bias;
+  if (pl.sk) {
+    pl.G = groups % 2 == 0 ? 2 : 1;
+    pl.bm = kSkBM;
+    pl.bn = kSkBN;
+    pl.bk = pl.G * kCB;
+    pl.tiles_m = cdiv(M, pl.bm);
+    pl.tiles_n = cdiv(P, pl.bn);
+    pl.ksteps = groups;
+    pl.kps = groups / pl.G;  // stages per tile
+    pl.S = 1;
+    return pl;
+  }
+  pl.G = 1;
   pl.bm = 64;
   pl.bn = 128;
-  const int groups = nbranch * cdiv(cimg, kCB) * 9;
-  pl.bk = groups % 2 == 0 ? 32 : 16;
+  pl.bk = 16;
   pl.tiles_m = cdiv(M, pl.bm);
   pl.tiles_n = cdiv(P, pl.bn);
-  pl.ksteps = groups / (pl.bk / kCB);
+  pl.ksteps = groups;
   int S = choose_split(pl.tiles_m * pl.tiles_n, pl.ksteps, 4);
   pl.kps = cdiv(pl.ksteps, S);
   pl.S = cdiv(pl.ksteps, pl.kps);
@@ -125,14 +149,14 @@ struct WgradPlan {
   int bm, bn, bk, tiles_m, tiles_n, ntap, ksteps, kps, S;
 };
 
-static WgradPlan plan_wgrad(int nbranch, int cin, int cout, int P) {
+static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P) {
   WgradPlan pl;
   pl.bm = 64;
   pl.bn = 128;
   pl.bk = 32;
   pl.tiles_m = cdiv(cout, pl.bm);
   pl.tiles_n = cdiv(cin, pl.bn);
-  pl.ntap = nbranch * 9;
+  pl.ntap = nbranch * taps;
   pl.ksteps = cdiv(P, pl.bk);
   int S = choose_split(pl.tiles_m * pl.tiles_n * pl.ntap, pl.ksteps, 8);
   pl.kps = cdiv(pl.ksteps, S);
@@ -140,15 +164,19 @@ static WgradPlan plan_wgrad(int nbranch, int cin, int cout, int P) {
   return pl;
 }
 
+// stream-K workspace: the published pieces, NW x 2 x BM*BN floats.  The arrival counters live in
+// a caller-owned, persistent int[kMaxCounters] that is zero on entry and left zero on exit (the
+// finishing workgroup of each tile re-arms its counter), so no per-call memset is needed.
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
+  if (pl.sk) return (size_t)kSkNW * 2 * kSkBM * kSkBN * sizeof(float);
   return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
 }
 
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
-                           int nbias, float* out, int nbranch, int h, int w, int dil0, int dil1,
-                           void* ws, size_t ws_bytes, hipStream_t st) {
+                           int nbias, float* out, int nbranch, int taps, int h, int w, int dil0,
+                           int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st) {
   const int P = h * w;
-  FwdPlan pl = plan_fwd(nbranch, cimg, M, P);
+  FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
   if (ws_bytes < fwd_ws_bytes(pl, M, P)) return MSL_ERR_WORKSPACE;
   FwdArgs a;
   a.A = packed;
@@ -167,12 +195,34 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   a.dil1 = dil1;
   a.ksteps = pl.ksteps;
   a.kps = pl.kps;
+  a.taps = taps;
   a.slab = (long long)M * P;
+  if (pl.sk) {
+    if (!counters) return MSL_ERR_ARG;
+    if ((long long)pl.tiles_m * pl.tiles_n > kMaxCounters) return MSL_ERR_SHAPE;
+    SkArgs sk;
+    sk.flags = counters;
+    sk.part = (float*)ws;
+    sk.tiles_m = pl.tiles_m;
+    sk.tiles_n = pl.tiles_n;
+    sk.KS = pl.kps;
+    const long long T = (long long)pl.tiles_m * pl.tiles_n * sk.KS;
+    // every workgroup must own at least one iteration: the piece count of a tile is the number
+    // of workgroups its iteration range touches
+    sk.NW = (int)std::min<long long>(kSkNW, T);
+    if (T * kSkNW >= (1LL << 31) || (long long)cimg * P >= (1LL << 29) ||
+        (long long)pl.ksteps * kCB * a.lda >= (1LL << 29))
+      return MSL_ERR_SHAPE;  // 32-bit index arithmetic in the kernel
+    sk.T = (int)T;
+    if (pl.G == 2)
+      hipLaunchKernelGGL((k_igemm_fwd_sk<kSkBM, kSkBN, 2, 2, 2, 2>), dim3(sk.NW), dim3(256), 0, st, a, sk);
+    else
+      hipLaunchKernelGGL((k_igemm_fwd_sk<kSkBM, kSkBN, 1, 3, 2, 2>), dim3(sk.NW), dim3(256), 0, st, a, sk);
+    MSL_CHECK_LAUNCH();
+    return MSL_OK;
+  }
   dim3 grid(pl.tiles_n, pl.tiles_m, pl.S);
-  if (pl.bk == 32)
-    hipLaunchKernelGGL((k_igemm_fwd<64, 128, 32, 2, 2>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_igemm_fwd<64, 128, 16, 2, 2>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((k_igemm_fwd<64, 128, 16, 2, 2>), grid, dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
   if (pl.S > 1) {
     const long long n = (long long)M * P;
@@ -189,91 +239,36 @@ static bool bad_dims(int nbranch, int cin, int cout, int h, int w) {
          (long long)h * w > (1LL << 30);
 }
 
-}  // namespace msl
-
-using namespace msl;
-
-extern "C" {
-
-int msl_abi_version(void) { return MSL_ABI_VERSION; }
-
-const char* msl_status_string(int status) {
-  switch (status) {
-    case MSL_OK: return "ok";
-    case MSL_ERR_SHAPE: return "invalid shape";
-    case MSL_ERR_WORKSPACE: return "workspace too small";
-    case MSL_ERR_ARG: return "invalid argument";
-    default: return status > 0 ? hipGetErrorString((hipError_t)status) : "unknown error";
-  }
-}
-
-long long msl_dconv_packed_elems(int nbranch, int cin, int cout, int for_dgrad) {
+// ---------------------------------------------------------------- shared by 3x3 and pointwise
+static long long packed_elems(int nbranch, int taps, int cin, int cout, int for_dgrad) {
   const int cimg = for_dgrad ? cout : cin;
   const int m = for_dgrad ? cin : cout;
-  return (long long)nbranch * cdiv(cimg, kCB) * 9 * kCB * pad_to(m, kPackPad);
+  return (long long)nbranch * cdiv(cimg, kCB) * taps * kCB * pad_to(m, kPackPad);
 }
 
-int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin, int cout,
-                   int for_dgrad, float* packed, msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, 1, 1) || !w || !packed) return MSL_ERR_ARG;
+static int pack(const float* w, long long branch_stride, int nbranch, int taps, int cin, int cout,
+                int for_dgrad, float* packed, hipStream_t st) {
   const int cimg = for_dgrad ? cout : cin;
   const int m = for_dgrad ? cin : cout;
-  const long long total = msl_dconv_packed_elems(nbranch, cin, cout, for_dgrad);
+  const long long total = packed_elems(nbranch, taps, cin, cout, for_dgrad);
   const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
-  hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, as_stream(stream), w, branch_stride, cin,
-                     cout, for_dgrad, cdiv(cimg, kCB), pad_to(m, kPackPad), total, packed);
+  hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
+                     cdiv(cimg, kCB), pad_to(m, kPackPad), taps, total, packed);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
 
-size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w) {
-  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
-  FwdPlan pl = plan_fwd(nbranch, cin, cout, h * w);
-  return fwd_ws_bytes(pl, cout, h * w);
+static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P) {
+  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P);
+  return pl.S > 1 ? (size_t)pl.S * nbranch * cout * cin * taps * sizeof(float) : 0;
 }
 
-int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                  int cin, int cout, int h, int w, int dil0, int dil1, void* ws, size_t ws_bytes,
-                  msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
-      (nbranch == 2 && dil1 < 1))
-    return MSL_ERR_ARG;
-  return launch_fwd_form(x, cin, packed, cout, bias, nbranch, y, nbranch, h, w, dil0, dil1, ws,
-                         ws_bytes, as_stream(stream));
-}
-
-size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
-  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
-  FwdPlan pl = plan_fwd(nbranch, cout, cin, h * w);
-  return fwd_ws_bytes(pl, cin, h * w);
-}
-
-int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, void* ws, size_t ws_bytes,
-                    msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
-      (nbranch == 2 && dil1 < 1))
-    return MSL_ERR_ARG;
-  return launch_fwd_form(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, h, w, dil0, dil1,
-                         ws, ws_bytes, as_stream(stream));
-}
-
-size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
-  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
-  WgradPlan pl = plan_wgrad(nbranch, cin, cout, h * w);
-  return pl.S > 1 ? (size_t)pl.S * nbranch * cout * cin * 9 * sizeof(float) : 0;
-}
-
-int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
-                    size_t ws_bytes, msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
-      (nbranch == 2 && dil1 < 1))
-    return MSL_ERR_ARG;
-  hipStream_t st = as_stream(stream);
+static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
+                        int taps, int cin, int cout, int h, int w, int dil0, int dil1,
+                        int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
   const int P = h * w;
-  WgradPlan pl = plan_wgrad(nbranch, cin, cout, P);
-  const long long nout = (long long)nbranch * cout * cin * 9;
+  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P);
+  const long long nout = (long long)nbranch * cout * cin * taps;
   if (pl.S > 1 && ws_bytes < (size_t)pl.S * nout * sizeof(float)) return MSL_ERR_WORKSPACE;
   WgradArgs a;
   a.dy = dy;
@@ -290,8 +285,9 @@ int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, in
   a.ksteps = pl.ksteps;
   a.kps = pl.kps;
   a.accumulate = pl.S > 1 ? 0 : accumulate;
+  a.taps = taps;
   a.slab = nout;
-  a.cbranch = (long long)cout * cin * 9;
+  a.cbranch = (long long)cout * cin * taps;
   dim3 grid(pl.tiles_n, pl.tiles_m, pl.S * pl.ntap);
   hipLaunchKernelGGL((k_igemm_wgrad<64, 128, 32, 2, 2>), grid, dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
@@ -307,6 +303,132 @@ int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, in
     MSL_CHECK_LAUNCH();
   }
   return MSL_OK;
+}
+
+}  // namespace msl
+
+using namespace msl;
+
+extern "C" {
+
+int msl_abi_version(void) { return MSL_ABI_VERSION; }
+
+int msl_counter_elems(void) { return kMaxCounters; }
+
+const char* msl_status_string(int status) {
+  switch (status) {
+    case MSL_OK: return "ok";
+    case MSL_ERR_SHAPE: return "invalid shape";
+    case MSL_ERR_WORKSPACE: return "workspace too small";
+    case MSL_ERR_ARG: return "invalid argument";
+    default: return status > 0 ? hipGetErrorString((hipError_t)status) : "unknown error";
+  }
+}
+
+// ------------------------------------------------------------------ dilated 3x3
+long long msl_dconv_packed_elems(int nbranch, int cin, int cout, int for_dgrad) {
+  return packed_elems(nbranch, 9, cin, cout, for_dgrad);
+}
+
+int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin, int cout,
+                   int for_dgrad, float* packed, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, 1, 1) || !w || !packed) return MSL_ERR_ARG;
+  return pack(w, branch_stride, nbranch, 9, cin, cout, for_dgrad, packed, as_stream(stream));
+}
+
+size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w) {
+  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
+  // large enough with or without a bias (the plan depends on it)
+  return std::max(fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, h * w, false), cout, h * w),
+                  fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, h * w, true), cout, h * w));
+}
+
+int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
+                  int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                  size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_fwd_form(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
+                         counters, ws, ws_bytes, as_stream(stream));
+}
+
+size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
+  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
+  return fwd_ws_bytes(plan_fwd(nbranch, 9, cout, cin, h * w, false), cin, h * w);
+}
+
+int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
+                    int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                    size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_fwd_form(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+                         counters, ws, ws_bytes, as_stream(stream));
+}
+
+size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
+  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
+  return wgrad_ws_bytes(nbranch, 9, cin, cout, h * w);
+}
+
+int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
+                    int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                    size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_wgrad(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
+                      ws_bytes, as_stream(stream));
+}
+
+// ------------------------------------------------------------------ pointwise (1x1, stride 1)
+// A pointwise conv is the same GEMM with one unshifted tap (dilation 0) over the flat pixel axis.
+long long msl_pconv_packed_elems(int cin, int cout, int for_dgrad) {
+  return packed_elems(1, 1, cin, cout, for_dgrad);
+}
+
+int msl_pconv_pack(const float* w, int cin, int cout, int for_dgrad, float* packed,
+                   msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, 1) || !w || !packed) return MSL_ERR_ARG;
+  return pack(w, 0, 1, 1, cin, cout, for_dgrad, packed, as_stream(stream));
+}
+
+size_t msl_pconv_fwd_workspace(int cin, int cout, int p) {
+  if (bad_dims(1, cin, cout, 1, p)) return 0;
+  return fwd_ws_bytes(plan_fwd(1, 1, cin, cout, p, false), cout, p);
+}
+
+int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
+                  int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
+  return launch_fwd_form(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
+                         ws_bytes, as_stream(stream));
+}
+
+size_t msl_pconv_dgrad_workspace(int cin, int cout, int p) {
+  if (bad_dims(1, cin, cout, 1, p)) return 0;
+  return fwd_ws_bytes(plan_fwd(1, 1, cout, cin, p, false), cin, p);
+}
+
+int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                    int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
+  return launch_fwd_form(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
+                         ws, ws_bytes, as_stream(stream));
+}
+
+size_t msl_pconv_wgrad_workspace(int cin, int cout, int p) {
+  if (bad_dims(1, cin, cout, 1, p)) return 0;
+  return wgrad_ws_bytes(1, 1, cin, cout, p);
+}
+
+int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,
+                    int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
+  return launch_wgrad(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+                      as_stream(stream));
 }
 
 }  // extern "C"

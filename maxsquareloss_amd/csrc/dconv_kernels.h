@@ -17,14 +17,16 @@ struct FwdArgs {
   const float* bias;  // [nbias][M] or null (only used when S == 1)
   int nbias;
   int M, lda, H, W, P, cimg, ncb, dil0, dil1, ksteps, kps;  // ksteps counts BK-deep steps
+  int taps;           // 9 (3x3) or 1 (pointwise: dil0 = 0, so the single tap has no shift)
   long long slab;
 };
 
 struct WgradArgs {
   const float* dy;  // [M][P]
   const float* x;   // [N][P]
-  float* C;         // dW [nbranch][M][N][9] or slabs of that
+  float* C;         // dW [nbranch][M][N][taps] or slabs of that
   int M, N, H, W, P, dil0, dil1, ntap, ksteps, kps, accumulate;
+  int taps;         // taps per branch: 9, or 1 for a pointwise conv (dil0 = 0)
   long long slab, cbranch;
 };
 
@@ -93,15 +95,15 @@ __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int per_b = a.ncb * 9;
+  const int per_b = a.ncb * a.taps;
   auto gload = [&](int s) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int q = s * G + g;  // tap-group index
       const int b = q / per_b;
       const int rem = q - b * per_b;
-      const int cb = rem / 9;
-      const int t = rem - cb * 9;
+      const int cb = rem / a.taps;
+      const int t = rem - cb * a.taps;
       const int d = b ? a.dil1 : a.dil0;
       const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
       const bool v = pin && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
@@ -192,7 +194,7 @@ __global__ void __launch_bounds__(256) k_igemm_wgrad(WgradArgs a) {
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int tapz = blockIdx.z % a.ntap;
   const int split = blockIdx.z / a.ntap;
-  const int br = tapz / 9, t = tapz - br * 9;
+  const int br = tapz / a.taps, t = tapz - br * a.taps;
   const int d = br ? a.dil1 : a.dil0;
   const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
   const int s_begin = split * a.kps;
@@ -253,7 +255,7 @@ __global__ void __launch_bounds__(256) k_igemm_wgrad(WgradArgs a) {
   }
 
   float* C = a.C + (long long)split * a.slab + (long long)br * a.cbranch;
-  const long long ldc = (long long)a.N * 9;
+  const long long ldc = (long long)a.N * a.taps;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -263,7 +265,7 @@ __global__ void __launch_bounds__(256) k_igemm_wgrad(WgradArgs a) {
         const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int n = n0 + wn + j * 32 + (lane & 31);
         if (m < a.M && n < a.N) {
-          const long long idx = (long long)m * ldc + (long long)n * 9 + t;
+          const long long idx = (long long)m * ldc + (long long)n * a.taps + t;
           C[idx] = a.accumulate ? C[idx] + acc[i][j][r] : acc[i][j][r];
         }
       }
@@ -331,7 +333,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
     py[h] = p / a.W;
     px[h] = p - py[h] * a.W;
   }
-  const int per_b = a.ncb * 9;
+  const int per_b = a.ncb * a.taps;
   constexpr unsigned OOB = 0x80000000u;
 
   auto issue = [&](int s, int slot) {
@@ -339,8 +341,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
     float* Bs = As + A_STAGE;
     const int b = s / per_b;
     const int rem = s - b * per_b;
-    const int cb = rem / 9;
-    const int t = rem - cb * 9;
+    const int cb = rem / a.taps;
+    const int t = rem - cb * a.taps;
     const int d = b ? a.dil1 : a.dil0;
     const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
     // A: wave wid loads instructions wid*A_INST_W .. ; each covers A_ROWS_PER_INST rows
@@ -414,33 +416,34 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
 
 
 // ---------------------------------------------------------------------------------------------
-// Stream-K forward form.  The (tile, K-step) iteration space of all output tiles is cut into NW
+// Stream-K forward form.  The (tile, stage) iteration space of all output tiles is cut into NW
 // equal ranges, one per persistent workgroup (NW = CUs x resident workgroups per CU), so every
 // CU gets the same MFMA work whatever the tile count (65x129 maps give 132 or 264 tiles, which
 // split-K can only spread over 256 CUs unevenly).  A tile cut by range boundaries is finished by
-// its OWNER - the workgroup that computes its K-step 0, which is the last thing in the owner's
-// range - after the later pieces' workgroups (which did them first in their ranges) published
-// fp32 partials: plain stores, vmcnt(0), barrier, agent-scope release fence, relaxed agent
-// atomic add on the tile's counter; the owner polls the counter relaxed, then one agent-scope
-// acquire, then plain loads (MI355X_MICROARCH.md, inter-workgroup visibility).  All NW
-// workgroups are resident (NW <= capacity) and every spin is bounded.
+// whichever of its workgroups arrives LAST: every piece is published (plain stores, vmcnt(0),
+// barrier, agent-scope release fence, then an agent-scope fetch_add on the tile's counter); the
+// workgroup that sees count == pieces-1 does an agent-scope acquire and sums all pieces in worker
+// order (MI355X_MICROARCH.md, inter-workgroup visibility).  Nothing ever waits on another
+// workgroup, so the kernel needs no co-residency and no dispatch-order assumption, and the sum
+// order - hence the result - does not depend on which workgroup came last.
 struct SkArgs {
-  float* part;     // [NW][kMaxSeg][BM*BN] partial accumulators (accumulator register order)
-  int* flags;      // [tiles] published-piece counters, zeroed before each launch
-  int* err;        // set to 1 if a spin timed out
+  float* part;     // [NW][2][BM*BN] published pieces (accumulator register order, lane-contiguous)
+  int* flags;      // [tiles] arrival counters, zero at launch; the finishing workgroup re-arms them
   int tiles_m, tiles_n, KS, NW;
   int T;           // tiles * KS  (T * NW < 2^31, checked by the planner)
 };
-constexpr int kMaxSeg = 4;
 
 __device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
 __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
   return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
 }
 
-template <int BM, int BN, int STAGES, int WM, int WN>
+template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false>
 __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
-  constexpr int BK = kCB;
+  // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
+  // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
+  // is 128 contiguous pixels and moves as dwordx4 (4 pixels per lane) instead of dwords.
+  constexpr int BK = G * kCB;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   static_assert(BN % 64 == 0 && BM % 64 == 0, "tiles");
@@ -448,10 +451,12 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   constexpr int A_ROWS_PER_INST = 256 / BM;
   constexpr int A_INST = BK / A_ROWS_PER_INST;
   constexpr int A_INST_W = A_INST / 4;
-  constexpr int B_INST_W = BK * (BN / 64) / 4;
-  constexpr int INST_W = A_INST_W + B_INST_W;
   constexpr int NH = BN / 64;
+  constexpr int BG_INST_W = PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B instructions per wave per K-step
+  static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
+  constexpr int INST_W = A_INST_W + G * BG_INST_W;
   static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
+  static_assert((STAGES - 2) * INST_W < 64, "vmcnt range");
   __shared__ __attribute__((aligned(16))) float smem[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -459,7 +464,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
   // XCD-aware worker id: workgroups b, b+8, ... share an XCD and get consecutive ranges
   const int nb = gridDim.x, b = blockIdx.x;
-  const int w = (b % 8) * (nb / 8) + b / 8;
+  const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);  // a bijection for any nb
   const int T = sk.T;
   const int it_begin = sk_start(w, T, sk.NW), it_end = sk_start(w + 1, T, sk.NW);
 
@@ -467,12 +472,11 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       (void*)a.A, (short)0, (int)min(0x7fffffffLL, (long long)sk.KS * BK * a.lda * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
-  const int per_b = a.ncb * 9;
+  const int per_b = a.ncb * a.taps;
   constexpr unsigned OOB = 0x80000000u;
 
   f32x16 acc[TM][TN];
-  int seg = 0;
-  for (int it = it_begin; it < it_end; ++seg) {
+  for (int it = it_begin; it < it_end;) {
     const int t = (unsigned)it / (unsigned)sk.KS;
     const int k_a = it - t * sk.KS;
     const int k_b = min(sk.KS, k_a + (it_end - it));
@@ -492,12 +496,6 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
     auto issue = [&](int s, int slot) {
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
-      const int br = s / per_b;
-      const int rem = s - br * per_b;
-      const int cb = rem / 9;
-      const int tp = rem - cb * 9;
-      const int d = br ? a.dil1 : a.dil0;
-      const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
 #pragma unroll
       for (int i = 0; i < A_INST_W; ++i) {
         const int inst = wid * A_INST_W + i;
@@ -506,17 +504,42 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
         const unsigned off = (unsigned)(((s * BK + row) * a.lda + m0 + c4 * 4) * 4);
         dma_b128(ra, As + inst * 256, off);
       }
-      const int cb16 = cb * kCB;
-      const int shift = dh * a.W + dw;
 #pragma unroll
-      for (int j = 0; j < B_INST_W; ++j) {
-        const int inst = wid * B_INST_W + j;
-        const int r = inst / NH, h = inst % NH;
-        const int ci = cb16 + r;
-        const bool v = pin[h] && ci < a.cimg && (unsigned)(py[h] + dh) < (unsigned)a.H &&
-                       (unsigned)(px[h] + dw) < (unsigned)a.W;
-        const unsigned e = (unsigned)(ci * a.P + (n0 + h * 64 + lane) + shift);
-        dma_b32(rb, Bs + r * BN + h * 64, v ? e * 4u : OOB);
+      for (int g = 0; g < G; ++g) {
+        const int ks = s * G + g;
+        const int br = ks / per_b;
+        const int rem = ks - br * per_b;
+        const int cb = rem / a.taps;
+        const int tp = rem - cb * a.taps;
+        const int d = br ? a.dil1 : a.dil0;
+        const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
+        const int cb16 = cb * kCB;
+        if constexpr (PW) {
+          // lanes 0-31 -> row 2*inst, lanes 32-63 -> row 2*inst+1; 4 pixels per lane.  A chunk
+          // that straddles P reads the next channel's first pixels: they only reach output
+          // columns >= P, which are never stored.
+          const int c4 = (lane & 31) * 4;
+#pragma unroll
+          for (int j = 0; j < BG_INST_W; ++j) {
+            const int inst = wid * BG_INST_W + j;
+            const int ci = cb16 + inst * 2 + (lane >> 5);
+            const bool v = ci < a.cimg && n0 + c4 < a.P;
+            const unsigned e = (unsigned)(ci * a.P + n0 + c4);
+            dma_b128(rb, Bs + (g * kCB + inst * 2) * BN, v ? e * 4u : OOB);
+          }
+        } else {
+          const int shift = dh * a.W + dw;
+#pragma unroll
+          for (int j = 0; j < BG_INST_W; ++j) {
+            const int inst = wid * BG_INST_W + j;
+            const int r = inst / NH, h = inst % NH;
+            const int ci = cb16 + r;
+            const bool v = pin[h] && ci < a.cimg && (unsigned)(py[h] + dh) < (unsigned)a.H &&
+                           (unsigned)(px[h] + dw) < (unsigned)a.W;
+            const unsigned e = (unsigned)(ci * a.P + (n0 + h * 64 + lane) + shift);
+            dma_b32(rb, Bs + (g * kCB + r) * BN + h * 64, v ? e * 4u : OOB);
+          }
+        }
       }
     };
 #pragma unroll
@@ -531,9 +554,16 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       if (k < nst) issue(k_a + k, k);
     for (int i = 0; i < nst; ++i) {
       const int younger = min(STAGES - 2, nst - 1 - i);
-      if (younger >= 2) wait_vmcnt<2 * INST_W>();
-      else if (younger == 1) wait_vmcnt<INST_W>();
-      else wait_vmcnt<0>();
+      if constexpr (STAGES >= 4) {
+        if (younger >= 2) wait_vmcnt<2 * INST_W>();
+        else if (younger == 1) wait_vmcnt<INST_W>();
+        else wait_vmcnt<0>();
+      } else if constexpr (STAGES == 3) {
+        if (younger == 1) wait_vmcnt<INST_W>();
+        else wait_vmcnt<0>();
+      } else {
+        wait_vmcnt<0>();
+      }
       __builtin_amdgcn_s_barrier();
       if (i + STAGES - 1 < nst) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
       const float* As = smem + (i % STAGES) * STAGE;
@@ -542,10 +572,11 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
     }
 
     constexpr int PSZ = BM * BN;
-    if (k_a > 0) {
-      // contributor: publish this piece for the tile's owner
-      // lane-contiguous layout: [TM*TN][4 waves][64 lanes][16 floats] (4 x dwordx4 per lane)
-      float4* pp = reinterpret_cast<float4*>(sk.part + ((long long)w * kMaxSeg + seg) * PSZ) + (wid * 64 + lane) * 4;
+    if (k_a > 0 || k_b < sk.KS) {
+      // a piece of a split tile: slot 0 = a piece that starts inside the tile (first segment of
+      // the range), slot 1 = the tile's head piece (last segment of the range)
+      float4* pp = reinterpret_cast<float4*>(sk.part + ((long long)w * 2 + (k_a > 0 ? 0 : 1)) * PSZ) +
+                   (wid * 64 + lane) * 4;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -556,37 +587,32 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
                                                        acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      const int w_lo = sk_worker_of(t * sk.KS, T, sk.NW);
+      const int w_hi = sk_worker_of((t + 1) * sk.KS - 1, T, sk.NW);
+      __shared__ int last;
       if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(sk.flags + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      continue;
-    }
-    if (k_b < sk.KS) {
-      // owner of a split tile: wait for the later pieces, then add them in worker order
-      const int w_hi = sk_worker_of((t + 1) * sk.KS - 1, T, sk.NW);
-      const int expect = w_hi - w;
-      if (tid == 0) {
-        int n = 0;
-        for (unsigned spin = 0;; ++spin) {
-          n = __hip_atomic_load(sk.flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (n >= expect) break;
-          if (spin > (1u << 24)) {
-            __hip_atomic_store(sk.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
+        const int old = __hip_atomic_fetch_add(sk.flags + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == w_hi - w_lo;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          __hip_atomic_store(sk.flags + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
+      if (!last) continue;
+      // every piece is in: sum them in worker order (independent of arrival order)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 #pragma unroll 1
-      for (int wc = w + 1; wc <= w_hi; ++wc) {
-        const int first_it = sk_start(wc, T, sk.NW);
-        const int segc = t - (int)((unsigned)first_it / (unsigned)sk.KS);
-        const float4* pp = reinterpret_cast<const float4*>(sk.part + ((long long)wc * kMaxSeg + segc) * PSZ) +
+      for (int wc = w_lo; wc <= w_hi; ++wc) {
+        const int slot = sk_start(wc, T, sk.NW) > t * sk.KS ? 0 : 1;
+        const float4* pc = reinterpret_cast<const float4*>(sk.part + ((long long)wc * 2 + slot) * PSZ) +
                            (wid * 64 + lane) * 4;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -594,7 +620,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
           for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const float4 v = pp[(i * TN + j) * 1024 + q];
+              const float4 v = pc[(i * TN + j) * 1024 + q];
               acc[i][j][4 * q] += v.x;
               acc[i][j][4 * q + 1] += v.y;
               acc[i][j][4 * q + 2] += v.z;
@@ -602,7 +628,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
             }
       }
     }
-    // owner (or sole worker of the tile): final output through a buffer resource - rows past M
+    // finishing workgroup (or sole worker of the tile): final output through a buffer resource - rows past M
     // fall outside the descriptor and are dropped; columns past P get an out-of-range offset.
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
@@ -616,7 +642,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int soff = ((r & 3) + 8 * (r >> 2)) * a.P * 4;
-          __builtin_amdgcn_raw_buffer_store_b32(acc[i][j][r], rc, voff, soff, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rc, voff, soff, 0);
         }
       }
   }

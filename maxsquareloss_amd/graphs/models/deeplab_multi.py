@@ -18,7 +18,9 @@ What runs where:
   - every BatchNorm (train mode, batch statistics of the one image, Q9) fused with the
     following ReLU and, for bn3, the residual add -> HIP kernels with fp64-accumulated
     statistics (MIOpen's single-pass variance is not accurate enough at bs=1);
-  - stem 7x7 conv, 1x1 convs, maxpool -> PyTorch-ROCm (MIOpen), SURVEY.md §8a row a13.
+  - 1x1 convs: `PointwiseConv` (the same HIP GEMM kernels with one unshifted tap) exists
+    behind USE_HIP_POINTWISE; by default they, the stem 7x7 conv and maxpool run on
+    PyTorch-ROCm (MIOpen/rocBLAS), which is faster on them today - SURVEY.md §8f row 1.
 """
 import torch
 import torch.nn as nn
@@ -40,6 +42,30 @@ class DilatedConv3x3(nn.Conv2d):
         return ops.dconv3x3(x, self.weight, self.dilation[0], self._pack)
 
 
+class PointwiseConv(nn.Conv2d):
+    """nn.Conv2d(cin, cout, 1, stride=1, bias=False) on the HIP kernels."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__(in_channels, out_channels, kernel_size=1, stride=1, bias=False)
+        self._pack = ops.PackCache(pointwise=True)
+
+    def forward(self, x):
+        return ops.pconv(x, self.weight, self._pack)
+
+
+# The HIP pointwise GEMMs run at 45-90 TFLOP/s on these shapes; rocBLAS's tuned FP32 GEMMs
+# (behind MIOpen) reach 85-113 on the forward and data gradient (scripts/bench_pconv.py,
+# profiles/).  Until the HIP core catches up the model keeps MIOpen for the 1x1 convs;
+# PointwiseConv stays available (and parity-tested) behind this switch.
+USE_HIP_POINTWISE = False
+
+
+def conv1x1(inplanes, planes, stride):
+    if stride == 1 and USE_HIP_POINTWISE:
+        return PointwiseConv(inplanes, planes)
+    return nn.Conv2d(inplanes, planes, kernel_size=1, stride=stride, bias=False)
+
+
 class Bottleneck(nn.Module):
     """deeplab_multi.py:8-48 (Caffe-style: the stride sits on conv1)."""
 
@@ -47,11 +73,11 @@ class Bottleneck(nn.Module):
 
     def __init__(self, inplanes, planes, stride=1, dilation=1, downsample=None, bn_momentum=0.1):
         super().__init__()
-        self.conv1 = nn.Conv2d(inplanes, planes, kernel_size=1, stride=stride, bias=False)
+        self.conv1 = conv1x1(inplanes, planes, stride)
         self.bn1 = nn.BatchNorm2d(planes, affine=affine_par)
         self.conv2 = DilatedConv3x3(planes, planes, dilation=dilation)
         self.bn2 = nn.BatchNorm2d(planes, affine=affine_par)
-        self.conv3 = nn.Conv2d(planes, planes * 4, kernel_size=1, bias=False)
+        self.conv3 = conv1x1(planes, planes * 4, 1)
         self.bn3 = nn.BatchNorm2d(planes * 4, affine=affine_par)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
@@ -120,7 +146,7 @@ class ResNetMulti(nn.Module):
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion or dilation == 2 or dilation == 4:
             downsample = nn.Sequential(
-                nn.Conv2d(self.inplanes, planes * block.expansion, kernel_size=1, stride=stride, bias=False),
+                conv1x1(self.inplanes, planes * block.expansion, stride),
                 nn.BatchNorm2d(planes * block.expansion, affine=affine_par))
         layers = [block(self.inplanes, planes, stride, dilation=dilation, downsample=downsample)]
         self.inplanes = planes * block.expansion

@@ -22,11 +22,20 @@ SIGNATURES = {
     "msl_dconv_packed_elems": (c_ll, [c_int, c_int, c_int, c_int]),
     "msl_dconv_pack": (c_int, [c_p, c_ll, c_int, c_int, c_int, c_int, c_p, c_p]),
     "msl_dconv_fwd_workspace": (c_sz, [c_int] * 5),
-    "msl_dconv_fwd": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_sz, c_p]),
+    "msl_counter_elems": (c_int, []),
+    "msl_dconv_fwd": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_dgrad_workspace": (c_sz, [c_int] * 5),
-    "msl_dconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_sz, c_p]),
+    "msl_dconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_wgrad_workspace": (c_sz, [c_int] * 5),
     "msl_dconv_wgrad": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p]),
+    "msl_pconv_packed_elems": (c_ll, [c_int] * 3),
+    "msl_pconv_pack": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p]),
+    "msl_pconv_fwd_workspace": (c_sz, [c_int] * 3),
+    "msl_pconv_fwd": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
+    "msl_pconv_dgrad_workspace": (c_sz, [c_int] * 3),
+    "msl_pconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
+    "msl_pconv_wgrad_workspace": (c_sz, [c_int] * 3),
+    "msl_pconv_wgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
     "msl_upsample_fwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p]),
     "msl_upsample_bwd_workspace": (c_sz, [c_int] * 5),
     "msl_upsample_bwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p, c_sz, c_p]),
@@ -93,6 +102,20 @@ def stream_ptr():
 
 def ptr(t):
     return None if t is None else t.data_ptr()
+
+
+_COUNTERS = {}
+
+
+def counters(device):
+    """The persistent, zero-initialised stream-K arrival counters for `device` and torch's current
+    stream (msl_counter_elems() ints; every conv call leaves them zero again)."""
+    key = (torch.device(device), torch.cuda.current_stream(device).cuda_stream)
+    buf = _COUNTERS.get(key)
+    if buf is None:
+        buf = torch.zeros(load().msl_counter_elems(), dtype=torch.int32, device=device)
+        _COUNTERS[key] = buf
+    return buf
 
 
 def workspace(nbytes, device):

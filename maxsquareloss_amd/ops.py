@@ -30,7 +30,8 @@ class PackCache:
     in-place version counters), not once per call.
     """
 
-    def __init__(self):
+    def __init__(self, pointwise=False):
+        self.pointwise = pointwise
         self.key = {0: None, 1: None}
         self.buf = {0: None, 1: None}
 
@@ -39,7 +40,10 @@ class PackCache:
         if self.key[for_dgrad] != key:
             lib = hip.load()
             nb = len(weights)
-            total = lib.msl_dconv_packed_elems(nb, cin, cout, for_dgrad)
+            if self.pointwise:
+                total = lib.msl_pconv_packed_elems(cin, cout, for_dgrad)
+            else:
+                total = lib.msl_dconv_packed_elems(nb, cin, cout, for_dgrad)
             per_branch = total // nb
             buf = self.buf[for_dgrad]
             if buf is None or buf.numel() != total or buf.device != weights[0].device:
@@ -47,9 +51,13 @@ class PackCache:
             s = hip.stream_ptr()
             for b, w in enumerate(weights):
                 wc = w.detach().contiguous()
-                hip.check(lib.msl_dconv_pack(wc.data_ptr(), 0, 1, cin, cout, for_dgrad,
-                                             buf.data_ptr() + 4 * b * per_branch, s),
-                          "msl_dconv_pack")
+                dst = buf.data_ptr() + 4 * b * per_branch
+                if self.pointwise:
+                    hip.check(lib.msl_pconv_pack(wc.data_ptr(), cin, cout, for_dgrad, dst, s),
+                              "msl_pconv_pack")
+                else:
+                    hip.check(lib.msl_dconv_pack(wc.data_ptr(), 0, 1, cin, cout, for_dgrad, dst, s),
+                              "msl_dconv_pack")
             self.buf[for_dgrad] = buf
             self.key[for_dgrad] = key
         return self.buf[for_dgrad]
@@ -86,7 +94,8 @@ class _DConv3x3(Function):
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         hip.check(lib.msl_dconv_fwd(x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb,
-                                    cin, cout, h, w, dil0, dil1 if nb > 1 else 0, ws.data_ptr(), wsb,
+                                    cin, cout, h, w, dil0, dil1 if nb > 1 else 0,
+                                    hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
                                     hip.stream_ptr()), "msl_dconv_fwd")
         if probe is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
@@ -111,7 +120,8 @@ class _DConv3x3(Function):
             wsb = lib.msl_dconv_dgrad_workspace(nb, cin, cout, h, w)
             ws = hip.workspace(wsb, x.device)
             hip.check(lib.msl_dconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin,
-                                          cout, h, w, dil0, d1, ws.data_ptr(), wsb, s), "msl_dconv_dgrad")
+                                          cout, h, w, dil0, d1, hip.counters(x.device).data_ptr(),
+                                          ws.data_ptr(), wsb, s), "msl_dconv_dgrad")
         dw_all = torch.empty((nb, cout, cin, 3, 3), dtype=_f32, device=x.device)
         db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
         wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w)
@@ -133,6 +143,61 @@ def dconv3x3(x, weight, dilation, cache):
 def aspp2(x, w0, b0, w1, b1, dil0, dil1, cache):
     """conv_d6(x) + conv_d12(x) with biases: the live part of Classifier_Module (deeplab_multi.py:62-66)."""
     return _DConv3x3.apply(x, w0, w1, b0, b1, int(dil0), int(dil1), cache)
+
+
+# --------------------------------------------------------------------------- pointwise conv
+class _PConv(Function):
+    """y = W x for a 1x1, stride-1, bias-free conv (W: [cout][cin][1][1])."""
+
+    @staticmethod
+    def forward(ctx, x, weight, cache):
+        x = _check_act(x, "pconv")
+        cout, cin = weight.shape[0], weight.shape[1]
+        if weight.shape[2:] != (1, 1) or x.size(1) != cin:
+            raise hip.MSLError(f"pconv: weight {tuple(weight.shape)} does not match input {tuple(x.shape)}")
+        h, w = x.shape[2], x.shape[3]
+        p = h * w
+        lib = hip.load()
+        packed = cache.get([weight], cin, cout, 0)
+        y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
+        wsb = lib.msl_pconv_fwd_workspace(cin, cout, p)
+        ws = hip.workspace(wsb, x.device)
+        hip.check(lib.msl_pconv_fwd(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
+                                    hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                                    hip.stream_ptr()), "msl_pconv_fwd")
+        ctx.save_for_backward(x, weight)
+        ctx.meta = (cin, cout, p, cache)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        cin, cout, p, cache = ctx.meta
+        gy = gy.contiguous()
+        lib = hip.load()
+        s = hip.stream_ptr()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            packed_d = cache.get([weight], cin, cout, 1)
+            dx = torch.empty_like(x)
+            wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
+            ws = hip.workspace(wsb, x.device)
+            hip.check(lib.msl_pconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
+                                          hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s),
+                      "msl_pconv_dgrad")
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(weight)
+            wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
+            ws = hip.workspace(wsb, x.device)
+            hip.check(lib.msl_pconv_wgrad(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), cin, cout, p, 0,
+                                          ws.data_ptr(), wsb, s), "msl_pconv_wgrad")
+        return dx, dw, None
+
+
+def pconv(x, weight, cache):
+    """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99)."""
+    return _PConv.apply(x, weight, cache)
 
 
 # --------------------------------------------------------------------------- upsample

@@ -1,0 +1,21 @@
+"""The bench's dominant kernel alone: the layer3 dilated conv forward (256->256, d=2) at the
+1024x512 feature size (65x129), launched through the same op as the training step.  Profiled
+with rocprofv3 (--kernel-trace --stats, then separate --pmc passes) by scripts/gpu_bench_prof.sh."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from maxsquareloss_amd import ops  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+g = torch.Generator(device="cuda").manual_seed(0)
+x = torch.randn(1, 256, 65, 129, device="cuda", generator=g)
+w = torch.randn(256, 256, 3, 3, device="cuda", generator=g) * 0.02
+cache = ops.PackCache()
+with torch.no_grad():
+    for _ in range(n):
+        y = ops.dconv3x3(x, w, 2, cache)
+torch.cuda.synchronize()
+print("launches", n, "checksum", float(y.double().sum()))

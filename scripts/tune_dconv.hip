@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 #include "dconv_kernels.h"
 
@@ -40,7 +41,7 @@ float run_fwd(const Shape& sh, const float* x, const float* wp, float* y, float*
   const int groups = a.ncb * 9;
   a.ksteps = groups / (BK / 16);
   a.kps = (a.ksteps + S - 1) / S;
-  a.slab = (long long)sh.cout * P;
+  a.slab = (long long)sh.cout * P; a.taps = 9;
   dim3 grid((P + BN - 1) / BN, (sh.cout + BM - 1) / BM, S);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -63,7 +64,7 @@ float run_fwd_dma(const Shape& sh, const float* x, const float* wp, float* y, fl
   a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
   a.ksteps = a.ncb * 9;
   a.kps = (a.ksteps + S - 1) / S;
-  a.slab = (long long)sh.cout * P;
+  a.slab = (long long)sh.cout * P; a.taps = 9;
   dim3 grid((P + BN - 1) / BN, (sh.cout + BM - 1) / BM, S);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -77,32 +78,32 @@ float run_fwd_dma(const Shape& sh, const float* x, const float* wp, float* y, fl
   return ms / iters;
 }
 
-template <int BM, int BN, int STAGES, int WM, int WN>
+template <int BM, int BN, int G, int STAGES, int WM, int WN>
 float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda, int* flags) {
   const int P = sh.h * sh.w;
   FwdArgs a;
   a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
-  a.ksteps = a.ncb * 9; a.kps = a.ksteps; a.slab = 0;
+  a.ksteps = a.ncb * 9; a.kps = a.ksteps; a.slab = 0; a.taps = 9;
   SkArgs sk;
-  sk.part = ws; sk.flags = flags + 64; sk.err = flags;
-  sk.tiles_m = (sh.cout + BM - 1) / BM; sk.tiles_n = (P + BN - 1) / BN; sk.KS = a.ksteps; sk.NW = NW;
+  sk.part = ws; sk.flags = flags;
+  sk.tiles_m = (sh.cout + BM - 1) / BM; sk.tiles_n = (P + BN - 1) / BN; sk.KS = a.ksteps / G; sk.NW = NW;
   sk.T = sk.tiles_m * sk.tiles_n * sk.KS;
   const int tiles = sk.tiles_m * sk.tiles_n;
   if (sk.T / NW > 2 * sk.KS) { printf("NW too small\n"); return 1e9f; }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  CK(hipMemset(flags, 0, 256));
+  CK(hipMemset(flags, 0, 1 << 20));
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    CK(hipMemsetAsync(flags + 64, 0, tiles * 4, 0));
-    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, STAGES, WM, WN>), dim3(NW), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, WM, WN>), dim3(NW), dim3(256), 0, 0, a, sk);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-  int err; CK(hipMemcpy(&err, flags, 4, hipMemcpyDeviceToHost));
-  if (err) printf("SPIN TIMEOUT\n");
+  std::vector<int> fl(tiles);
+  CK(hipMemcpy(fl.data(), flags, tiles * 4, hipMemcpyDeviceToHost));
+  for (int i = 0; i < tiles; ++i) if (fl[i]) { printf("COUNTER NOT RE-ARMED tile %d\n", i); break; }
   return ms / iters;
 }
 
@@ -112,7 +113,7 @@ float run_wgrad(const Shape& sh, const float* x, const float* dy, float* dw, flo
   WgradArgs a;
   a.dy = dy; a.x = x; a.C = S > 1 ? ws : dw; a.M = sh.cout; a.N = sh.cin; a.H = sh.h; a.W = sh.w; a.P = P;
   a.dil0 = sh.dil; a.dil1 = 0; a.ntap = 9; a.ksteps = (P + BK - 1) / BK; a.kps = (a.ksteps + S - 1) / S;
-  a.accumulate = 0; a.slab = (long long)sh.cout * sh.cin * 9; a.cbranch = a.slab;
+  a.accumulate = 0; a.taps = 9; a.slab = (long long)sh.cout * sh.cin * 9; a.cbranch = a.slab;
   dim3 grid((sh.cin + BN - 1) / BN, (sh.cout + BM - 1) / BM, S * 9);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -137,7 +138,9 @@ static double maxdiff(const float* a, const float* b, size_t n, double* scale) {
 }
 
 int main(int argc, char** argv) {
-  const int iters = 20;
+  // "sk": only the library's stream-K configuration on the layer3 shape (profiling runs)
+  const bool sk_only = argc > 1 && std::string(argv[1]) == "sk";
+  const int iters = sk_only ? 5 : 20;
   Shape shapes[] = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
   for (const Shape& sh : shapes) {
     const int P = sh.h * sh.w;
@@ -166,11 +169,17 @@ int main(int argc, char** argv) {
       double md = maxdiff(y, yref, (size_t)sh.cout * P, &sc); \
       printf("fdma  BM %3d BN %3d ST %2d W %dx%d S %d grid %5d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, ST, WM, WN, S, \
              ((P + BN - 1) / BN) * ((sh.cout + BM - 1) / BM) * S, ms * 1e3, gf / ms, md, sc); }
-#define FSK(BM, BN, ST, WM, WN, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); float ms = run_fwd_sk<BM, BN, ST, WM, WN>(sh, x, wp, y, ws, NW, iters, lda, flags); \
+#define FSK(BM, BN, G, ST, WM, WN, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); float ms = run_fwd_sk<BM, BN, G, ST, WM, WN>(sh, x, wp, y, ws, NW, iters, lda, flags); \
       double md = maxdiff(y, yref, (size_t)sh.cout * P, &sc); \
-      printf("fsk   BM %3d BN %3d ST %2d W %dx%d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, ST, WM, WN, NW, ms * 1e3, gf / ms, md, sc); }
-    FSK(128, 128, 3, 2, 2, 256) FSK(128, 128, 3, 2, 2, 512) FSK(128, 128, 3, 2, 2, 768)
-    FSK(64, 128, 3, 2, 2, 512) FSK(64, 128, 3, 2, 2, 768) FSK(64, 128, 3, 2, 2, 1024)
+      printf("fsk   BM %3d BN %3d G %d ST %2d W %dx%d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, G, ST, WM, WN, NW, ms * 1e3, gf / ms, md, sc); }
+    if (sk_only) {
+      FSK(128, 128, 2, 2, 2, 2, 512)
+      break;
+    }
+    FSK(128, 128, 1, 3, 2, 2, 256) FSK(128, 128, 1, 3, 2, 2, 512)
+    FSK(128, 128, 1, 2, 2, 2, 512) FSK(128, 128, 2, 2, 2, 2, 512) FSK(128, 128, 2, 2, 2, 2, 256)
+    FSK(128, 128, 2, 3, 2, 2, 256) FSK(128, 128, 4, 2, 2, 2, 256)
+    FSK(64, 128, 1, 3, 2, 2, 768) FSK(64, 128, 2, 2, 2, 2, 768) FSK(64, 128, 2, 2, 2, 2, 512)
     FDMA(128, 128, 3, 2, 2, 1) FDMA(128, 128, 3, 2, 2, 2) FDMA(128, 128, 3, 2, 2, 3) FDMA(128, 128, 3, 2, 2, 4)
     FDMA(128, 128, 3, 2, 2, 6) FDMA(128, 128, 3, 2, 2, 8)
     FDMA(64, 128, 3, 2, 2, 1) FDMA(64, 128, 3, 2, 2, 2) FDMA(64, 128, 3, 2, 2, 3) FDMA(64, 128, 3, 2, 2, 4)

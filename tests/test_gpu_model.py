@@ -36,6 +36,28 @@ def _normwise(a, b):
     return ((a - b).abs().max() / b.abs().max()).item()
 
 
+def _guidance_slack(model, xt, thr, scale, eps=5e-4):
+    """How far the multi-level-guidance CE (solve_gta5.py:220-235) may move under rounding-level
+    logit changes: it is a mean over a thresholded, argmax-labelled pixel set, so a pixel whose
+    max probability sits within eps of the threshold (or whose two top averaged classes are
+    within eps) may enter, leave or change label.  Such a pixel can carry a large CE (x2 says
+    > 0.95 while x1 disagrees), so the bar is the sum of their possible contributions."""
+    import torch.nn.functional as F
+    with torch.no_grad():
+        r2, r1 = orc.forward(model.params, model.buffers, xt)
+        P, P2 = F.softmax(r2, 1), F.softmax(r1, 1)
+        mp, mp2 = P.max(1)[0], P2.max(1)[0]
+        top2, cls2 = ((P + P2) / 2).topk(2, dim=1)
+        mask = (mp > thr) | (mp2 > thr)
+        risk = ((mp - thr).abs() < eps) | ((mp2 - thr).abs() < eps) | (mask & (top2[:, 0] - top2[:, 1] < eps))
+        nll = -F.log_softmax(r1, 1)
+        worst = nll.gather(1, cls2).max(1)[0]  # the label is one of the two top averaged classes
+        n_sel = max(int(mask.sum()), 1)
+        label = orc.multi_guidance_label(P, P2, thr)
+        mean = orc.ce(r1, label).item()
+        return scale * float(((worst + mean) * risk).sum()) / n_sel
+
+
 def test_forward_matches_oracle():
     tr = UDATrainer(_args(["--target_mode", "maxsquare", "--multi", "False"]), cuda=True)
     ref = orc.Model({k: v.cpu() for k, v in tr.model.state_dict().items()})
@@ -76,6 +98,8 @@ def test_uda_steps_match_goldens_and_oracle(tag, extra):
         xt = synthetic_image(H, W, 500 + it)
         tr.uda_step(xs.cuda(), ys.cuda(), xt.cuda())
         torch.cuda.synchronize()
+        slack2 = (_guidance_slack(model, xt, cfg["threshold"], cfg["lambda_seg"] * cfg["lambda_target"])
+                  if tr.args.multi else 0.0)
         out = orc.uda_step(model, opt, xs, ys, xt, cfg, it)
         if it == 0:
             orc.uda_step(m64, opt64, xs, ys, xt, cfg, it)
@@ -84,11 +108,12 @@ def test_uda_steps_match_goldens_and_oracle(tag, extra):
             mine["loss_target_2"] = tr.loss_target_2.item()
         for k, v in mine.items():
             # rounding-only differences: 1e-3; loss_target_2 is a CE over a
-            # thresholded pseudo-label (discontinuous in the logits): 5e-3
-            tol = 5e-3 if k == "loss_target_2" else 1e-3
-            assert v == pytest.approx(out[k], rel=tol), f"{k} it{it} vs oracle"
+            # thresholded pseudo-label (discontinuous in the logits): 1e-3 plus the possible
+            # contribution of the pixels within rounding of a threshold / argmax decision
+            ab = slack2 if k == "loss_target_2" else 0.0
+            assert v == pytest.approx(out[k], rel=1e-3, abs=ab), f"{k} it{it} vs oracle (slack {ab:.3g})"
             if it == 0:
-                assert v == pytest.approx(float(g[f"{tag}_it{it}_{k}"]), rel=tol), f"{k} it0 vs golden"
+                assert v == pytest.approx(float(g[f"{tag}_it{it}_{k}"]), rel=1e-3, abs=ab), f"{k} it0 vs golden"
             elif k != "loss_target_2":
                 # loss curve vs the reference itself after a step: the fp32 drift of the step is
                 # amplified (the box's CPU oracle is itself 2e-2 off on the IW loss here).  The
