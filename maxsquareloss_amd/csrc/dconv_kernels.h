@@ -56,6 +56,39 @@ __device__ __forceinline__ void mfma_stage(const float* __restrict__ As, const f
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kp][i], bv[kp][j], acc[i][j], 0, 0, 0);
 }
 
+// Software-pipelined variant: the operands of k-pair kp+1 are read while the MFMAs of k-pair kp
+// run (scheduling barriers keep the compiler from sinking the reads next to their use, which
+// exposes the LDS latency once per k-pair), and `mid` - the next stage's DMA issue - is placed
+// after the first k-pair so its address arithmetic overlaps the MFMA pipe.
+template <int BK, int TM, int TN, int LDA_S, int LDB_S, typename F>
+__device__ __forceinline__ void mfma_stage_pipe(const float* __restrict__ As, const float* __restrict__ Bs,
+                                                int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
+  const int l32 = lane & 31, kh = lane >> 5;
+  constexpr int KP = BK / 2;
+  float av[2][TM], bv[2][TN];
+  auto load = [&](int kp, int buf) {
+    const int kr = 2 * kp + kh;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[buf][i] = As[kr * LDA_S + wm + i * 32 + l32];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[buf][j] = Bs[kr * LDB_S + wn + j * 32 + l32];
+  };
+  load(0, 0);
+#pragma unroll
+  for (int kp = 0; kp < KP; ++kp) {
+    const int cur = kp & 1;
+    if (kp + 1 < KP) load(kp + 1, cur ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
+    if (kp == 0) mid();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Forward form: C[m][p] = sum_k A[k][m] * B[k][p], BK = G * 16 (G tap-groups per K-step).
 template <int BM, int BN, int BK, int WM, int WN>
 __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
@@ -494,6 +527,9 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       px[h] = p - py[h] * a.W;
     }
     auto issue = [&](int s, int slot) {
+#ifdef MSL_SK_NODMA  // tuning-harness experiment only: no operand traffic
+      return;
+#endif
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
 #pragma unroll
@@ -565,9 +601,11 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
         wait_vmcnt<0>();
       }
       __builtin_amdgcn_s_barrier();
-      if (i + STAGES - 1 < nst) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
       const float* As = smem + (i % STAGES) * STAGE;
-      mfma_stage<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc);
+      const bool more = i + STAGES - 1 < nst;
+      mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, [&] {
+        if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
+      });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
