@@ -197,12 +197,13 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
                float* save_mean, float* save_invstd, int c, int p, int training,
                int update_running, float momentum, float eps, int relu, void* ws,
                size_t ws_bytes, msl_stream_t stream);
-/* dx (nullable), dres = d residual (nullable), dgamma / dbeta (nullable); y is the
- * forward output (needed when relu). */
+/* dx (nullable), dres = d residual (nullable), dgamma / dbeta (nullable, = or += when
+ * accumulate_params: the training step accumulates straight into the flat gradient buffer);
+ * y is the forward output (needed when relu). */
 int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gamma,
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
-               float* dgamma, float* dbeta, int c, int p, int training, int relu, void* ws,
-               size_t ws_bytes, msl_stream_t stream);
+               float* dgamma, float* dbeta, int c, int p, int training, int relu,
+               int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * SGD step with the reference's duplicated-parameter semantics (quirk Q2):

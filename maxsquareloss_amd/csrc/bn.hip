@@ -8,19 +8,27 @@
 // statistics are accumulated in fp64 around a per-channel shift (its first element), which
 // is at least as accurate as the CPU's two-pass fp32 sums.
 //
-// Layout [C][P] (N = 1).  Forward: stats kernel (grid C x S partial fp64 sums) + apply kernel
-// (each block folds the S partials of its channel, block (c, 0) updates running stats).
-// Backward: reduce kernel (sum g, sum g*xhat with g = dy masked by y > 0 when ReLU) + apply
-// kernel (dx, d residual, dgamma, dbeta).  HBM-bound: fwd reads x twice, writes y; bwd reads
-// dy, x, y twice, writes dx (+ dres).
+// Layout [C][P] (N = 1).  Forward: stats kernel (grid C x S partial fp64 sums per channel) +
+// a flat apply kernel over the whole tensor in float4s (each block folds the partials of the
+// channels it touches).  Backward: per-channel reduce (sum g, sum g*xhat with g = dy masked by
+// y > 0 when ReLU) + flat apply (dx, d residual, dgamma, dbeta).  HBM-bound: fwd reads x twice,
+// writes y (+ reads the residual); bwd reads dy, x, y twice, writes dx (+ dres).
 #include "msl_internal.h"
 
 namespace msl {
 
 constexpr int kBnMaxSplit = 16;
-constexpr int kBnChunk = 8192;  // pixels per stats block
+constexpr int kBnChunk = 8192;  // pixels per statistics block
 
 static int bn_splits(int P) { return std::max(1, std::min(kBnMaxSplit, cdiv(P, kBnChunk))); }
+
+// Elements per block of the flat (channel-crossing) apply kernels: a multiple of 4 small enough
+// that a block touches at most 256 channels (their coefficients are staged in LDS).
+static int bn_flat_chunk(int P) {
+  int ch = 4096;
+  while (ch > 4 && ch / P + 2 > 256) ch /= 2;
+  return ch;
+}
 
 __device__ __forceinline__ void block_sum2_d(double& a, double& b, double* red) {
   a = wave_sum_d(a);
@@ -36,20 +44,40 @@ __device__ __forceinline__ void block_sum2_d(double& a, double& b, double* red) 
   b = (red[1] + red[3]) + (red[5] + red[7]);
 }
 
+// Visit elements [e0, e1) of a flat array: a 16-B-aligned float4 body shared over the block's
+// threads plus a scalar head and tail (< 4 elements each).  f(e, v...) gets the element index.
+template <bool VEC, typename F4, typename F1>
+__device__ __forceinline__ void visit_range(long long e0, long long e1, F4&& f4, F1&& f1) {
+  long long a0 = VEC ? ((e0 + 3) & ~3LL) : e1;
+  long long a1 = VEC ? (e1 & ~3LL) : e1;
+  if (a0 > a1) a0 = a1 = e1;
+  for (long long e = e0 + threadIdx.x; e < a0; e += 256) f1(e);
+  for (long long i = a0 / 4 + threadIdx.x; i < a1 / 4; i += 256) f4(i);
+  for (long long e = a1 + threadIdx.x; e < e1; e += 256) f1(e);
+}
+
+template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_stats(const float* __restrict__ x, int P, int S,
                                                    double* __restrict__ part) {
   __shared__ double red[8];
   const int c = blockIdx.x, s = blockIdx.y;
-  const float* xc = x + (long long)c * P;
-  const double shift = (double)xc[0];
+  const long long base = (long long)c * P;
+  const double shift = (double)x[base];
   const int chunk = cdiv(P, S);
   const int beg = s * chunk, end = min(P, beg + chunk);
   double s1 = 0.0, s2 = 0.0;
-  for (int p = beg + threadIdx.x; p < end; p += 256) {
-    const double d = (double)xc[p] - shift;
+  auto acc = [&](float v) {
+    const double d = (double)v - shift;
     s1 += d;
     s2 += d * d;
-  }
+  };
+  visit_range<VEC>(
+      base + beg, base + end,
+      [&](long long i) {
+        const float4 v = reinterpret_cast<const float4*>(x)[i];
+        acc(v.x); acc(v.y); acc(v.z); acc(v.w);
+      },
+      [&](long long e) { acc(x[e]); });
   block_sum2_d(s1, s2, red);
   if (threadIdx.x == 0) {
     part[((long long)c * S + s) * 2] = s1;
@@ -69,14 +97,25 @@ struct BnArgs {
   float* save_invstd;
   long long* num_batches;
   const double* part;
-  int P, S, relu, training, update_running;
+  int C, P, S, chunk, relu, training, update_running;
   float eps, momentum;
 };
 
+// Flat apply: block b covers elements [b*chunk, (b+1)*chunk) of the [C][P] tensor (possibly
+// several channels).  Each block derives the (alpha, beta') of the channels it touches from the
+// fp64 partial sums; the block holding a channel's first element also publishes its saved /
+// running statistics.
+template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_apply(BnArgs a) {
-  __shared__ float coef[2];
-  const int c = blockIdx.x;
-  if (threadIdx.x == 0) {
+  __shared__ float coef[2][256];
+  const long long N = (long long)a.C * a.P;
+  const long long start = (long long)blockIdx.x * a.chunk;
+  const long long end = min(N, start + a.chunk);
+  const int c0 = (int)(start / a.P);
+  const int nch = (int)((end - 1) / a.P) - c0 + 1;
+  if ((int)threadIdx.x < nch) {
+    const int c = c0 + threadIdx.x;
+    const bool owner = (long long)c * a.P >= start;  // this block holds the channel's first element
     float mean, invstd;
     if (a.training) {
       double s1 = 0.0, s2 = 0.0;
@@ -91,41 +130,50 @@ __global__ void __launch_bounds__(256) k_bn_apply(BnArgs a) {
       if (var < 0.0) var = 0.0;
       mean = (float)(shift + dm);
       invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-      if (blockIdx.y == 0) {
-        a.save_mean[c] = mean;
-        a.save_invstd[c] = invstd;
-        if (a.update_running) {
-          const float m = a.momentum;
-          const float unbiased = (float)(a.P > 1 ? var * n / (n - 1.0) : var);
-          a.running_mean[c] = (1.f - m) * a.running_mean[c] + m * mean;
-          a.running_var[c] = (1.f - m) * a.running_var[c] + m * unbiased;
-          if (c == 0 && a.num_batches) a.num_batches[0] += 1;
-        }
+      if (owner && a.update_running) {
+        const float m = a.momentum;
+        const float unbiased = (float)(a.P > 1 ? var * n / (n - 1.0) : var);
+        a.running_mean[c] = (1.f - m) * a.running_mean[c] + m * mean;
+        a.running_var[c] = (1.f - m) * a.running_var[c] + m * unbiased;
+        if (c == 0 && a.num_batches) a.num_batches[0] += 1;
       }
     } else {
       mean = a.running_mean[c];
       invstd = 1.f / sqrtf(a.running_var[c] + a.eps);
-      if (blockIdx.y == 0) {
-        a.save_mean[c] = mean;
-        a.save_invstd[c] = invstd;
-      }
+    }
+    if (owner) {
+      a.save_mean[c] = mean;
+      a.save_invstd[c] = invstd;
     }
     // y = x * alpha + beta'  (batch_norm_cpu_transform_input form)
     const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
-    coef[0] = alpha;
-    coef[1] = (a.beta ? a.beta[c] : 0.f) - mean * alpha;
+    coef[0][threadIdx.x] = alpha;
+    coef[1][threadIdx.x] = (a.beta ? a.beta[c] : 0.f) - mean * alpha;
   }
   __syncthreads();
-  const float alpha = coef[0], bb = coef[1];
-  const long long base = (long long)c * a.P;
-  const int chunk = cdiv(a.P, gridDim.y);
-  const int beg = blockIdx.y * chunk, end = min(a.P, beg + chunk);
-  for (int p = beg + threadIdx.x; p < end; p += 256) {
-    float v = a.x[base + p] * alpha + bb;
-    if (a.residual) v += a.residual[base + p];
-    if (a.relu) v = fmaxf(v, 0.f);
-    a.y[base + p] = v;
-  }
+  const long long cbound = (long long)(c0 + 1) * a.P;  // first element of channel c0+1
+  auto one = [&](long long e, float xv, float rv) {
+    int k = 0;
+    if (e >= cbound) k = (int)(e / a.P) - c0;
+    float v = xv * coef[0][k] + coef[1][k];
+    v += rv;
+    return a.relu ? fmaxf(v, 0.f) : v;
+  };
+  visit_range<VEC>(
+      start, end,
+      [&](long long i) {
+        const float4 xv = reinterpret_cast<const float4*>(a.x)[i];
+        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.residual) rv = reinterpret_cast<const float4*>(a.residual)[i];
+        const long long e = 4 * i;
+        float4 o;
+        o.x = one(e, xv.x, rv.x);
+        o.y = one(e + 1, xv.y, rv.y);
+        o.z = one(e + 2, xv.z, rv.z);
+        o.w = one(e + 3, xv.w, rv.w);
+        reinterpret_cast<float4*>(a.y)[i] = o;
+      },
+      [&](long long e) { a.y[e] = one(e, a.x[e], a.residual ? a.residual[e] : 0.f); });
 }
 
 struct BnBwdArgs {
@@ -140,9 +188,10 @@ struct BnBwdArgs {
   float* dgamma;
   float* dbeta;
   double* part;
-  int P, S, relu, training;
+  int C, P, S, chunk, relu, training, accumulate;
 };
 
+template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_bwd_reduce(BnBwdArgs a) {
   __shared__ double red[8];
   const int c = blockIdx.x, s = blockIdx.y;
@@ -151,13 +200,22 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(BnBwdArgs a) {
   const int chunk = cdiv(a.P, a.S);
   const int beg = s * chunk, end = min(a.P, beg + chunk);
   double sg = 0.0, sgx = 0.0;
-  for (int p = beg + threadIdx.x; p < end; p += 256) {
-    float g = a.dy[base + p];
-    if (a.relu && !(a.y[base + p] > 0.f)) g = 0.f;
-    const float xh = (a.x[base + p] - mean) * invstd;
+  auto acc = [&](float g, float yv, float xv) {
+    if (a.relu && !(yv > 0.f)) g = 0.f;
+    const float xh = (xv - mean) * invstd;
     sg += (double)g;
     sgx += (double)g * (double)xh;
-  }
+  };
+  visit_range<VEC>(
+      base + beg, base + end,
+      [&](long long i) {
+        const float4 g = reinterpret_cast<const float4*>(a.dy)[i];
+        const float4 xv = reinterpret_cast<const float4*>(a.x)[i];
+        float4 yv = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (a.relu) yv = reinterpret_cast<const float4*>(a.y)[i];
+        acc(g.x, yv.x, xv.x); acc(g.y, yv.y, xv.y); acc(g.z, yv.z, xv.z); acc(g.w, yv.w, xv.w);
+      },
+      [&](long long e) { acc(a.dy[e], a.relu ? a.y[e] : 1.f, a.x[e]); });
   block_sum2_d(sg, sgx, red);
   if (threadIdx.x == 0) {
     a.part[((long long)c * a.S + s) * 2] = sg;
@@ -165,40 +223,68 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(BnBwdArgs a) {
   }
 }
 
+template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
-  __shared__ float coef[3];
-  const int c = blockIdx.x;
-  if (threadIdx.x == 0) {
+  __shared__ float coef[5][256];
+  const long long N = (long long)a.C * a.P;
+  const long long start = (long long)blockIdx.x * a.chunk;
+  const long long end = min(N, start + a.chunk);
+  const int c0 = (int)(start / a.P);
+  const int nch = (int)((end - 1) / a.P) - c0 + 1;
+  if ((int)threadIdx.x < nch) {
+    const int c = c0 + threadIdx.x;
     double sg = 0.0, sgx = 0.0;
     for (int s = 0; s < a.S; ++s) {
       sg += a.part[((long long)c * a.S + s) * 2];
       sgx += a.part[((long long)c * a.S + s) * 2 + 1];
     }
-    if (blockIdx.y == 0) {
-      if (a.dgamma) a.dgamma[c] = (float)sgx;
-      if (a.dbeta) a.dbeta[c] = (float)sg;
+    if ((long long)c * a.P >= start) {
+      if (a.dgamma) a.dgamma[c] = a.accumulate ? a.dgamma[c] + (float)sgx : (float)sgx;
+      if (a.dbeta) a.dbeta[c] = a.accumulate ? a.dbeta[c] + (float)sg : (float)sg;
     }
     const float w = a.gamma ? a.gamma[c] : 1.f;
-    coef[0] = a.save_invstd[c] * w;  // invstd * gamma
-    coef[1] = a.training ? (float)(sg / (double)a.P) : 0.f;
-    coef[2] = a.training ? (float)(sgx / (double)a.P) : 0.f;
+    coef[0][threadIdx.x] = a.save_invstd[c] * w;  // invstd * gamma
+    coef[1][threadIdx.x] = a.training ? (float)(sg / (double)a.P) : 0.f;
+    coef[2][threadIdx.x] = a.training ? (float)(sgx / (double)a.P) : 0.f;
+    coef[3][threadIdx.x] = a.save_mean[c];
+    coef[4][threadIdx.x] = a.save_invstd[c];
   }
   __syncthreads();
-  const float k = coef[0], mg = coef[1], mgx = coef[2];
-  const float mean = a.save_mean[c], invstd = a.save_invstd[c];
-  const long long base = (long long)c * a.P;
-  const int chunk = cdiv(a.P, gridDim.y);
-  const int beg = blockIdx.y * chunk, end = min(a.P, beg + chunk);
-  for (int p = beg + threadIdx.x; p < end; p += 256) {
-    float g = a.dy[base + p];
-    if (a.relu && !(a.y[base + p] > 0.f)) g = 0.f;
-    if (a.dres) a.dres[base + p] = g;
-    if (a.dx) {
-      const float xh = (a.x[base + p] - mean) * invstd;
-      a.dx[base + p] = (g - mg - xh * mgx) * k;
-    }
-  }
+  const long long cbound = (long long)(c0 + 1) * a.P;
+  // returns the masked upstream gradient g; dx through the reference's formula
+  auto one = [&](long long e, float g, float yv, float xv, float& dxv) {
+    int k = 0;
+    if (e >= cbound) k = (int)(e / a.P) - c0;
+    if (a.relu && !(yv > 0.f)) g = 0.f;
+    const float xh = (xv - coef[3][k]) * coef[4][k];
+    dxv = (g - coef[1][k] - xh * coef[2][k]) * coef[0][k];
+    return g;
+  };
+  visit_range<VEC>(
+      start, end,
+      [&](long long i) {
+        const float4 g = reinterpret_cast<const float4*>(a.dy)[i];
+        const float4 xv = reinterpret_cast<const float4*>(a.x)[i];
+        float4 yv = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (a.relu) yv = reinterpret_cast<const float4*>(a.y)[i];
+        const long long e = 4 * i;
+        float4 gm, d;
+        gm.x = one(e, g.x, yv.x, xv.x, d.x);
+        gm.y = one(e + 1, g.y, yv.y, xv.y, d.y);
+        gm.z = one(e + 2, g.z, yv.z, xv.z, d.z);
+        gm.w = one(e + 3, g.w, yv.w, xv.w, d.w);
+        if (a.dres) reinterpret_cast<float4*>(a.dres)[i] = gm;
+        if (a.dx) reinterpret_cast<float4*>(a.dx)[i] = d;
+      },
+      [&](long long e) {
+        float d;
+        const float gm = one(e, a.dy[e], a.relu ? a.y[e] : 1.f, a.x[e], d);
+        if (a.dres) a.dres[e] = gm;
+        if (a.dx) a.dx[e] = d;
+      });
 }
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace msl
 
@@ -221,8 +307,12 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   const int S = bn_splits(p);
   if (training && ws_bytes < msl_bn_workspace(c, p)) return MSL_ERR_WORKSPACE;
   double* part = (double*)ws;
+  const bool vec = al16(x) && al16(y) && (!residual || al16(residual));
   if (training) {
-    hipLaunchKernelGGL(k_bn_stats, dim3(c, S), dim3(256), 0, st, x, p, S, part);
+    if (vec)
+      hipLaunchKernelGGL(k_bn_stats<true>, dim3(c, S), dim3(256), 0, st, x, p, S, part);
+    else
+      hipLaunchKernelGGL(k_bn_stats<false>, dim3(c, S), dim3(256), 0, st, x, p, S, part);
     MSL_CHECK_LAUNCH();
   }
   BnArgs a;
@@ -237,22 +327,28 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   a.save_invstd = save_invstd;
   a.num_batches = num_batches_tracked;
   a.part = part;
+  a.C = c;
   a.P = p;
   a.S = S;
+  a.chunk = bn_flat_chunk(p);
   a.relu = relu;
   a.training = training;
   a.update_running = update_running;
   a.eps = eps;
   a.momentum = momentum;
-  hipLaunchKernelGGL(k_bn_apply, dim3(c, S), dim3(256), 0, st, a);
+  const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
+  if (vec)
+    hipLaunchKernelGGL(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_bn_apply<false>, dim3(blocks), dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
 
 int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gamma,
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
-               float* dgamma, float* dbeta, int c, int p, int training, int relu, void* ws,
-               size_t ws_bytes, msl_stream_t stream) {
+               float* dgamma, float* dbeta, int c, int p, int training, int relu,
+               int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || (relu && !y)) return MSL_ERR_ARG;
   if (ws_bytes < msl_bn_workspace(c, p)) return MSL_ERR_WORKSPACE;
   hipStream_t st = as_stream(stream);
@@ -269,13 +365,24 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
   a.dgamma = dgamma;
   a.dbeta = dbeta;
   a.part = (double*)ws;
+  a.C = c;
   a.P = p;
   a.S = S;
+  a.chunk = bn_flat_chunk(p);
   a.relu = relu;
   a.training = training;
-  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(c, S), dim3(256), 0, st, a);
-  MSL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(c, S), dim3(256), 0, st, a);
+  a.accumulate = accumulate_params;
+  const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
+  const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
+  if (vec) {
+    hipLaunchKernelGGL(k_bn_bwd_reduce<true>, dim3(c, S), dim3(256), 0, st, a);
+    MSL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_bn_bwd_apply<true>, dim3(blocks), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(c, S), dim3(256), 0, st, a);
+    MSL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_bn_bwd_apply<false>, dim3(blocks), dim3(256), 0, st, a);
+  }
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }

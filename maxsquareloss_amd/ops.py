@@ -20,6 +20,26 @@ def _check_act(x, name):
     return x.contiguous()
 
 
+# --------------------------------------------------------------------------- gradient sinks
+def grad_sink(p):
+    """(grad view, FlatGrads, index) when `p`'s .grad is its slice of the optimizer's flat buffer.
+
+    The backward of a HIP op then accumulates the weight gradient straight into that slice (the
+    wgrad / BN kernels have an accumulate mode), notifies the flat buffer as AccumulateGrad's
+    hook would (the data-parallel reducer listens there), and returns None for the parameter -
+    saving autograd's separate `grad += new` kernel per parameter per backward.  Only for
+    .backward()-driven training: torch.autograd.grad() on such a parameter would see None.
+    """
+    s = getattr(p, "_msl_flat", None)
+    if s is None or p.grad is None or torch.is_grad_enabled():
+        return None
+    fg, i = s
+    g = p.grad
+    if g.data_ptr() != fg.flat.data_ptr() + 4 * int(fg.offsets[i]):
+        return None
+    return g, fg, i
+
+
 # --------------------------------------------------------------------------- packing cache
 class PackCache:
     """Packed copies of a conv's weights, rebuilt when any weight changes.
@@ -122,10 +142,17 @@ class _DConv3x3(Function):
             hip.check(lib.msl_dconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin,
                                           cout, h, w, dil0, d1, hip.counters(x.device).data_ptr(),
                                           ws.data_ptr(), wsb, s), "msl_dconv_dgrad")
-        dw_all = torch.empty((nb, cout, cin, 3, 3), dtype=_f32, device=x.device)
-        db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
+        sink = grad_sink(weights[0]) if (nb == 1 and not has_bias and ctx.needs_input_grad[1]) else None
         wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w)
         ws = hip.workspace(wsb, x.device)
+        if sink is not None:
+            g, fg, i = sink
+            hip.check(lib.msl_dconv_wgrad(x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w,
+                                          dil0, 0, 1, ws.data_ptr(), wsb, s), "msl_dconv_wgrad")
+            fg.notify(i)
+            return dx, None, None, None, None, None, None, None
+        dw_all = torch.empty((nb, cout, cin, 3, 3), dtype=_f32, device=x.device)
+        db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
         hip.check(lib.msl_dconv_wgrad(x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb,
                                       cin, cout, h, w, dil0, d1, 0, ws.data_ptr(), wsb, s), "msl_dconv_wgrad")
         dw0 = dw_all[0]
@@ -492,6 +519,7 @@ class _BNAct(Function):
                                  float(momentum), float(eps), int(bool(relu)), ws.data_ptr(), wsb, hip.stream_ptr()),
                   "msl_bn_fwd")
         ctx.save_for_backward(x, weight, y if relu else None, save_mean, save_invstd)
+        ctx.bias = bias
         ctx.meta = (c, p, bool(training), bool(relu))
         return y
 
@@ -503,14 +531,25 @@ class _BNAct(Function):
         lib = hip.load()
         nig = ctx.needs_input_grad
         dx = torch.empty_like(x) if nig[0] else None
-        dgamma = torch.empty(c, dtype=_f32, device=x.device) if nig[1] else None
-        dbeta = torch.empty(c, dtype=_f32, device=x.device) if nig[2] else None
         dres = torch.empty_like(x) if nig[3] else None
+        sw = grad_sink(weight) if nig[1] else None
+        sb = grad_sink(ctx.bias) if nig[2] else None
+        direct = sw is not None and sb is not None
+        if direct:
+            dgamma, dbeta = sw[0], sb[0]
+        else:
+            dgamma = torch.empty(c, dtype=_f32, device=x.device) if nig[1] else None
+            dbeta = torch.empty(c, dtype=_f32, device=x.device) if nig[2] else None
         wsb = lib.msl_bn_workspace(c, p)
         ws = hip.workspace(wsb, x.device)
         hip.check(lib.msl_bn_bwd(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight), save_mean.data_ptr(),
                                  save_invstd.data_ptr(), hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta),
-                                 c, p, int(training), int(relu), ws.data_ptr(), wsb, hip.stream_ptr()), "msl_bn_bwd")
+                                 c, p, int(training), int(relu), int(direct), ws.data_ptr(), wsb, hip.stream_ptr()),
+                  "msl_bn_bwd")
+        if direct:
+            sw[1].notify(sw[2])
+            sb[1].notify(sb[2])
+            dgamma = dbeta = None
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
 
 

@@ -58,13 +58,23 @@ class FlatGrads:
         for i, p in enumerate(self.params):
             p.grad = self.flat[self.offsets[i]:self.offsets[i + 1]].view_as(p)
             p.register_post_accumulate_grad_hook(self._make_hook(i))
+            # lets the HIP ops accumulate this parameter's gradient in place (ops.grad_sink)
+            p._msl_flat = (self, i)
 
     def _make_hook(self, i):
         def hook(_p):
-            self.used[i] = True
-            for fn in self.listeners:
-                fn(i)
+            self.notify(i)
         return hook
+
+    def notify(self, i):
+        """Parameter i's gradient for this backward is complete (AccumulateGrad's hook, or a
+        HIP op that accumulated it directly into the flat buffer)."""
+        self.used[i] = True
+        for fn in self.listeners:
+            fn(i)
+
+    def view(self, i):
+        return self.flat[self.offsets[i]:self.offsets[i + 1]]
 
     def zero_(self):
         self.flat.zero_()
