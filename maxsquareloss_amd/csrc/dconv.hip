@@ -93,11 +93,11 @@ __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long 
 }
 
 // ---------------------------------------------------------------- planning
-// Forward form (fwd and dgrad).  Unbiased GEMMs with M >= 128 run stream-K (k_igemm_fwd_sk,
-// 128x128 tiles, two K-steps per LDS stage, 512 persistent workgroups = 2 per CU): every CU
-// gets the same number of MFMA stages whatever the tile count.  The ASPP forward (M = 19
-// classes, bias) keeps the split-K tile kernel with 64-row tiles.
-constexpr int kSkBM = 128, kSkBN = 128, kSkNW = 512;
+// Forward form (fwd and dgrad) runs stream-K (k_igemm_fwd_sk): 128-pixel tiles of 128, 64 or
+// 32 rows (by M: the ASPP forward has 19 classes), two K-steps per LDS stage, up to 512
+// persistent workgroups (2 per CU), so every CU gets the same number of MFMA stages whatever
+// the tile count.  The split-K tile kernel remains for an odd K-step count with M <= 32.
+constexpr int kSkBN = 128, kSkNW = 512;
 constexpr int kMaxCounters = 65536;  // stream-K arrival counters (one per output tile)
 
 struct FwdPlan {
@@ -119,10 +119,11 @@ static int choose_split(int tiles, int ksteps, int min_steps) {
 static FwdPlan plan_fwd(int nbranch, int taps, int cimg, int M, int P, bool has_bias) {
   FwdPlan pl;
   const int groups = nbranch * cdiv(cimg, kCB) * taps;
-  pl.sk = M >= kSkBM && !has_bias;
+  const int bm = M > 64 ? 128 : (M > 32 ? 64 : 32);
+  pl.sk = groups % 2 == 0 || bm > 32;
   if (pl.sk) {
     pl.G = groups % 2 == 0 ? 2 : 1;
-    pl.bm = kSkBM;
+    pl.bm = bm;
     pl.bn = kSkBN;
     pl.bk = pl.G * kCB;
     pl.tiles_m = cdiv(M, pl.bm);
@@ -168,7 +169,7 @@ static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P) {
 // a caller-owned, persistent int[kMaxCounters] that is zero on entry and left zero on exit (the
 // finishing workgroup of each tile re-arms its counter), so no per-call memset is needed.
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
-  if (pl.sk) return (size_t)kSkNW * 2 * kSkBM * kSkBN * sizeof(float);
+  if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float);
   return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
 }
 
@@ -214,10 +215,22 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         (long long)pl.ksteps * kCB * a.lda >= (1LL << 29))
       return MSL_ERR_SHAPE;  // 32-bit index arithmetic in the kernel
     sk.T = (int)T;
-    if (pl.G == 2)
-      hipLaunchKernelGGL((k_igemm_fwd_sk<kSkBM, kSkBN, 2, 2, 2, 2>), dim3(sk.NW), dim3(256), 0, st, a, sk);
-    else
-      hipLaunchKernelGGL((k_igemm_fwd_sk<kSkBM, kSkBN, 1, 3, 2, 2>), dim3(sk.NW), dim3(256), 0, st, a, sk);
+    a.C = out;
+    a.bias = bias;
+    const dim3 grid(sk.NW), block(256);
+    if (pl.bm == 128) {
+      if (pl.G == 2)
+        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2>), grid, block, 0, st, a, sk);
+      else
+        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2>), grid, block, 0, st, a, sk);
+    } else if (pl.bm == 64) {
+      if (pl.G == 2)
+        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2>), grid, block, 0, st, a, sk);
+      else
+        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2>), grid, block, 0, st, a, sk);
+    } else {
+      hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4>), grid, block, 0, st, a, sk);
+    }
     MSL_CHECK_LAUNCH();
     return MSL_OK;
   }

@@ -479,7 +479,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   constexpr int BK = G * kCB;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
-  static_assert(BN % 64 == 0 && BM % 64 == 0, "tiles");
+  static_assert(BN % 64 == 0 && BM % 32 == 0, "tiles");
   constexpr int A_STAGE = BK * BM, STAGE = A_STAGE + BK * BN;
   constexpr int A_ROWS_PER_INST = 256 / BM;
   constexpr int A_INST = BK / A_ROWS_PER_INST;
@@ -666,10 +666,11 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
             }
       }
     }
-    // finishing workgroup (or sole worker of the tile): final output through a buffer resource - rows past M
-    // fall outside the descriptor and are dropped; columns past P get an out-of-range offset.
+    // finishing workgroup (or sole worker of the tile): final output (+ the summed branch biases)
+    // through a buffer resource; columns past P get an out-of-range offset, rows past M too.
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
+    const bool full_m = m0 + BM <= a.M;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -679,8 +680,18 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
         const unsigned voff = n < a.P ? (unsigned)((mrow * a.P + n) * 4) : OOB;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int soff = ((r & 3) + 8 * (r >> 2)) * a.P * 4;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rc, voff, soff, 0);
+          const int ro = (r & 3) + 8 * (r >> 2);
+          float v = acc[i][j][r];
+          if (a.bias && mrow + ro < a.M) {
+            float bsum = a.bias[mrow + ro];
+            for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + mrow + ro];
+            v += bsum;
+          }
+          if (full_m)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, voff, ro * a.P * 4, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
+                                                  mrow + ro < a.M ? voff + ro * a.P * 4 : OOB, 0, 0);
         }
       }
   }
