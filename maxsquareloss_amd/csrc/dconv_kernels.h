@@ -6,6 +6,8 @@
 namespace msl {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;  // buffer-op cache policy: sc1 (bypass L1, drop from L2 on store)
 
 constexpr int kCB = 16;        // image channels per forward K-group (one tap, 16 channels)
 constexpr int kPackPad = 128;  // packed-weight row padding (>= any BM)
@@ -453,10 +455,11 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
 // equal ranges, one per persistent workgroup (NW = CUs x resident workgroups per CU), so every
 // CU gets the same MFMA work whatever the tile count (65x129 maps give 132 or 264 tiles, which
 // split-K can only spread over 256 CUs unevenly).  A tile cut by range boundaries is finished by
-// whichever of its workgroups arrives LAST: every piece is published (plain stores, vmcnt(0),
-// barrier, agent-scope release fence, then an agent-scope fetch_add on the tile's counter); the
-// workgroup that sees count == pieces-1 does an agent-scope acquire and sums all pieces in worker
-// order (MI355X_MICROARCH.md, inter-workgroup visibility).  Nothing ever waits on another
+// whichever of its workgroups arrives LAST: every piece is published (sc1 stores, vmcnt(0),
+// barrier, then one agent-scope fetch_add on the tile's counter); the workgroup that sees
+// count == pieces-1 sums all pieces (sc1 loads) in worker order (MI355X_MICROARCH.md,
+// inter-workgroup visibility: the sc1 hand-off needs no L2 write-back or invalidate, which the
+// agent release / acquire fences would cost once per piece).  Nothing ever waits on another
 // workgroup, so the kernel needs no co-residency and no dispatch-order assumption, and the sum
 // order - hence the result - does not depend on which workgroup came last.
 struct SkArgs {
@@ -611,36 +614,44 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 
     constexpr int PSZ = BM * BN;
     if (k_a > 0 || k_b < sk.KS) {
-      // a piece of a split tile: slot 0 = a piece that starts inside the tile (first segment of
-      // the range), slot 1 = the tile's head piece (last segment of the range)
-      float4* pp = reinterpret_cast<float4*>(sk.part + ((long long)w * 2 + (k_a > 0 ? 0 : 1)) * PSZ) +
-                   (wid * 64 + lane) * 4;
+      // A piece of a split tile: slot 0 = a piece that starts inside the tile (first segment of
+      // the range), slot 1 = the tile's head piece (last segment of the range).  Hand-off without
+      // L2 write-back / invalidate (MI355X_MICROARCH.md, sc1 hand-off table, first row): pieces
+      // are stored and loaded with sc1 16-B buffer ops, every storing wave waits vmcnt(0),
+      // a barrier, then ONE lane adds to the tile's counter; the workgroup whose add returns
+      // pieces-1 is the last one and loads after a barrier.
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)sk.part, (short)0, (int)min(0x7fffffffLL, (long long)sk.NW * 2 * PSZ * 4), 0x00020000);
+      const unsigned lane_off = (unsigned)((wid * 64 + lane) * 4 * 16);
+      {
+        const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4) + lane_off;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+          for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            pp[(i * TN + j) * 1024 + q] = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1],
-                                                       acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+            for (int q = 0; q < 4; ++q) {
+              u32x4 v;
+              v.x = __float_as_uint(acc[i][j][4 * q]);
+              v.y = __float_as_uint(acc[i][j][4 * q + 1]);
+              v.z = __float_as_uint(acc[i][j][4 * q + 2]);
+              v.w = __float_as_uint(acc[i][j][4 * q + 3]);
+              __builtin_amdgcn_raw_buffer_store_b128(v, rp, pbase + ((i * TN + j) * 1024 + q) * 16, 0, kSc1);
+            }
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       const int w_lo = sk_worker_of(t * sk.KS, T, sk.NW);
       const int w_hi = sk_worker_of((t + 1) * sk.KS - 1, T, sk.NW);
       __shared__ int last;
       if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int old = __hip_atomic_fetch_add(sk.flags + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = old == w_hi - w_lo;
-        if (last) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          __hip_atomic_store(sk.flags + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-        }
+        if (last) __hip_atomic_store(sk.flags + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
       }
       __syncthreads();
       if (!last) continue;
       // every piece is in: sum them in worker order (independent of arrival order)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -650,19 +661,18 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 #pragma unroll 1
       for (int wc = w_lo; wc <= w_hi; ++wc) {
         const int slot = sk_start(wc, T, sk.NW) > t * sk.KS ? 0 : 1;
-        const float4* pc = reinterpret_cast<const float4*>(sk.part + ((long long)wc * 2 + slot) * PSZ) +
-                           (wid * 64 + lane) * 4;
+        const unsigned pbase = (unsigned)((wc * 2 + slot) * PSZ * 4) + lane_off;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const float4 v = pc[(i * TN + j) * 1024 + q];
-              acc[i][j][4 * q] += v.x;
-              acc[i][j][4 * q + 1] += v.y;
-              acc[i][j][4 * q + 2] += v.z;
-              acc[i][j][4 * q + 3] += v.w;
+              const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, pbase + ((i * TN + j) * 1024 + q) * 16, 0, kSc1);
+              acc[i][j][4 * q] += __uint_as_float(v.x);
+              acc[i][j][4 * q + 1] += __uint_as_float(v.y);
+              acc[i][j][4 * q + 2] += __uint_as_float(v.z);
+              acc[i][j][4 * q + 3] += __uint_as_float(v.w);
             }
       }
     }

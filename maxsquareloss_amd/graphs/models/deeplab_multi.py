@@ -18,9 +18,11 @@ What runs where:
   - every BatchNorm (train mode, batch statistics of the one image, Q9) fused with the
     following ReLU and, for bn3, the residual add -> HIP kernels with fp64-accumulated
     statistics (MIOpen's single-pass variance is not accurate enough at bs=1);
-  - 1x1 convs: `PointwiseConv` (the same HIP GEMM kernels with one unshifted tap) exists
-    behind USE_HIP_POINTWISE; by default they, the stem 7x7 conv and maxpool run on
-    PyTorch-ROCm (MIOpen/rocBLAS), which is faster on them today - SURVEY.md §8f row 1.
+  - stride-1 1x1 convs -> `PointwiseConv`: three plain GEMMs on the fastest library per GEMM
+    (MIOpen/rocBLAS, hipBLASLt; the HIP pointwise kernels behind USE_HIP_POINTWISE), weight
+    gradients accumulated in place into the flat gradient buffer;
+  - stem 7x7 conv, the two stride-2 1x1 convs of layer2 block 0, maxpool -> PyTorch-ROCm
+    (MIOpen), SURVEY.md §8f row 1.
 """
 import torch
 import torch.nn as nn
@@ -42,26 +44,28 @@ class DilatedConv3x3(nn.Conv2d):
         return ops.dconv3x3(x, self.weight, self.dilation[0], self._pack)
 
 
+# The HIP pointwise GEMMs run at 45-90 TFLOP/s on these shapes; the library FP32 GEMMs reach
+# 85-145 on most of them (scripts/bench_pconv.py, scripts/bench_mm.py, profiles/).  By default
+# a stride-1 1x1 conv therefore runs each of its three GEMMs on the fastest library
+# (ops.conv1x1); USE_HIP_POINTWISE switches all three to the HIP kernels (parity-tested).
+USE_HIP_POINTWISE = False
+
+
 class PointwiseConv(nn.Conv2d):
-    """nn.Conv2d(cin, cout, 1, stride=1, bias=False) on the HIP kernels."""
+    """nn.Conv2d(cin, cout, 1, stride=1, bias=False): ops.conv1x1, or the HIP pointwise kernels."""
 
     def __init__(self, in_channels, out_channels):
         super().__init__(in_channels, out_channels, kernel_size=1, stride=1, bias=False)
         self._pack = ops.PackCache(pointwise=True)
 
     def forward(self, x):
-        return ops.pconv(x, self.weight, self._pack)
-
-
-# The HIP pointwise GEMMs run at 45-90 TFLOP/s on these shapes; rocBLAS's tuned FP32 GEMMs
-# (behind MIOpen) reach 85-113 on the forward and data gradient (scripts/bench_pconv.py,
-# profiles/).  Until the HIP core catches up the model keeps MIOpen for the 1x1 convs;
-# PointwiseConv stays available (and parity-tested) behind this switch.
-USE_HIP_POINTWISE = False
+        if USE_HIP_POINTWISE:
+            return ops.pconv(x, self.weight, self._pack)
+        return ops.conv1x1(x, self.weight, self._pack)
 
 
 def conv1x1(inplanes, planes, stride):
-    if stride == 1 and USE_HIP_POINTWISE:
+    if stride == 1:
         return PointwiseConv(inplanes, planes)
     return nn.Conv2d(inplanes, planes, kernel_size=1, stride=stride, bias=False)
 

@@ -6,6 +6,7 @@ reference only runs bs=1: IW_MaxSquareloss broadcasts (N,H,W) weights against
 (N,C,H,W) probabilities, which only works for N=1 - SURVEY.md quirk Q3).
 """
 import torch
+import torch.nn.functional as F
 from torch.autograd import Function
 
 from . import hip
@@ -225,6 +226,70 @@ class _PConv(Function):
 def pconv(x, weight, cache):
     """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99)."""
     return _PConv.apply(x, weight, cache)
+
+
+# --------------------------------------------------------------------------- 1x1 conv, library GEMMs
+class _Conv1x1(Function):
+    """1x1, stride-1, bias-free conv as three plain GEMMs, each on the library that is fastest for
+    it on MI355X (scripts/bench_mm.py, profiles/r01_gemm_libraries.txt):
+      y  = W x        MIOpen (rocBLAS kernels)
+      dx = W^T dy     hipBLASLt (torch.mm) when cout > cin, else MIOpen
+      dW += dy x^T    hipBLASLt addmm straight into the flat gradient buffer (beta = 1), or the
+                      HIP pointwise wgrad at the 33k-pixel layer1 maps where it is the fastest.
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, cache):
+        y = F.conv2d(x, weight)
+        ctx.save_for_backward(x, weight)
+        ctx.cache = cache
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        cout, cin = weight.shape[0], weight.shape[1]
+        h, w = x.shape[2], x.shape[3]
+        p = h * w
+        gy = gy.contiguous()
+        g2 = gy.view(cout, p)
+        x2 = x.view(cin, p)
+        w2 = weight.view(cout, cin)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if cout > cin:
+                dx = torch.mm(w2.t(), g2).view(1, cin, h, w)
+            else:
+                dx = torch.ops.aten.convolution_backward(gy, x, weight, None, (1, 1), (0, 0), (1, 1), False,
+                                                         (0, 0), 1, (True, False, False))[0]
+        if not ctx.needs_input_grad[1]:
+            return dx, None, None
+        sink = grad_sink(weight)
+        if p > 16384:
+            # HIP pointwise wgrad (accumulating into the flat buffer when it can)
+            lib = hip.load()
+            dst = sink[0] if sink is not None else torch.empty_like(weight)
+            wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
+            ws = hip.workspace(wsb, x.device)
+            hip.check(lib.msl_pconv_wgrad(x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p,
+                                          int(sink is not None), ws.data_ptr(), wsb, hip.stream_ptr()),
+                      "msl_pconv_wgrad")
+            if sink is None:
+                return dx, dst, None
+        elif sink is not None:
+            sink[0].view(cout, cin).addmm_(g2, x2.t())
+        else:
+            return dx, torch.mm(g2, x2.t()).view_as(weight), None
+        sink[1].notify(sink[2])
+        return dx, None, None
+
+
+def conv1x1(x, weight, cache):
+    """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99)."""
+    x = _check_act(x, "conv1x1")
+    if weight.shape[2:] != (1, 1) or x.size(1) != weight.shape[1]:
+        raise hip.MSLError(f"conv1x1: weight {tuple(weight.shape)} does not match input {tuple(x.shape)}")
+    return _Conv1x1.apply(x, weight, cache)
 
 
 # --------------------------------------------------------------------------- upsample

@@ -66,10 +66,11 @@ float run_sk(const Shape& sh, const float* x, const float* wp, float* y, float* 
   return ms / iters;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool big_only = argc > 1;
   const int iters = 20;
   // (cimg, M, P): fwd of conv1/conv3/downsample and the dgrad forms (cimg = cout, M = cin)
-  Shape shapes[] = {{1024, 256, 8385}, {256, 1024, 8385}, {512, 1024, 8385}, {2048, 512, 8385},
+  Shape shapes[] = {{4096, 4096, 4096}, {1024, 256, 8385}, {256, 1024, 8385}, {512, 1024, 8385}, {2048, 512, 8385},
                     {512, 2048, 8385}, {1024, 2048, 8385}, {256, 64, 33153}, {64, 256, 33153}};
   for (const Shape& sh : shapes) {
     const int lda = (sh.M + 127) / 128 * 128;
@@ -99,6 +100,7 @@ int main() {
     }
     SK(64, 128, 2, 2, true, 512) SK(64, 128, 2, 3, true, 512) SK(64, 128, 1, 4, true, 768)
     CK(hipFree(x)); CK(hipFree(wp)); CK(hipFree(y)); CK(hipFree(yref)); CK(hipFree(ws)); CK(hipFree(flags));
+    if (big_only) break;
   }
   return 0;
 }

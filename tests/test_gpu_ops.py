@@ -77,6 +77,27 @@ def test_pconv_fwd_bwd(cin, cout, h, w):
     assert _rel(y2, -2.0 * yr.detach()) < 1e-5
 
 
+@pytest.mark.parametrize("cin,cout,h,w", [(64, 256, 129, 257), (256, 64, 129, 257), (1024, 256, 65, 129),
+                                           (256, 1024, 65, 129), (512, 2048, 17, 33)])
+def test_conv1x1_library_gemms(cin, cout, h, w):
+    """ops.conv1x1: MIOpen / hipBLASLt / HIP-wgrad mix, every gradient against fp64."""
+    g = torch.Generator().manual_seed(cin + 5 * cout)
+    x = torch.randn(1, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 1, 1, generator=g) * 0.05
+    gy = torch.randn(1, cout, h, w, generator=g)
+    xr, wr = x.double().requires_grad_(), wt.double().requires_grad_()
+    yr = F.conv2d(xr, wr)
+    yr.backward(gy.double())
+    xg = x.to(DEV).requires_grad_()
+    wg = wt.to(DEV).requires_grad_()
+    y = ops.conv1x1(xg, wg, ops.PackCache(pointwise=True))
+    y.backward(gy.to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 1e-5
+    assert _rel(xg.grad, xr.grad) < 1e-5
+    assert _rel(wg.grad, wr.grad) < 1e-5
+
+
 @pytest.mark.parametrize("cin,c,h,w", [(1024, 19, 17, 33), (2048, 19, 33, 65), (96, 16, 9, 17), (64, 13, 65, 129)])
 def test_aspp2_fwd_bwd(cin, c, h, w):
     g = torch.Generator().manual_seed(cin + c)
