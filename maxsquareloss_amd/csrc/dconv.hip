@@ -12,7 +12,8 @@
 //
 // GEMM mapping (MFMA v_mfma_f32_32x32x2_f32: exact f32 FMA chains):
 //   forward / dgrad:  C[m][p] = sum_k A[k][m] * B[k][p]
-//       k = ((branch*ncb + cb)*9 + tap)*16 + ci_local  (one tap, 16 channels per K-step)
+//       k = ((branch*9 + tap)*ncb + cb)*16 + ci_local  (one tap, 16 channels per K-step;
+//       tap-major, so the shifted-pixel offsets change only every ncb K-steps)
 //       A = packed weights [Kp][lda] (m contiguous; dgrad: transposed + tap-flipped)
 //       B = image[cb*16 + ci_local][p + shift(tap)]  (zero outside the image)
 //   wgrad (one GEMM per tap, batched over grid.z):
@@ -63,7 +64,7 @@ __global__ void __launch_bounds__(256) k_bias_grad(const float* __restrict__ dy,
 // Packed operand for the forward-form GEMM.
 //   for_dgrad = 0: image = x (cin channels),  m = co: P[k][co] = W[co][ci][t]
 //   for_dgrad = 1: image = dy (cout channels), m = ci: P[k][ci] = W[co][ci][8 - t]
-// k = ((b*ncb + cb)*taps + t)*16 + c_local with c = cb*16 + c_local (image channel); taps = 9
+// k = ((b*taps + t)*ncb + cb)*16 + c_local with c = cb*16 + c_local (image channel); taps = 9
 // for the 3x3 convs, 1 for the pointwise ones.
 __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long long branch_stride,
                                                int cin, int cout, int for_dgrad, int ncb, int lda,
@@ -75,10 +76,10 @@ __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long 
     const long long k = e / lda;
     const int cl = (int)(k % kCB);
     const long long q = k / kCB;
-    const int t = (int)(q % taps);
-    const long long q2 = q / taps;
-    const int cb = (int)(q2 % ncb);
-    const int b = (int)(q2 / ncb);
+    const int cb = (int)(q % ncb);
+    const long long q2 = q / ncb;
+    const int t = (int)(q2 % taps);
+    const int b = (int)(q2 / taps);
     const int c = cb * kCB + cl;
     float v = 0.f;
     if (c < cimg && m < mreal) {
@@ -218,18 +219,25 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     a.C = out;
     a.bias = bias;
     const dim3 grid(sk.NW), block(256);
+    const dim3 rgrid(pl.bm * kSkBN / 1024, pl.tiles_m * pl.tiles_n);
     if (pl.bm == 128) {
       if (pl.G == 2)
         hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2>), grid, block, 0, st, a, sk);
       else
         hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2>), grid, block, 0, st, a, sk);
+      MSL_CHECK_LAUNCH();
+      hipLaunchKernelGGL((k_sk_reduce<128, kSkBN, 2, 2>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
       if (pl.G == 2)
         hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2>), grid, block, 0, st, a, sk);
       else
         hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2>), grid, block, 0, st, a, sk);
+      MSL_CHECK_LAUNCH();
+      hipLaunchKernelGGL((k_sk_reduce<64, kSkBN, 2, 2>), rgrid, block, 0, st, a, sk);
     } else {
       hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4>), grid, block, 0, st, a, sk);
+      MSL_CHECK_LAUNCH();
+      hipLaunchKernelGGL((k_sk_reduce<32, kSkBN, 1, 4>), rgrid, block, 0, st, a, sk);
     }
     MSL_CHECK_LAUNCH();
     return MSL_OK;

@@ -69,6 +69,11 @@ __device__ __forceinline__ void mfma_stage_pipe(const float* __restrict__ As, co
   constexpr int KP = BK / 2;
   float av[2][TM], bv[2][TN];
   auto load = [&](int kp, int buf) {
+#ifdef MSL_SK_NOLDS  // tuning-harness experiment only: operands from registers, no LDS reads
+    for (int i = 0; i < TM; ++i) av[buf][i] = __int_as_float(lane + kp + i);
+    for (int j = 0; j < TN; ++j) bv[buf][j] = __int_as_float(lane * 3 + kp + j);
+    return;
+#endif
     const int kr = 2 * kp + kh;
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[buf][i] = As[kr * LDA_S + wm + i * 32 + l32];
@@ -137,8 +142,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
       const int q = s * G + g;  // tap-group index
       const int b = q / per_b;
       const int rem = q - b * per_b;
-      const int cb = rem / a.taps;
-      const int t = rem - cb * a.taps;
+      const int t = rem / a.ncb;
+      const int cb = rem - t * a.ncb;
       const int d = b ? a.dil1 : a.dil0;
       const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
       const bool v = pin && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
@@ -376,8 +381,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
     float* Bs = As + A_STAGE;
     const int b = s / per_b;
     const int rem = s - b * per_b;
-    const int cb = rem / a.taps;
-    const int t = rem - cb * a.taps;
+    const int t = rem / a.ncb;
+    const int cb = rem - t * a.ncb;
     const int d = b ? a.dil1 : a.dil0;
     const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
     // A: wave wid loads instructions wid*A_INST_W .. ; each covers A_ROWS_PER_INST rows
@@ -454,17 +459,13 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
 // Stream-K forward form.  The (tile, stage) iteration space of all output tiles is cut into NW
 // equal ranges, one per persistent workgroup (NW = CUs x resident workgroups per CU), so every
 // CU gets the same MFMA work whatever the tile count (65x129 maps give 132 or 264 tiles, which
-// split-K can only spread over 256 CUs unevenly).  A tile cut by range boundaries is finished by
-// whichever of its workgroups arrives LAST: every piece is published (sc1 stores, vmcnt(0),
-// barrier, then one agent-scope fetch_add on the tile's counter); the workgroup that sees
-// count == pieces-1 sums all pieces (sc1 loads) in worker order (MI355X_MICROARCH.md,
-// inter-workgroup visibility: the sc1 hand-off needs no L2 write-back or invalidate, which the
-// agent release / acquire fences would cost once per piece).  Nothing ever waits on another
-// workgroup, so the kernel needs no co-residency and no dispatch-order assumption, and the sum
-// order - hence the result - does not depend on which workgroup came last.
+// split-K can only spread over 256 CUs unevenly).  A tile cut by range boundaries leaves one
+// piece per workgroup that touched it; k_sk_reduce (the next launch on the stream) sums them in
+// worker order.  Nothing ever waits on another workgroup, so the kernel needs no co-residency
+// and no dispatch-order assumption, and the sum order - hence the result - is fixed.
 struct SkArgs {
-  float* part;     // [NW][2][BM*BN] published pieces (accumulator register order, lane-contiguous)
-  int* flags;      // [tiles] arrival counters, zero at launch; the finishing workgroup re-arms them
+  float* part;     // [NW][2][BM*BN] pieces of split tiles (accumulator register order, lane-contiguous)
+  int* flags;      // unused (kept for the C-ABI's caller-owned counter array)
   int tiles_m, tiles_n, KS, NW;
   int T;           // tiles * KS  (T * NW < 2^31, checked by the planner)
 };
@@ -493,6 +494,9 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   constexpr int INST_W = A_INST_W + G * BG_INST_W;
   static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
   static_assert((STAGES - 2) * INST_W < 64, "vmcnt range");
+  // ONE __shared__ object: a second one (even a 4-byte flag) makes hipcc emit vmcnt(0) before the
+  // first ds_read after every DMA issue, which drains the in-flight stage (cdna_hip_programming.md
+  // §5, M = 256 item 4(a)).
   __shared__ __attribute__((aligned(16))) float smem[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -508,8 +512,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       (void*)a.A, (short)0, (int)min(0x7fffffffLL, (long long)sk.KS * BK * a.lda * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
-  const int per_b = a.ncb * a.taps;
   constexpr unsigned OOB = 0x80000000u;
+  const unsigned chan_bytes = (unsigned)a.P * 4u;
 
   f32x16 acc[TM][TN];
   for (int it = it_begin; it < it_end;) {
@@ -520,6 +524,15 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
     it += nst;
     const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
     const int m0 = tm * BM, n0 = tn * BN;
+    // per-lane constants of this tile: A byte offsets (stage 0), pixel coordinates
+    unsigned a_off[A_INST_W];
+#pragma unroll
+    for (int i = 0; i < A_INST_W; ++i) {
+      const int inst = wid * A_INST_W + i;
+      const int row = inst * A_ROWS_PER_INST + lane / (BM / 4);
+      a_off[i] = (unsigned)((row * a.lda + m0 + (lane % (BM / 4)) * 4) * 4);
+    }
+    const unsigned a_stage_bytes = (unsigned)(BK * a.lda * 4);
     int py[NH], px[NH];
     bool pin[NH];
 #pragma unroll
@@ -529,30 +542,45 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       py[h] = p / a.W;
       px[h] = p - py[h] * a.W;
     }
+    // Issue cursor over the K-steps, in order (K is tap-major: ks = (branch*taps + tap)*ncb + cb):
+    // the wave-uniform (tap, channel block) advances incrementally and the per-lane shifted pixel
+    // offsets (OOB outside the image) are recomputed only when the tap changes.
+    int c_cb, c_tap = -1;
+    unsigned vrow[NH];
+    {
+      const int ks0 = k_a * G;
+      const int tq = ks0 / a.ncb;  // branch*taps + tap
+      c_cb = ks0 - tq * a.ncb;
+      c_tap = tq;
+    }
+    auto set_tap = [&](int tq) {
+      const int br = tq / a.taps;
+      const int tp = tq - br * a.taps;
+      const int d = br ? a.dil1 : a.dil0;
+      const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
+      const int shift = dh * a.W + dw;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const bool v = pin[h] && (unsigned)(py[h] + dh) < (unsigned)a.H && (unsigned)(px[h] + dw) < (unsigned)a.W;
+        vrow[h] = v ? (unsigned)((n0 + h * 64 + lane + shift) * 4) : OOB;
+      }
+    };
+    set_tap(c_tap);
     auto issue = [&](int s, int slot) {
 #ifdef MSL_SK_NODMA  // tuning-harness experiment only: no operand traffic
       return;
 #endif
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
+      const unsigned a_base = (unsigned)s * a_stage_bytes;
 #pragma unroll
       for (int i = 0; i < A_INST_W; ++i) {
         const int inst = wid * A_INST_W + i;
-        const int row = inst * A_ROWS_PER_INST + lane / (BM / 4);
-        const int c4 = lane % (BM / 4);
-        const unsigned off = (unsigned)(((s * BK + row) * a.lda + m0 + c4 * 4) * 4);
-        dma_b128(ra, As + inst * 256, off);
+        dma_b128(ra, As + inst * 256, a_off[i] + a_base);
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const int ks = s * G + g;
-        const int br = ks / per_b;
-        const int rem = ks - br * per_b;
-        const int cb = rem / a.taps;
-        const int tp = rem - cb * a.taps;
-        const int d = br ? a.dil1 : a.dil0;
-        const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
-        const int cb16 = cb * kCB;
+        const int cb16 = c_cb * kCB;
         if constexpr (PW) {
           // lanes 0-31 -> row 2*inst, lanes 32-63 -> row 2*inst+1; 4 pixels per lane.  A chunk
           // that straddles P reads the next channel's first pixels: they only reach output
@@ -567,17 +595,18 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
             dma_b128(rb, Bs + (g * kCB + inst * 2) * BN, v ? e * 4u : OOB);
           }
         } else {
-          const int shift = dh * a.W + dw;
 #pragma unroll
           for (int j = 0; j < BG_INST_W; ++j) {
             const int inst = wid * BG_INST_W + j;
-            const int r = inst / NH, h = inst % NH;
+            const int r = inst / NH, h = inst % NH;  // wave-uniform
             const int ci = cb16 + r;
-            const bool v = pin[h] && ci < a.cimg && (unsigned)(py[h] + dh) < (unsigned)a.H &&
-                           (unsigned)(px[h] + dw) < (unsigned)a.W;
-            const unsigned e = (unsigned)(ci * a.P + (n0 + h * 64 + lane) + shift);
-            dma_b32(rb, Bs + (g * kCB + r) * BN + h * 64, v ? e * 4u : OOB);
+            const unsigned cofs = ci < a.cimg ? (unsigned)ci * chan_bytes : OOB;  // scalar
+            dma_b32(rb, Bs + (g * kCB + r) * BN + h * 64, vrow[h] + cofs);
           }
+        }
+        if (++c_cb == a.ncb) {
+          c_cb = 0;
+          if (++c_tap * a.ncb < a.ksteps) set_tap(c_tap);  // (past the last K-step: nothing to set)
         }
       }
     };
@@ -613,70 +642,36 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
     }
 
     constexpr int PSZ = BM * BN;
+#ifdef MSL_SK_NOFIX  // tuning-harness experiment only: every piece stores as if it were the whole tile
+    if (false) {
+#else
     if (k_a > 0 || k_b < sk.KS) {
+#endif
       // A piece of a split tile: slot 0 = a piece that starts inside the tile (first segment of
-      // the range), slot 1 = the tile's head piece (last segment of the range).  Hand-off without
-      // L2 write-back / invalidate (MI355X_MICROARCH.md, sc1 hand-off table, first row): pieces
-      // are stored and loaded with sc1 16-B buffer ops, every storing wave waits vmcnt(0),
-      // a barrier, then ONE lane adds to the tile's counter; the workgroup whose add returns
-      // pieces-1 is the last one and loads after a barrier.
+      // the range), slot 1 = the tile's head piece (last segment of the range).  Stored with
+      // plain 16-B stores in accumulator register order and summed by k_sk_reduce after this
+      // launch: no flag, no fence, no wait.  (A last-arriver fix-up inside the launch puts every
+      // tile's reduction at the very end of the kernel, where all workgroups read pieces at once
+      // with nothing to overlap: measured 38 of 135 us on the layer3 conv.)
       const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
           (void*)sk.part, (short)0, (int)min(0x7fffffffLL, (long long)sk.NW * 2 * PSZ * 4), 0x00020000);
-      const unsigned lane_off = (unsigned)((wid * 64 + lane) * 4 * 16);
-      {
-        const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4) + lane_off;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              u32x4 v;
-              v.x = __float_as_uint(acc[i][j][4 * q]);
-              v.y = __float_as_uint(acc[i][j][4 * q + 1]);
-              v.z = __float_as_uint(acc[i][j][4 * q + 2]);
-              v.w = __float_as_uint(acc[i][j][4 * q + 3]);
-              __builtin_amdgcn_raw_buffer_store_b128(v, rp, pbase + ((i * TN + j) * 1024 + q) * 16, 0, kSc1);
-            }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const int w_lo = sk_worker_of(t * sk.KS, T, sk.NW);
-      const int w_hi = sk_worker_of((t + 1) * sk.KS - 1, T, sk.NW);
-      __shared__ int last;
-      if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(sk.flags + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old == w_hi - w_lo;
-        if (last) __hip_atomic_store(sk.flags + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-      }
-      __syncthreads();
-      if (!last) continue;
-      // every piece is in: sum them in worker order (independent of arrival order)
+      const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4) + (unsigned)((wid * 64 + lane) * 64);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-#pragma unroll 1
-      for (int wc = w_lo; wc <= w_hi; ++wc) {
-        const int slot = sk_start(wc, T, sk.NW) > t * sk.KS ? 0 : 1;
-        const unsigned pbase = (unsigned)((wc * 2 + slot) * PSZ * 4) + lane_off;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, pbase + ((i * TN + j) * 1024 + q) * 16, 0, kSc1);
-              acc[i][j][4 * q] += __uint_as_float(v.x);
-              acc[i][j][4 * q + 1] += __uint_as_float(v.y);
-              acc[i][j][4 * q + 2] += __uint_as_float(v.z);
-              acc[i][j][4 * q + 3] += __uint_as_float(v.w);
-            }
-      }
+          for (int q = 0; q < 4; ++q) {
+            u32x4 v;
+            v.x = __float_as_uint(acc[i][j][4 * q]);
+            v.y = __float_as_uint(acc[i][j][4 * q + 1]);
+            v.z = __float_as_uint(acc[i][j][4 * q + 2]);
+            v.w = __float_as_uint(acc[i][j][4 * q + 3]);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rp, pbase + ((i * TN + j) * 1024 + q) * 16, 0, 0);
+          }
+      continue;
     }
-    // finishing workgroup (or sole worker of the tile): final output (+ the summed branch biases)
+    // sole worker of the tile: final output (+ the summed branch biases)
     // through a buffer resource; columns past P get an out-of-range offset, rows past M too.
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
@@ -704,6 +699,52 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
                                                   mrow + ro < a.M ? voff + ro * a.P * 4 : OOB, 0, 0);
         }
       }
+  }
+}
+
+// Sum of the pieces of every split stream-K tile (worker order: deterministic), + the branch
+// biases, into the output.  grid = (PSZ / 1024 chunks, tiles); blocks of unsplit tiles exit.
+// Thread order (ij, q, lane-slot) keeps the output stores coalesced along pixels.
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  constexpr int PSZ = BM * BN;
+  const int t = blockIdx.y;
+  const int w_lo = sk_worker_of(t * sk.KS, sk.T, sk.NW);
+  const int w_hi = sk_worker_of((t + 1) * sk.KS - 1, sk.T, sk.NW);
+  if (w_lo == w_hi) return;
+  const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float4* __restrict__ part = reinterpret_cast<const float4*>(sk.part);
+  for (int g = blockIdx.x * 256 + threadIdx.x; g < PSZ / 4; g += gridDim.x * 256) {
+    const int L = g & 255, q = (g >> 8) & 3, ij = g >> 10;
+    const int f = ij * 1024 + L * 4 + q;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int wc = w_lo; wc <= w_hi; ++wc) {
+      const int slot = sk_start(wc, sk.T, sk.NW) > t * sk.KS ? 0 : 1;
+      const float4 v = part[(long long)(wc * 2 + slot) * (PSZ / 4) + f];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    const int wid = L >> 6, lane = L & 63;
+    const int i = ij / TN, j = ij - (ij / TN) * TN;
+    const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
+    const int n = n0 + wn + j * 32 + (lane & 31);
+    const int mb = m0 + wm + i * 32 + 8 * q + 4 * (lane >> 5);
+    if (n >= a.P) continue;
+    const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int m = mb + c;
+      if (m < a.M) {
+        float v = vals[c];
+        if (a.bias) {
+          float bsum = a.bias[m];
+          for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + m];
+          v += bsum;
+        }
+        a.C[(long long)m * a.P + n] = v;
+      }
+    }
   }
 }
 

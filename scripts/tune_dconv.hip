@@ -98,6 +98,7 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
     hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, WM, WN>), dim3(NW), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_sk_reduce<BM, BN, WM, WN>), dim3(BM * BN / 1024, tiles), dim3(256), 0, 0, a, sk);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -140,6 +141,8 @@ static double maxdiff(const float* a, const float* b, size_t n, double* scale) {
 int main(int argc, char** argv) {
   // "sk": only the library's stream-K configuration on the layer3 shape (profiling runs)
   const bool sk_only = argc > 1 && std::string(argv[1]) == "sk";
+  // "fsk": every stream-K row, nothing else
+  const bool fsk_only = argc > 1 && std::string(argv[1]) == "fsk";
   const int iters = sk_only ? 5 : 20;
   Shape shapes[] = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
   for (const Shape& sh : shapes) {
@@ -180,6 +183,7 @@ int main(int argc, char** argv) {
     FSK(128, 128, 1, 2, 2, 2, 512) FSK(128, 128, 2, 2, 2, 2, 512) FSK(128, 128, 2, 2, 2, 2, 256)
     FSK(128, 128, 2, 3, 2, 2, 256) FSK(128, 128, 4, 2, 2, 2, 256)
     FSK(64, 128, 1, 3, 2, 2, 768) FSK(64, 128, 2, 2, 2, 2, 768) FSK(64, 128, 2, 2, 2, 2, 512)
+    if (fsk_only) continue;
     FDMA(128, 128, 3, 2, 2, 1) FDMA(128, 128, 3, 2, 2, 2) FDMA(128, 128, 3, 2, 2, 3) FDMA(128, 128, 3, 2, 2, 4)
     FDMA(128, 128, 3, 2, 2, 6) FDMA(128, 128, 3, 2, 2, 8)
     FDMA(64, 128, 3, 2, 2, 1) FDMA(64, 128, 3, 2, 2, 2) FDMA(64, 128, 3, 2, 2, 3) FDMA(64, 128, 3, 2, 2, 4)
