@@ -226,18 +226,18 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
       else
         hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL((k_sk_reduce<128, kSkBN, 2, 2>), rgrid, block, 0, st, a, sk);
+      hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
       if (pl.G == 2)
         hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2>), grid, block, 0, st, a, sk);
       else
         hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL((k_sk_reduce<64, kSkBN, 2, 2>), rgrid, block, 0, st, a, sk);
+      hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
     } else {
       hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL((k_sk_reduce<32, kSkBN, 1, 4>), rgrid, block, 0, st, a, sk);
+      hipLaunchKernelGGL((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
     }
     MSL_CHECK_LAUNCH();
     return MSL_OK;

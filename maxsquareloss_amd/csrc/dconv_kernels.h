@@ -464,7 +464,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
 // worker order.  Nothing ever waits on another workgroup, so the kernel needs no co-residency
 // and no dispatch-order assumption, and the sum order - hence the result - is fixed.
 struct SkArgs {
-  float* part;     // [NW][2][BM*BN] pieces of split tiles (accumulator register order, lane-contiguous)
+  float* part;     // [NW][2][BM][BN] pieces of split tiles (row-major)
   int* flags;      // unused (kept for the C-ABI's caller-owned counter array)
   int tiles_m, tiles_n, KS, NW;
   int T;           // tiles * KS  (T * NW < 2^31, checked by the planner)
@@ -489,7 +489,11 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   constexpr int A_INST = BK / A_ROWS_PER_INST;
   constexpr int A_INST_W = A_INST / 4;
   constexpr int NH = BN / 64;
+#ifdef MSL_SK_FAKEX4
+  constexpr int BG_INST_W = kCB * BN / 256 / 4;
+#else
   constexpr int BG_INST_W = PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B instructions per wave per K-step
+#endif
   static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
   constexpr int INST_W = A_INST_W + G * BG_INST_W;
   static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
@@ -581,7 +585,11 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int cb16 = c_cb * kCB;
+#ifdef MSL_SK_FAKEX4  // tuning-harness experiment only: dwordx4 B loads of unshifted rows (wrong results)
+        if constexpr (true) {
+#else
         if constexpr (PW) {
+#endif
           // lanes 0-31 -> row 2*inst, lanes 32-63 -> row 2*inst+1; 4 pixels per lane.  A chunk
           // that straddles P reads the next channel's first pixels: they only reach output
           // columns >= P, which are never stored.
@@ -648,27 +656,27 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
     if (k_a > 0 || k_b < sk.KS) {
 #endif
       // A piece of a split tile: slot 0 = a piece that starts inside the tile (first segment of
-      // the range), slot 1 = the tile's head piece (last segment of the range).  Stored with
-      // plain 16-B stores in accumulator register order and summed by k_sk_reduce after this
-      // launch: no flag, no fence, no wait.  (A last-arriver fix-up inside the launch puts every
-      // tile's reduction at the very end of the kernel, where all workgroups read pieces at once
-      // with nothing to overlap: measured 38 of 135 us on the layer3 conv.)
+      // the range), slot 1 = the tile's head piece (last segment of the range).  Stored row-major
+      // [BM][BN] with plain stores (each half-wave writes 128 contiguous bytes per register) and
+      // summed by k_sk_reduce after this launch: no flag, no fence, no wait.  (A last-arriver
+      // fix-up inside the launch puts every tile's reduction at the very end of the kernel, where
+      // all workgroups read pieces at once with nothing to overlap: 38 of 135 us on layer3.)
       const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
           (void*)sk.part, (short)0, (int)min(0x7fffffffLL, (long long)sk.NW * 2 * PSZ * 4), 0x00020000);
-      const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4) + (unsigned)((wid * 64 + lane) * 64);
+      const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TN; ++j) {
+          const int nl = wn + j * 32 + (lane & 31);
+          const int ml = wm + i * 32 + 4 * (lane >> 5);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            u32x4 v;
-            v.x = __float_as_uint(acc[i][j][4 * q]);
-            v.y = __float_as_uint(acc[i][j][4 * q + 1]);
-            v.z = __float_as_uint(acc[i][j][4 * q + 2]);
-            v.w = __float_as_uint(acc[i][j][4 * q + 3]);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rp, pbase + ((i * TN + j) * 1024 + q) * 16, 0, 0);
+          for (int r = 0; r < 16; ++r) {
+            const int ro = (r & 3) + 8 * (r >> 2);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rp,
+                                                  pbase + (unsigned)(((ml + ro) * BN + nl) * 4), 0, 0);
           }
+        }
       continue;
     }
     // sole worker of the tile: final output (+ the summed branch biases)
@@ -703,11 +711,10 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 }
 
 // Sum of the pieces of every split stream-K tile (worker order: deterministic), + the branch
-// biases, into the output.  grid = (PSZ / 1024 chunks, tiles); blocks of unsplit tiles exit.
-// Thread order (ij, q, lane-slot) keeps the output stores coalesced along pixels.
-template <int BM, int BN, int WM, int WN>
+// biases, into the output.  grid = (BM*BN / 1024 chunks, tiles); blocks of unsplit tiles exit.
+// Pieces are row-major [BM][BN]: one float4 of 4 consecutive pixels per thread.
+template <int BM, int BN>
 __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
-  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   constexpr int PSZ = BM * BN;
   const int t = blockIdx.y;
   const int w_lo = sk_worker_of(t * sk.KS, sk.T, sk.NW);
@@ -717,34 +724,24 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   const int m0 = tm * BM, n0 = tn * BN;
   const float4* __restrict__ part = reinterpret_cast<const float4*>(sk.part);
   for (int g = blockIdx.x * 256 + threadIdx.x; g < PSZ / 4; g += gridDim.x * 256) {
-    const int L = g & 255, q = (g >> 8) & 3, ij = g >> 10;
-    const int f = ij * 1024 + L * 4 + q;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int wc = w_lo; wc <= w_hi; ++wc) {
       const int slot = sk_start(wc, sk.T, sk.NW) > t * sk.KS ? 0 : 1;
-      const float4 v = part[(long long)(wc * 2 + slot) * (PSZ / 4) + f];
+      const float4 v = part[(long long)(wc * 2 + slot) * (PSZ / 4) + g];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    const int wid = L >> 6, lane = L & 63;
-    const int i = ij / TN, j = ij - (ij / TN) * TN;
-    const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
-    const int n = n0 + wn + j * 32 + (lane & 31);
-    const int mb = m0 + wm + i * 32 + 8 * q + 4 * (lane >> 5);
-    if (n >= a.P) continue;
+    const int m = m0 + (g * 4) / BN, n = n0 + (g * 4) % BN;
+    if (m >= a.M) continue;
+    float bsum = 0.f;
+    if (a.bias) {
+      bsum = a.bias[m];
+      for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + m];
+    }
+    float* dst = a.C + (long long)m * a.P + n;
     const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int m = mb + c;
-      if (m < a.M) {
-        float v = vals[c];
-        if (a.bias) {
-          float bsum = a.bias[m];
-          for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + m];
-          v += bsum;
-        }
-        a.C[(long long)m * a.P + n] = v;
-      }
-    }
+    for (int c = 0; c < 4; ++c)
+      if (n + c < a.P) dst[c] = a.bias ? vals[c] + bsum : vals[c];
   }
 }
 

@@ -98,7 +98,7 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
     hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, WM, WN>), dim3(NW), dim3(256), 0, 0, a, sk);
-    hipLaunchKernelGGL((k_sk_reduce<BM, BN, WM, WN>), dim3(BM * BN / 1024, tiles), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_sk_reduce<BM, BN>), dim3(BM * BN / 1024, tiles), dim3(256), 0, 0, a, sk);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
