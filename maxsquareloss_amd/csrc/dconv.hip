@@ -147,22 +147,31 @@ static FwdPlan plan_fwd(int nbranch, int taps, int cimg, int M, int P, bool has_
   return pl;
 }
 
+// Weight gradient: stream-K over (tile, 64-pixel stage) (k_wgrad_sk + k_wsk_reduce).  Tiles by
+// shape (scripts/tune_dconv.hip wsk, profiles/): 128x128 at one workgroup per CU for the
+// 512-channel layer4 convs, 64x64 at two per CU below, 32-row tiles for the 19-class ASPP.
 struct WgradPlan {
-  int bm, bn, bk, tiles_m, tiles_n, ntap, ksteps, kps, S;
+  int bm, bn, nw, tiles_m, tiles_n, ntap, KS, slots;
+  long long T;
 };
 
 static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P) {
   WgradPlan pl;
-  pl.bm = 64;
-  pl.bn = 128;
-  pl.bk = 32;
+  if (cout <= 32) {
+    pl.bm = 32; pl.bn = 128; pl.nw = 256;
+  } else if (cout >= 512 && cin >= 512) {
+    pl.bm = 128; pl.bn = 128; pl.nw = 256;
+  } else {
+    pl.bm = 64; pl.bn = 64; pl.nw = 512;
+  }
   pl.tiles_m = cdiv(cout, pl.bm);
   pl.tiles_n = cdiv(cin, pl.bn);
   pl.ntap = nbranch * taps;
-  pl.ksteps = cdiv(P, pl.bk);
-  int S = choose_split(pl.tiles_m * pl.tiles_n * pl.ntap, pl.ksteps, 8);
-  pl.kps = cdiv(pl.ksteps, S);
-  pl.S = cdiv(pl.ksteps, pl.kps);
+  pl.KS = cdiv(P, kWskBK);
+  pl.T = (long long)pl.tiles_m * pl.tiles_n * pl.ntap * pl.KS;
+  pl.nw = (int)std::min<long long>(pl.nw, pl.T);
+  // tiles a worker range can touch: its length (<= ceil(T/NW) stages) starting anywhere in a tile
+  pl.slots = (int)((cdiv(pl.T, (long long)pl.nw) + pl.KS - 2) / pl.KS + 1);
   return pl;
 }
 
@@ -281,7 +290,7 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
 
 static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P) {
   WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P);
-  return pl.S > 1 ? (size_t)pl.S * nbranch * cout * cin * taps * sizeof(float) : 0;
+  return (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float);
 }
 
 static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
@@ -289,12 +298,15 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
                         int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
   const int P = h * w;
   WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P);
-  const long long nout = (long long)nbranch * cout * cin * taps;
-  if (pl.S > 1 && ws_bytes < (size_t)pl.S * nout * sizeof(float)) return MSL_ERR_WORKSPACE;
-  WgradArgs a;
+  if (ws_bytes < wgrad_ws_bytes(nbranch, taps, cin, cout, P)) return MSL_ERR_WORKSPACE;
+  if (pl.T * pl.nw >= (1LL << 31) || (long long)pl.nw * pl.slots * pl.bm * pl.bn * 4 >= (1LL << 31) || (long long)std::max(cin, cout) * P >= (1LL << 29) ||
+      (long long)P + kWskBK >= (1LL << 22))
+    return MSL_ERR_SHAPE;  // 32-bit index arithmetic, float pixel-row division in the kernel
+  WskArgs a;
   a.dy = dy;
   a.x = x;
-  a.C = pl.S > 1 ? (float*)ws : dw;
+  a.dw = dw;
+  a.part = (float*)ws;
   a.M = cout;
   a.N = cin;
   a.H = h;
@@ -302,22 +314,32 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   a.P = P;
   a.dil0 = dil0;
   a.dil1 = dil1;
-  a.ntap = pl.ntap;
-  a.ksteps = pl.ksteps;
-  a.kps = pl.kps;
-  a.accumulate = pl.S > 1 ? 0 : accumulate;
   a.taps = taps;
-  a.slab = nout;
+  a.accumulate = accumulate;
+  a.slots = pl.slots;
+  a.invW = 1.0f / (float)w;
+  a.tiles_m = pl.tiles_m;
+  a.tiles_n = pl.tiles_n;
+  a.KS = pl.KS;
+  a.NW = pl.nw;
+  a.T = (int)pl.T;
   a.cbranch = (long long)cout * cin * taps;
-  dim3 grid(pl.tiles_n, pl.tiles_m, pl.S * pl.ntap);
-  hipLaunchKernelGGL((k_igemm_wgrad<64, 128, 32, 2, 2>), grid, dim3(256), 0, st, a);
-  MSL_CHECK_LAUNCH();
-  if (pl.S > 1) {
-    const int blocks = (int)std::min<long long>(cdiv(nout, 256), 4096);
-    hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, (const float*)ws, pl.S, nout,
-                       dw, accumulate, (const float*)nullptr, 0, 1, 1);
+  const dim3 grid(pl.nw), block(256);
+  const dim3 rgrid(cdiv((long long)pl.bm * pl.bn * taps, 256), pl.tiles_m * pl.tiles_n * nbranch), rblock(256);
+  if (pl.bm == 128) {
+    hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
+  } else if (pl.bm == 64) {
+    hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2>), grid, block, 0, st, a);
+    MSL_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_wsk_reduce<64, 64>), rgrid, rblock, 0, st, a);
+  } else {
+    hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4>), grid, block, 0, st, a);
+    MSL_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_wsk_reduce<32, 128>), rgrid, rblock, 0, st, a);
   }
+  MSL_CHECK_LAUNCH();
   if (dbias) {
     hipLaunchKernelGGL(k_bias_grad, dim3(cout), dim3(256), 0, st, dy, P, dbias, cout, nbranch,
                        accumulate);

@@ -724,12 +724,20 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   const int m0 = tm * BM, n0 = tn * BN;
   const float4* __restrict__ part = reinterpret_cast<const float4*>(sk.part);
   for (int g = blockIdx.x * 256 + threadIdx.x; g < PSZ / 4; g += gridDim.x * 256) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int wc = w_lo; wc <= w_hi; ++wc) {
+    auto piece = [&](int wc) {
       const int slot = sk_start(wc, sk.T, sk.NW) > t * sk.KS ? 0 : 1;
-      const float4 v = part[(long long)(wc * 2 + slot) * (PSZ / 4) + g];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      return part[(long long)(wc * 2 + slot) * (PSZ / 4) + g];
+    };
+    auto add = [](float4& acc, const float4& v) { acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w; };
+    // two loads in flight per step (the sum stays in worker order)
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int wc = w_lo;
+    for (; wc + 1 <= w_hi; wc += 2) {
+      const float4 p0 = piece(wc), p1 = piece(wc + 1);
+      add(acc, p0);
+      add(acc, p1);
     }
+    if (wc <= w_hi) add(acc, piece(wc));
     const int m = m0 + (g * 4) / BN, n = n0 + (g * 4) % BN;
     if (m >= a.M) continue;
     float bsum = 0.f;
@@ -743,6 +751,201 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
     for (int c = 0; c < 4; ++c)
       if (n + c < a.P) dst[c] = a.bias ? vals[c] + bsum : vals[c];
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stream-K weight gradient.  dW[br][m][n][tap] = sum_p dY[m][p] * X[n][p + shift(br, tap)]:
+// one GEMM tile (BM output channels x BN input channels) per (branch, tap, m-block, n-block),
+// K = pixels in 64-pixel stages.  The (tile, stage) space is cut into NW equal worker ranges
+// like k_igemm_fwd_sk; pieces of split tiles go to `part` and k_wsk_reduce sums them.
+// Operands move by LDS-DMA, one 64-pixel row per wave-instruction (lane = pixel), into rows
+// padded to 66 floats: the DMA of one row is lane-linear, and the MFMA operand reads - lane l32
+// reads row l32 at two consecutive k (ds_read_b64) - hit 64 distinct banks.  A pixel outside the
+// image (tap shift, row wrap) or past P gets an out-of-range offset, which the buffer unit
+// zero-fills.  K is permuted inside a stage: half-wave kh takes pixels kh*32 .. kh*32+31, so a
+// lane's two k of consecutive MFMAs are adjacent in LDS (any bijection of K is valid as long as
+// both operands use it).
+struct WskArgs {
+  const float* dy;  // [M][P]
+  const float* x;   // [N][P]
+  float* dw;        // [nbranch][M][N][taps]
+  float* part;      // [NW][slots][BM][BN]: worker w's piece of tile t in slot t - first_tile(w)
+  int M, N, H, W, P, dil0, dil1, taps, accumulate, slots;
+  float invW;
+  int tiles_m, tiles_n, KS, NW, T;
+  long long cbranch;  // M * N * taps
+};
+
+constexpr int kWskBK = 64, kWskLD = 66;
+
+template <int BM, int BN, int STAGES, int WM, int WN>
+__global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(TM >= 1 && TN >= 1, "tiles");
+  constexpr int A_STAGE = BM * kWskLD, STAGE = (BM + BN) * kWskLD;
+  constexpr int AR_W = BM / 4, BR_W = BN / 4;  // rows (= DMA instructions) per wave and stage
+  constexpr int INST_W = AR_W + BR_W;
+  static_assert((STAGES - 2) * INST_W < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) float smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
+  const int it_begin = sk_start(w, a.T, a.NW), it_end = sk_start(w + 1, a.T, a.NW);
+
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.dy, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)min(0x7fffffffLL, (long long)a.N * a.P * 4), 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  const unsigned row_bytes = (unsigned)a.P * 4u;
+
+  f32x16 acc[TM][TN];
+  for (int it = it_begin; it < it_end;) {
+    const int t = (unsigned)it / (unsigned)a.KS;
+    const int k_a = it - t * a.KS;
+    const int k_b = min(a.KS, k_a + (it_end - it));
+    const int nst = k_b - k_a;
+    it += nst;
+    const int tm = t % a.tiles_m;
+    const int t2 = t / a.tiles_m;
+    const int tn = t2 % a.tiles_n;
+    const int z = t2 / a.tiles_n;  // branch * taps + tap
+    const int br = z / a.taps, tap = z - br * a.taps;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int d = br ? a.dil1 : a.dil0;
+    const int dh = (tap / 3 - 1) * d, dw = (tap % 3 - 1) * d;
+    const int shift = dh * a.W + dw;
+    // scalar row offsets of this wave's rows (OOB past M / N)
+    auto issue = [&](int s, int slot) {
+      float* As = smem + slot * STAGE;
+      float* Bs = As + A_STAGE;
+      const int p = s * kWskBK + lane;
+      const int py = (int)(((float)p + 0.5f) * a.invW);
+      const int px = p - py * a.W;
+      const unsigned va = p < a.P ? (unsigned)p * 4u : OOB;
+      const bool vb = p < a.P && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
+      const unsigned vbo = vb ? (unsigned)(p + shift) * 4u : OOB;
+#pragma unroll
+      for (int i = 0; i < AR_W; ++i) {
+        const int r = wid * AR_W + i;
+        const unsigned ro = m0 + r < a.M ? (unsigned)(m0 + r) * row_bytes : OOB;
+        dma_b32(rA, As + r * kWskLD, va + ro);
+      }
+#pragma unroll
+      for (int i = 0; i < BR_W; ++i) {
+        const int r = wid * BR_W + i;
+        const unsigned ro = n0 + r < a.N ? (unsigned)(n0 + r) * row_bytes : OOB;
+        dma_b32(rB, Bs + r * kWskLD, vbo + ro);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int k = 0; k < STAGES - 1; ++k)
+      if (k < nst) issue(k_a + k, k);
+    for (int i = 0; i < nst; ++i) {
+      const int younger = min(STAGES - 2, nst - 1 - i);
+      if constexpr (STAGES >= 3) {
+        if (younger >= 1) wait_vmcnt<INST_W>();
+        else wait_vmcnt<0>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      if (i + STAGES - 1 < nst) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
+      const float* As = smem + (i % STAGES) * STAGE;
+      const float* Bs = As + A_STAGE;
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int kq = 0; kq < kWskBK / 4; ++kq) {
+        const int kc = kh * 32 + 2 * kq;
+        f32x2 av[TM], bv[TN];
+#pragma unroll
+        for (int ii = 0; ii < TM; ++ii)
+          av[ii] = *reinterpret_cast<const f32x2*>(As + (wm + ii * 32 + l32) * kWskLD + kc);
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj)
+          bv[jj] = *reinterpret_cast<const f32x2*>(Bs + (wn + jj * 32 + l32) * kWskLD + kc);
+#pragma unroll
+        for (int ii = 0; ii < TM; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj)
+            acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ii].x, bv[jj].x, acc[ii][jj], 0, 0, 0);
+#pragma unroll
+        for (int ii = 0; ii < TM; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj)
+            acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ii].y, bv[jj].y, acc[ii][jj], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    // Every tile leaves its piece(s) in `part` (an unsplit tile: one slot-1 piece): dW is
+    // [m][n][tap], so a tile's own stores would be 36-B strided; k_wsk_reduce writes all taps of
+    // an (m, n) together.
+    constexpr int PSZ = BM * BN;
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.part, (short)0, (int)min(0x7fffffffLL, (long long)a.NW * a.slots * PSZ * 4), 0x00020000);
+    const int slot = t - it_begin / a.KS;
+    const unsigned pbase = (unsigned)((w * a.slots + slot) * PSZ * 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn + j * 32 + l32;
+        const int ml = wm + i * 32 + 4 * kh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rp,
+                                                pbase + (unsigned)(((ml + ro) * BN + nl) * 4), 0, 0);
+        }
+      }
+  }
+}
+
+// dW (=|+=) the sum of every tile's pieces, in worker order.  One thread per (m, n, tap) of an
+// (m-block, n-block, branch) group, tap fastest: the dW stores are contiguous, and there are
+// enough waves in flight to hide the (serial, per-thread) piece loads.
+// grid = (ceil(BM*BN*taps / 256), tiles_m * tiles_n * nbranch).
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
+  constexpr int PSZ = BM * BN;
+  const int gsz = a.tiles_m * a.tiles_n;
+  const int br = blockIdx.y / gsz;
+  const int rem = blockIdx.y - br * gsz;
+  const int tn = rem / a.tiles_m, tm = rem - tn * a.tiles_m;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int g = e / a.taps, tap = e - g * a.taps;
+  const int m = tm * BM + g / BN, n = tn * BN + g % BN;
+  if (g >= PSZ || m >= a.M || n >= a.N) return;
+  const int t = ((br * a.taps + tap) * a.tiles_n + tn) * a.tiles_m + tm;
+  const int w_lo = sk_worker_of(t * a.KS, a.T, a.NW);
+  const int w_hi = sk_worker_of((t + 1) * a.KS - 1, a.T, a.NW);
+  const float* __restrict__ part = a.part;
+  auto piece = [&](int wc) {
+    const int slot = t - sk_start(wc, a.T, a.NW) / a.KS;
+    return part[(long long)(wc * a.slots + slot) * PSZ + g];
+  };
+  // four loads in flight per step (the sum stays in worker order)
+  float v = 0.f;
+  int wc = w_lo;
+  for (; wc + 3 <= w_hi; wc += 4) {
+    const float p0 = piece(wc), p1 = piece(wc + 1), p2 = piece(wc + 2), p3 = piece(wc + 3);
+    v += p0; v += p1; v += p2; v += p3;
+  }
+  for (; wc <= w_hi; ++wc) v += piece(wc);
+  float* dst = a.dw + br * a.cbranch + (long long)m * a.N * a.taps + (long long)n * a.taps + tap;
+  *dst = a.accumulate ? *dst + v : v;
 }
 
 }  // namespace msl

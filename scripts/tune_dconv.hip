@@ -128,6 +128,28 @@ float run_wgrad(const Shape& sh, const float* x, const float* dy, float* dw, flo
   return ms / iters;
 }
 
+template <int BM, int BN, int ST>
+float run_wgrad_sk(const Shape& sh, const float* x, const float* dy, float* dw, float* ws, int NWmax, int iters) {
+  const int P = sh.h * sh.w;
+  WskArgs a;
+  a.dy = dy; a.x = x; a.dw = dw; a.part = ws; a.M = sh.cout; a.N = sh.cin; a.H = sh.h; a.W = sh.w; a.P = P;
+  a.dil0 = sh.dil; a.dil1 = 0; a.taps = 9; a.accumulate = 0; a.invW = 1.0f / sh.w;
+  a.tiles_m = (sh.cout + BM - 1) / BM; a.tiles_n = (sh.cin + BN - 1) / BN; a.KS = (P + kWskBK - 1) / kWskBK;
+  const int tiles = a.tiles_m * a.tiles_n * 9;
+  a.T = tiles * a.KS; a.NW = std::min(NWmax, a.T); a.cbranch = (long long)sh.cout * sh.cin * 9;
+  a.slots = ((a.T + a.NW - 1) / a.NW + a.KS - 2) / a.KS + 1;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_wgrad_sk<BM, BN, ST, (BM >= 64 ? 2 : 1), (BM >= 64 ? 2 : 4)>), dim3(a.NW), dim3(256), 0, 0, a);
+    hipLaunchKernelGGL((k_wsk_reduce<BM, BN>), dim3(BM * BN * 9 / 256, a.tiles_m * a.tiles_n), dim3(256), 0, 0, a);
+  }
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
 static double maxdiff(const float* a, const float* b, size_t n, double* scale) {
   std::vector<float> ha(n), hb(n);
   CK(hipMemcpy(ha.data(), a, n * 4, hipMemcpyDeviceToHost));
@@ -143,6 +165,7 @@ int main(int argc, char** argv) {
   const bool sk_only = argc > 1 && std::string(argv[1]) == "sk";
   // "fsk": every stream-K row, nothing else
   const bool fsk_only = argc > 1 && std::string(argv[1]) == "fsk";
+  const bool wsk_only = argc > 1 && std::string(argv[1]) == "wsk";
   const int iters = sk_only ? 5 : 20;
   Shape shapes[] = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
   for (const Shape& sh : shapes) {
@@ -175,6 +198,19 @@ int main(int argc, char** argv) {
 #define FSK(BM, BN, G, ST, WM, WN, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); float ms = run_fwd_sk<BM, BN, G, ST, WM, WN>(sh, x, wp, y, ws, NW, iters, lda, flags); \
       double md = maxdiff(y, yref, (size_t)sh.cout * P, &sc); \
       printf("fsk   BM %3d BN %3d G %d ST %2d W %dx%d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, G, ST, WM, WN, NW, ms * 1e3, gf / ms, md, sc); }
+#define WGR(BM, BN, BK, WM, WN, S) { float ms = run_wgrad<BM, BN, BK, WM, WN>(sh, x, dy, dw, ws, S, iters); \
+      double md = maxdiff(dw, dwref, (size_t)sh.cout * sh.cin * 9, &sc); \
+      printf("wgrad BM %3d BN %3d BK %2d W %dx%d S %2d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, BK, WM, WN, S, ms * 1e3, gf / ms, md, sc); }
+#define WSK(BM, BN, ST, NW) { float ms = run_wgrad_sk<BM, BN, ST>(sh, x, dy, dw, ws, NW, iters); \
+      double md = maxdiff(dw, dwref, (size_t)sh.cout * sh.cin * 9, &sc); \
+      printf("wsk   BM %3d BN %3d ST %d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, ST, NW, ms * 1e3, gf / ms, md, sc); }
+    if (wsk_only) {
+      run_wgrad<64, 128, 32, 2, 2>(sh, x, dy, dwref, ws, 1, 1);
+      WGR(64, 128, 32, 2, 2, 8)
+      WSK(128, 128, 2, 256) WSK(64, 128, 2, 256) WSK(64, 128, 2, 512) WSK(64, 64, 2, 512) WSK(64, 64, 3, 256)
+      WSK(128, 64, 2, 256)
+      continue;
+    }
     if (sk_only) {
       FSK(128, 128, 2, 2, 2, 2, 512)
       break;
@@ -188,9 +224,6 @@ int main(int argc, char** argv) {
     FDMA(128, 128, 3, 2, 2, 6) FDMA(128, 128, 3, 2, 2, 8)
     FDMA(64, 128, 3, 2, 2, 1) FDMA(64, 128, 3, 2, 2, 2) FDMA(64, 128, 3, 2, 2, 3) FDMA(64, 128, 3, 2, 2, 4)
     FDMA(64, 64, 3, 2, 2, 1) FDMA(64, 64, 3, 2, 2, 2) FDMA(64, 64, 3, 2, 2, 3)
-#define WGR(BM, BN, BK, WM, WN, S) { float ms = run_wgrad<BM, BN, BK, WM, WN>(sh, x, dy, dw, ws, S, iters); \
-      double md = maxdiff(dw, dwref, (size_t)sh.cout * sh.cin * 9, &sc); \
-      printf("wgrad BM %3d BN %3d BK %2d W %dx%d S %2d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, BK, WM, WN, S, ms * 1e3, gf / ms, md, sc); }
     run_wgrad<64, 128, 32, 2, 2>(sh, x, dy, dwref, ws, 1, 1);
     WGR(64, 128, 32, 2, 2, 8)
     CK(hipFree(x)); CK(hipFree(wp)); CK(hipFree(dy)); CK(hipFree(y)); CK(hipFree(yref)); CK(hipFree(ws)); CK(hipFree(dw)); CK(hipFree(dwref));
