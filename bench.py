@@ -34,6 +34,7 @@ from maxsquareloss_amd.utils.synthetic import synthetic_image, synthetic_labels 
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense BF16 matrix peak (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -57,6 +58,8 @@ def parse():
     ap.add_argument("--multi", default="False")
     ap.add_argument("--lambda-target", type=float, default=0.1)
     ap.add_argument("--num-classes", type=int, default=19)
+    ap.add_argument("--conv-math", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16 = BASELINE config 5's fp16/bf16 MFMA path (fp32 accumulation)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=2, help="0 disables the CPU baseline")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM traffic per launch of the dominant kernel (from a rocprofv3 --pmc run)")
@@ -71,7 +74,7 @@ def main():
     argv = ["--crop_size", f"{a.width},{a.height}", "--target_crop_size", f"{a.width},{a.height}",
             "--imagenet_pretrained", "False", "--save_dir", "", "--num_classes", str(a.num_classes),
             "--target_mode", a.target_mode, "--multi", a.multi, "--lambda_target", str(a.lambda_target),
-            "--iter_max", "200000"]
+            "--iter_max", "200000", "--conv_math", a.conv_math]
     args, _, _ = init_args(build_parser().parse_args(argv))
     tr = UDATrainer(args, cuda=True)
     rank, dev = tr.rank, tr.device
@@ -127,8 +130,11 @@ def main():
             traffic = json.load(open(a.pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+    peak = BF16_MFMA_PEAK_TFLOPS if a.conv_math == "bf16" else FP32_MFMA_PEAK_TFLOPS
+    if a.conv_math != "fp32":
+        traffic = None  # the committed PMC figure is for the fp32 kernel
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": "dconv3x3 fwd layer3 d=2 (k_igemm_fwd_sk, stream-K)",
                 "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
@@ -162,9 +168,11 @@ def main():
     line = {
         "metric": METRIC, "value": round(images / elapsed, 3), "unit": "images/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if a.conv_math == "fp32" else "bf16 (conv MFMA), fp32",
         "data": "synthetic (counter-generated uint8 images -> BGR-mean, uniform labels; random-init weights)",
-        "config": {"workload": f"GTA5->Cityscapes {args.target_mode} UDA step (solve_gta5.py), {W}x{H}, bs=1/GPU",
+        "config": {"workload": f"{'SYNTHIA' if C == 16 else 'GTA5'}->Cityscapes {args.target_mode} UDA step "
+                               f"(solve_gta5.py), {W}x{H}, bs=1/GPU",
+                   "conv_math": a.conv_math,
                    "target_mode": args.target_mode, "multi": args.multi, "lambda_target": args.lambda_target,
                    "num_classes": C, "global_batch": 2 * world, "parallelism": f"dp{world}"},
         "roofline": roofline, "cpu_baseline": cpu,

@@ -109,6 +109,28 @@ int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cou
                     int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * BF16-MFMA forms of the six conv calls above (BASELINE config 5, "fp16/bf16 MFMA
+ * path"): identical arguments, workspaces and output layout; the fp32 operands are
+ * rounded to bf16 (RNE) as they are read from LDS and multiplied by
+ * v_mfma_f32_32x32x16_bf16 with fp32 accumulation.  Same reference sites.
+ * ---------------------------------------------------------------------- */
+int msl_dconv_fwd_bf16(const float* x, const float* packed, const float* bias, float* y, int nbranch,
+                       int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                       size_t ws_bytes, msl_stream_t stream);
+int msl_dconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
+                         int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                         size_t ws_bytes, msl_stream_t stream);
+int msl_dconv_wgrad_bf16(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
+                         int cin, int cout, int h, int w, int dil0, int dil1, int accumulate,
+                         void* ws, size_t ws_bytes, msl_stream_t stream);
+int msl_pconv_fwd_bf16(const float* x, const float* packed, float* y, int cin, int cout, int p,
+                       int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+int msl_pconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout,
+                         int p, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, int cout, int p,
+                         int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * Bilinear upsample, align_corners=True (F.interpolate at deeplab_multi.py:124,
  * :128).  The forward reproduces torch-CPU's rounding bit for bit.
  * ---------------------------------------------------------------------- */

@@ -183,6 +183,7 @@ static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
   return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
 }
 
+template <bool BF>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int dil0,
                            int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -231,26 +232,27 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     const dim3 rgrid(pl.bm * kSkBN / 1024, pl.tiles_m * pl.tiles_n);
     if (pl.bm == 128) {
       if (pl.G == 2)
-        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2, false, BF>), grid, block, 0, st, a, sk);
       else
-        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2, false, BF>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
       if (pl.G == 2)
-        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2, false, BF>), grid, block, 0, st, a, sk);
       else
-        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2, false, BF>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
     } else {
-      hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4>), grid, block, 0, st, a, sk);
+      hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4, false, BF>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
     }
     MSL_CHECK_LAUNCH();
     return MSL_OK;
   }
+  if (BF) return MSL_ERR_SHAPE;  // the split-K tile kernel (odd K-step count, M <= 32) is f32 only
   dim3 grid(pl.tiles_n, pl.tiles_m, pl.S);
   hipLaunchKernelGGL((k_igemm_fwd<64, 128, 16, 2, 2>), grid, dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
@@ -293,6 +295,7 @@ static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P) {
   return (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float);
 }
 
+template <bool BF>
 static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
                         int taps, int cin, int cout, int h, int w, int dil0, int dil1,
                         int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -327,15 +330,15 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   const dim3 grid(pl.nw), block(256);
   const dim3 rgrid(cdiv((long long)pl.bm * pl.bn * taps, 256), pl.tiles_m * pl.tiles_n * nbranch), rblock(256);
   if (pl.bm == 128) {
-    hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2, BF>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
   } else if (pl.bm == 64) {
-    hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2, BF>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<64, 64>), rgrid, rblock, 0, st, a);
   } else {
-    hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4, BF>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<32, 128>), rgrid, rblock, 0, st, a);
   }
@@ -392,7 +395,7 @@ int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float*
   if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
+  return launch_fwd_form<false>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
@@ -407,7 +410,7 @@ int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int n
   if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+  return launch_fwd_form<false>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
@@ -422,7 +425,7 @@ int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, in
   if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_wgrad(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
+  return launch_wgrad<false>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
                       ws_bytes, as_stream(stream));
 }
 
@@ -446,7 +449,7 @@ size_t msl_pconv_fwd_workspace(int cin, int cout, int p) {
 int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
                   int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return launch_fwd_form(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
+  return launch_fwd_form<false>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
                          ws_bytes, as_stream(stream));
 }
 
@@ -458,7 +461,7 @@ size_t msl_pconv_dgrad_workspace(int cin, int cout, int p) {
 int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return launch_fwd_form(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
+  return launch_fwd_form<false>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
                          ws, ws_bytes, as_stream(stream));
 }
 
@@ -470,7 +473,62 @@ size_t msl_pconv_wgrad_workspace(int cin, int cout, int p) {
 int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,
                     int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
-  return launch_wgrad(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+  return launch_wgrad<false>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+                      as_stream(stream));
+}
+
+
+// ------------------------------------------------------------------ BF16-MFMA forms
+// Same operands, workspaces and results layout; products in bf16 (RNE from the fp32 operands),
+// sums in fp32 (BASELINE config 5's fp16/bf16 MFMA path).
+int msl_dconv_fwd_bf16(const float* x, const float* packed, const float* bias, float* y, int nbranch,
+                  int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                  size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_fwd_form<true>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
+                         counters, ws, ws_bytes, as_stream(stream));
+}
+
+int msl_dconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
+                    int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                    size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_fwd_form<true>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+                         counters, ws, ws_bytes, as_stream(stream));
+}
+
+int msl_dconv_wgrad_bf16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
+                    int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                    size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_wgrad<true>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
+                      ws_bytes, as_stream(stream));
+}
+
+int msl_pconv_fwd_bf16(const float* x, const float* packed, float* y, int cin, int cout, int p,
+                  int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
+  return launch_fwd_form<true>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
+                         ws_bytes, as_stream(stream));
+}
+
+int msl_pconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                    int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
+  return launch_fwd_form<true>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
+                         ws, ws_bytes, as_stream(stream));
+}
+
+int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, int cout, int p,
+                    int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
+  return launch_wgrad<true>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
                       as_stream(stream));
 }
 

@@ -96,6 +96,37 @@ __device__ __forceinline__ void mfma_stage_pipe(const float* __restrict__ As, co
   }
 }
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// BF16 MFMA over one LDS stage of fp32 operands ([k][m] / [k][n] images, as the f32 stage):
+// v_mfma_f32_32x32x16_bf16, lane (r = l&31, h = l>>5) takes A[m = r][k = 8h + j] and
+// B[k = 8h + j][n = r], j = 0..7: eight conflict-free ds_read_b32 per operand (32 consecutive
+// floats per half-wave), rounded to bf16 (RNE, v_cvt_pk_bf16_f32) in registers; fp32
+// accumulation.  `mid` runs after the first 16-deep group.
+template <int BK, int TM, int TN, int LDA_S, int LDB_S, typename F>
+__device__ __forceinline__ void mfma_stage_bf16(const float* __restrict__ As, const float* __restrict__ Bs,
+                                                int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int kk = 0; kk < BK / 16; ++kk) {
+    bf16x8 av[TM], bv[TN];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kr = kk * 16 + 8 * h + j;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i][j] = (__bf16)As[kr * LDA_S + wm + i * 32 + l32];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) bv[t][j] = (__bf16)Bs[kr * LDB_S + wn + t * 32 + l32];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[t], acc[i][t], 0, 0, 0);
+    if (kk == 0) mid();
+  }
+}
+
 // Forward form: C[m][p] = sum_k A[k][m] * B[k][p], BK = G * 16 (G tap-groups per K-step).
 template <int BM, int BN, int BK, int WM, int WN>
 __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
@@ -475,7 +506,7 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
   return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
 }
 
-template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false>
+template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, bool BF = false>
 __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -643,9 +674,13 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       __builtin_amdgcn_s_barrier();
       const float* As = smem + (i % STAGES) * STAGE;
       const bool more = i + STAGES - 1 < nst;
-      mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, [&] {
+      auto mid = [&] {
         if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
-      });
+      };
+      if constexpr (BF)
+        mfma_stage_bf16<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
+      else
+        mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
@@ -776,11 +811,14 @@ struct WskArgs {
   long long cbranch;  // M * N * taps
 };
 
-constexpr int kWskBK = 64, kWskLD = 66;
+constexpr int kWskBK = 64;
 
-template <int BM, int BN, int STAGES, int WM, int WN>
+template <int BM, int BN, int STAGES, int WM, int WN, bool BF = false>
 __global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
   static_assert(WM * WN == 4, "4 waves");
+  // row stride: 66 floats for the f32 b64 reads (64 distinct banks); 68 for the bf16 form's
+  // 16-B aligned b128 reads (4-dword chunks at 4*row: conflict-free per 16-lane group)
+  constexpr int kWskLD = BF ? 68 : 66;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(TM >= 1 && TN >= 1, "tiles");
   constexpr int A_STAGE = BM * kWskLD, STAGE = (BM + BN) * kWskLD;
@@ -866,6 +904,33 @@ __global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
       const float* As = smem + (i % STAGES) * STAGE;
       const float* Bs = As + A_STAGE;
       typedef float f32x2 __attribute__((ext_vector_type(2)));
+      if constexpr (BF) {
+        // lane (r, h) of v_mfma_f32_32x32x16_bf16 takes pixels kk*16 + 8h .. +7 of row r
+#pragma unroll
+        for (int kk = 0; kk < kWskBK / 16; ++kk) {
+          const int kc = kk * 16 + 8 * kh;
+          bf16x8 av[TM], bv[TN];
+#pragma unroll
+          for (int ii = 0; ii < TM; ++ii) {
+            const float4* src = reinterpret_cast<const float4*>(As + (wm + ii * 32 + l32) * kWskLD + kc);
+            const float4 u = src[0], v = src[1];
+            av[ii][0] = (__bf16)u.x; av[ii][1] = (__bf16)u.y; av[ii][2] = (__bf16)u.z; av[ii][3] = (__bf16)u.w;
+            av[ii][4] = (__bf16)v.x; av[ii][5] = (__bf16)v.y; av[ii][6] = (__bf16)v.z; av[ii][7] = (__bf16)v.w;
+          }
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj) {
+            const float4* src = reinterpret_cast<const float4*>(Bs + (wn + jj * 32 + l32) * kWskLD + kc);
+            const float4 u = src[0], v = src[1];
+            bv[jj][0] = (__bf16)u.x; bv[jj][1] = (__bf16)u.y; bv[jj][2] = (__bf16)u.z; bv[jj][3] = (__bf16)u.w;
+            bv[jj][4] = (__bf16)v.x; bv[jj][5] = (__bf16)v.y; bv[jj][6] = (__bf16)v.z; bv[jj][7] = (__bf16)v.w;
+          }
+#pragma unroll
+          for (int ii = 0; ii < TM; ++ii)
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj)
+              acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[ii], bv[jj], acc[ii][jj], 0, 0, 0);
+        }
+      } else {
 #pragma unroll
       for (int kq = 0; kq < kWskBK / 4; ++kq) {
         const int kc = kh * 32 + 2 * kq;
@@ -886,6 +951,7 @@ __global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
 #pragma unroll
           for (int jj = 0; jj < TN; ++jj)
             acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ii].y, bv[jj].y, acc[ii][jj], 0, 0, 0);
+      }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }

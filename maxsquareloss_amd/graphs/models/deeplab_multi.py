@@ -47,7 +47,8 @@ class DilatedConv3x3(nn.Conv2d):
 # The HIP pointwise GEMMs run at 45-90 TFLOP/s on these shapes; the library FP32 GEMMs reach
 # 85-145 on most of them (scripts/bench_pconv.py, scripts/bench_mm.py, profiles/).  By default
 # a stride-1 1x1 conv therefore runs each of its three GEMMs on the fastest library
-# (ops.conv1x1); USE_HIP_POINTWISE switches all three to the HIP kernels (parity-tested).
+# (ops.conv1x1); USE_HIP_POINTWISE switches all three to the HIP kernels (parity-tested), and
+# so does the bf16 conv math (ops.set_conv_math), which has no library form here.
 USE_HIP_POINTWISE = False
 
 
@@ -59,7 +60,7 @@ class PointwiseConv(nn.Conv2d):
         self._pack = ops.PackCache(pointwise=True)
 
     def forward(self, x):
-        if USE_HIP_POINTWISE:
+        if USE_HIP_POINTWISE or ops.CONV_MATH != "fp32":
             return ops.pconv(x, self.weight, self._pack)
         return ops.conv1x1(x, self.weight, self._pack)
 

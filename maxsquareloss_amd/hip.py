@@ -36,6 +36,12 @@ SIGNATURES = {
     "msl_pconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_wgrad_workspace": (c_sz, [c_int] * 3),
     "msl_pconv_wgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
+    "msl_dconv_fwd_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
+    "msl_dconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
+    "msl_dconv_wgrad_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p]),
+    "msl_pconv_fwd_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
+    "msl_pconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
+    "msl_pconv_wgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
     "msl_upsample_fwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p]),
     "msl_upsample_bwd_workspace": (c_sz, [c_int] * 5),
     "msl_upsample_bwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p, c_sz, c_p]),

@@ -13,6 +13,22 @@ from . import hip
 
 _f32 = torch.float32
 
+# Conv MFMA precision: "fp32" (v_mfma_f32_32x32x2_f32, the reference's arithmetic) or "bf16"
+# (v_mfma_f32_32x32x16_bf16 on operands rounded to bf16, fp32 sums: BASELINE config 5's
+# fp16/bf16 MFMA path).  Activations, BN, losses and the optimizer stay fp32 either way.
+CONV_MATH = "fp32"
+
+
+def set_conv_math(math):
+    global CONV_MATH
+    if math not in ("fp32", "bf16"):
+        raise ValueError(f"conv math must be 'fp32' or 'bf16', got {math!r}")
+    CONV_MATH = math
+
+
+def _fn(lib, name, math):
+    return getattr(lib, name + "_bf16") if math == "bf16" else getattr(lib, name)
+
 
 def _check_act(x, name):
     if not x.is_cuda or x.dtype != _f32 or x.dim() != 4 or x.size(0) != 1:
@@ -114,7 +130,8 @@ class _DConv3x3(Function):
         if probe is not None:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-        hip.check(lib.msl_dconv_fwd(x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb,
+        math = CONV_MATH
+        hip.check(_fn(lib, "msl_dconv_fwd", math)(x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb,
                                     cin, cout, h, w, dil0, dil1 if nb > 1 else 0,
                                     hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
                                     hip.stream_ptr()), "msl_dconv_fwd")
@@ -123,13 +140,13 @@ class _DConv3x3(Function):
             ev1.record()
             probe.append((ev0, ev1))
         ctx.save_for_backward(x, *weights)
-        ctx.meta = (nb, cin, cout, h, w, dil0, dil1, b0 is not None, cache)
+        ctx.meta = (nb, cin, cout, h, w, dil0, dil1, b0 is not None, cache, math)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, *weights = ctx.saved_tensors
-        nb, cin, cout, h, w, dil0, dil1, has_bias, cache = ctx.meta
+        nb, cin, cout, h, w, dil0, dil1, has_bias, cache, math = ctx.meta
         gy = gy.contiguous()
         lib = hip.load()
         s = hip.stream_ptr()
@@ -140,7 +157,7 @@ class _DConv3x3(Function):
             dx = torch.empty_like(x)
             wsb = lib.msl_dconv_dgrad_workspace(nb, cin, cout, h, w)
             ws = hip.workspace(wsb, x.device)
-            hip.check(lib.msl_dconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin,
+            hip.check(_fn(lib, "msl_dconv_dgrad", math)(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin,
                                           cout, h, w, dil0, d1, hip.counters(x.device).data_ptr(),
                                           ws.data_ptr(), wsb, s), "msl_dconv_dgrad")
         sink = grad_sink(weights[0]) if (nb == 1 and not has_bias and ctx.needs_input_grad[1]) else None
@@ -148,13 +165,13 @@ class _DConv3x3(Function):
         ws = hip.workspace(wsb, x.device)
         if sink is not None:
             g, fg, i = sink
-            hip.check(lib.msl_dconv_wgrad(x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w,
+            hip.check(_fn(lib, "msl_dconv_wgrad", math)(x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w,
                                           dil0, 0, 1, ws.data_ptr(), wsb, s), "msl_dconv_wgrad")
             fg.notify(i)
             return dx, None, None, None, None, None, None, None
         dw_all = torch.empty((nb, cout, cin, 3, 3), dtype=_f32, device=x.device)
         db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
-        hip.check(lib.msl_dconv_wgrad(x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb,
+        hip.check(_fn(lib, "msl_dconv_wgrad", math)(x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb,
                                       cin, cout, h, w, dil0, d1, 0, ws.data_ptr(), wsb, s), "msl_dconv_wgrad")
         dw0 = dw_all[0]
         dw1 = dw_all[1] if nb > 1 else None
@@ -190,17 +207,18 @@ class _PConv(Function):
         y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
         wsb = lib.msl_pconv_fwd_workspace(cin, cout, p)
         ws = hip.workspace(wsb, x.device)
-        hip.check(lib.msl_pconv_fwd(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
+        math = CONV_MATH
+        hip.check(_fn(lib, "msl_pconv_fwd", math)(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
                                     hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
                                     hip.stream_ptr()), "msl_pconv_fwd")
         ctx.save_for_backward(x, weight)
-        ctx.meta = (cin, cout, p, cache)
+        ctx.meta = (cin, cout, p, cache, math)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
-        cin, cout, p, cache = ctx.meta
+        cin, cout, p, cache, math = ctx.meta
         gy = gy.contiguous()
         lib = hip.load()
         s = hip.stream_ptr()
@@ -210,17 +228,21 @@ class _PConv(Function):
             dx = torch.empty_like(x)
             wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
             ws = hip.workspace(wsb, x.device)
-            hip.check(lib.msl_pconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
+            hip.check(_fn(lib, "msl_pconv_dgrad", math)(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
                                           hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s),
                       "msl_pconv_dgrad")
-        dw = None
-        if ctx.needs_input_grad[1]:
-            dw = torch.empty_like(weight)
-            wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
-            ws = hip.workspace(wsb, x.device)
-            hip.check(lib.msl_pconv_wgrad(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), cin, cout, p, 0,
-                                          ws.data_ptr(), wsb, s), "msl_pconv_wgrad")
-        return dx, dw, None
+        if not ctx.needs_input_grad[1]:
+            return dx, None, None
+        sink = grad_sink(weight)
+        dst = sink[0] if sink is not None else torch.empty_like(weight)
+        wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
+        ws = hip.workspace(wsb, x.device)
+        hip.check(_fn(lib, "msl_pconv_wgrad", math)(x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p,
+                                                   int(sink is not None), ws.data_ptr(), wsb, s), "msl_pconv_wgrad")
+        if sink is None:
+            return dx, dst, None
+        sink[1].notify(sink[2])
+        return dx, None, None
 
 
 def pconv(x, weight, cache):

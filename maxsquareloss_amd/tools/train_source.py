@@ -23,6 +23,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .. import ops
 from ..utils.dist import GradReducer
 from ..utils.loss import CrossEntropyLoss
 from ..utils.optim import SGD
@@ -68,6 +69,7 @@ class Trainer:
         self.current_iter = 0
 
         self.loss = CrossEntropyLoss(weight=None, ignore_index=-1)
+        ops.set_conv_math(getattr(self.args, "conv_math", "fp32"))
 
         self.model, self.params = get_model(self.args)
         init_weights(self.model, seed=self.args.seed)
@@ -219,6 +221,9 @@ def add_train_args(arg_parser):
     a("--multi", default=True, type=str2bool)
     a("--lambda_seg", type=float, default=0.1)
     a("--synthetic_images", type=int, default=4, help="synthetic items per domain (no datasets offline)")
+    a("--conv_math", default="fp32", choices=["fp32", "bf16"],
+      help="conv MFMA precision (not in the reference, which is fp32): bf16 = BASELINE config 5's "
+           "fp16/bf16 MFMA path (bf16 products, fp32 sums; BN, losses, SGD stay fp32)")
     return arg_parser
 
 

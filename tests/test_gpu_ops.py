@@ -311,3 +311,62 @@ def test_bn_act(c, h, w, res, relu, train):
     if res:
         assert _rel(rg.grad.cpu().double() * keep, rr.grad * keep) < 1e-6
     assert _rel(bn.running_mean, rmr) < 1e-5 and _rel(bn.running_var, rvr) < 1e-5
+
+
+# ----------------------------------------------------------------------------- bf16 conv math
+def _bf(t):
+    """The operand as the bf16 kernels see it: fp32 rounded to bf16 (RNE), exact in fp64."""
+    return t.bfloat16().double()
+
+
+@pytest.mark.parametrize("kind,cin,cout,h,w,d", [
+    ("dconv", 256, 256, 17, 33, 2), ("dconv", 512, 512, 17, 33, 4), ("dconv", 64, 64, 33, 65, 1),
+    ("pconv", 256, 1024, 17, 33, 0), ("pconv", 1024, 256, 17, 33, 0), ("aspp", 1024, 16, 17, 33, 6)])
+def test_conv_bf16_math(kind, cin, cout, h, w, d):
+    """BASELINE config 5's bf16 MFMA path: products of bf16-rounded operands summed in fp32.
+    Reference: the same conv in fp64 on the bf16-rounded operands, so the only admissible
+    difference is the fp32 accumulation (1e-5 of max|ref|, as the fp32 kernels)."""
+    g = torch.Generator().manual_seed(cin + 11 * cout + d)
+    k = 1 if kind == "pconv" else 3
+    x = torch.randn(1, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) * 0.05
+    w2 = torch.randn(cout, cin, k, k, generator=g) * 0.05
+    b0, b1 = torch.randn(cout, generator=g), torch.randn(cout, generator=g)
+    gy = torch.randn(1, cout, h, w, generator=g)
+    ops.set_conv_math("bf16")
+    try:
+        xg = x.to(DEV).requires_grad_()
+        wg = wt.to(DEV).requires_grad_()
+        if kind == "dconv":
+            y = ops.dconv3x3(xg, wg, d, ops.PackCache())
+        elif kind == "pconv":
+            y = ops.pconv(xg, wg, ops.PackCache(pointwise=True))
+        else:
+            w2g = w2.to(DEV).requires_grad_()
+            y = ops.aspp2(xg, wg, b0.to(DEV), w2g, b1.to(DEV), d, 2 * d, ops.PackCache())
+        y.backward(gy.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        ops.set_conv_math("fp32")
+    pad = 0 if kind == "pconv" else d
+    dil = 1 if kind == "pconv" else d
+
+    def conv(xx, ww, dd=dil, pp=pad):
+        return F.conv2d(xx, ww, padding=pp, dilation=dd)
+
+    yr = conv(_bf(x), _bf(wt))
+    if kind == "aspp":
+        yr = yr + conv(_bf(x), _bf(w2), 2 * d, 2 * d) + (b0 + b1).double().view(1, -1, 1, 1)
+    assert _rel(y, yr) < 1e-5
+    # data gradient: dy and W rounded; weight gradient: x and dy rounded
+    xr = _bf(x).requires_grad_()
+    conv(xr, _bf(wt)).backward(_bf(gy))
+    dx_ref = xr.grad
+    if kind == "aspp":
+        xr2 = _bf(x).requires_grad_()
+        conv(xr2, _bf(w2), 2 * d, 2 * d).backward(_bf(gy))
+        dx_ref = dx_ref + xr2.grad
+    wr = _bf(wt).requires_grad_()
+    conv(_bf(x), wr).backward(_bf(gy))
+    assert _rel(xg.grad, dx_ref) < 1e-5
+    assert _rel(wg.grad, wr.grad) < 1e-5
