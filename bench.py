@@ -135,7 +135,7 @@ def main():
         traffic = None  # the committed PMC figure is for the fp32 kernel
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": "dconv3x3 fwd layer3 d=2 (k_igemm_fwd_sk, stream-K)",
+                "kernel": "dconv3x3 fwd layer3 d=2 (stream-K k_igemm_fwd_sk + k_sk_reduce, one op call)",
                 "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
 

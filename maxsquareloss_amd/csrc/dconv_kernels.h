@@ -127,6 +127,63 @@ __device__ __forceinline__ void mfma_stage_bf16(const float* __restrict__ As, co
   }
 }
 
+// FP32 GEMM on the BF16 matrix cores ("x6"): each fp32 operand is split into three bf16 terms
+// v = hi + mid + lo + e (RNE at each step, exact fp32 remainders: |mid| <= 2^-8 |v|,
+// |lo| <= 2^-16 |v|, |e| <= 2^-24 |v|), and the six products down to 2^-16 relative are
+// accumulated in fp32, smallest first: lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi (a bf16 x
+// bf16 product is exact in fp32).  The dropped terms (mid*lo, lo*mid, lo*lo) and the residuals
+// sit at the 2^-24 level of fp32's own rounding, so the result is fp32-accurate (checked against
+// fp64: scripts/tune_dconv.hip x6).  Six 32x32x16 bf16 MFMAs (6 x 32 cycles) replace eight
+// 32x32x2 f32 MFMAs (8 x 64 cycles) for one 16-deep K slice.
+struct Split3 {
+  bf16x8 hi, mid, lo;
+};
+
+// matrix-core form of a conv kernel (template argument MT)
+constexpr int kMathF32 = 0, kMathBf16 = 1, kMathX6 = 2;
+
+__device__ __forceinline__ void split3_set(Split3& s, int j, float v) {
+  const __bf16 h = (__bf16)v;
+  const float r = v - (float)h;
+  const __bf16 m = (__bf16)r;
+  s.hi[j] = h;
+  s.mid[j] = m;
+  s.lo[j] = (__bf16)(r - (float)m);
+}
+
+__device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.lo, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.lo, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.mid, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.mid, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, c, 0, 0, 0);
+}
+
+// One LDS stage of fp32 operands through mfma_x6 (same operand reads as mfma_stage_bf16).
+template <int BK, int TM, int TN, int LDA_S, int LDB_S, typename F>
+__device__ __forceinline__ void mfma_stage_x6(const float* __restrict__ As, const float* __restrict__ Bs,
+                                              int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int kk = 0; kk < BK / 16; ++kk) {
+    Split3 av[TM], bv[TN];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kr = kk * 16 + 8 * h + j;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) split3_set(av[i], j, As[kr * LDA_S + wm + i * 32 + l32]);
+#pragma unroll
+      for (int t = 0; t < TN; ++t) split3_set(bv[t], j, Bs[kr * LDB_S + wn + t * 32 + l32]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) acc[i][t] = mfma_x6(av[i], bv[t], acc[i][t]);
+    if (kk == 0) mid();
+  }
+}
+
 // Forward form: C[m][p] = sum_k A[k][m] * B[k][p], BK = G * 16 (G tap-groups per K-step).
 template <int BM, int BN, int BK, int WM, int WN>
 __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
