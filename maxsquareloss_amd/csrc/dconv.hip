@@ -183,7 +183,7 @@ static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
   return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
 }
 
-template <bool BF>
+template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int dil0,
                            int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -232,27 +232,28 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     const dim3 rgrid(pl.bm * kSkBN / 1024, pl.tiles_m * pl.tiles_n);
     if (pl.bm == 128) {
       if (pl.G == 2)
-        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2, false, BF>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2, false, MT>), grid, block, 0, st, a, sk);
       else
-        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2, false, BF>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2, false, MT>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
       if (pl.G == 2)
-        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2, false, BF>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2, false, MT>), grid, block, 0, st, a, sk);
       else
-        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2, false, BF>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2, false, MT>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
     } else {
-      hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4, false, BF>), grid, block, 0, st, a, sk);
+      hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4, false, MT>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
     }
     MSL_CHECK_LAUNCH();
     return MSL_OK;
   }
-  if (BF) return MSL_ERR_SHAPE;  // the split-K tile kernel (odd K-step count, M <= 32) is f32 only
+  // the split-K tile kernel (odd K-step count, M <= 32) has no bf16 form; x6 runs it in exact f32
+  if (MT == kMathBf16) return MSL_ERR_SHAPE;
   dim3 grid(pl.tiles_n, pl.tiles_m, pl.S);
   hipLaunchKernelGGL((k_igemm_fwd<64, 128, 16, 2, 2>), grid, dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
@@ -295,7 +296,7 @@ static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P) {
   return (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float);
 }
 
-template <bool BF>
+template <int MT>
 static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
                         int taps, int cin, int cout, int h, int w, int dil0, int dil1,
                         int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -330,15 +331,15 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   const dim3 grid(pl.nw), block(256);
   const dim3 rgrid(cdiv((long long)pl.bm * pl.bn * taps, 256), pl.tiles_m * pl.tiles_n * nbranch), rblock(256);
   if (pl.bm == 128) {
-    hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2, BF>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2, MT>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
   } else if (pl.bm == 64) {
-    hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2, BF>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2, MT>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<64, 64>), rgrid, rblock, 0, st, a);
   } else {
-    hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4, BF>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4, MT>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<32, 128>), rgrid, rblock, 0, st, a);
   }
@@ -351,6 +352,21 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   return MSL_OK;
 }
 
+// Matrix-core form of the fp32 entry points (msl_conv_set_f32_form): kMathF32 runs
+// v_mfma_f32_32x32x2_f32 (an exact fmaf chain), kMathX6 the three-way bf16 split on the BF16
+// matrix cores (fp32-accurate, dconv_kernels.h).  Process-wide.
+static int g_f32_form = kMathF32;
+
+template <typename... Args>
+static int fwd_f32(Args... args) {
+  return g_f32_form == kMathX6 ? launch_fwd_form<kMathX6>(args...) : launch_fwd_form<kMathF32>(args...);
+}
+
+template <typename... Args>
+static int wgrad_f32(Args... args) {
+  return g_f32_form == kMathX6 ? launch_wgrad<kMathX6>(args...) : launch_wgrad<kMathF32>(args...);
+}
+
 }  // namespace msl
 
 using namespace msl;
@@ -360,6 +376,14 @@ extern "C" {
 int msl_abi_version(void) { return MSL_ABI_VERSION; }
 
 int msl_counter_elems(void) { return kMaxCounters; }
+
+int msl_conv_set_f32_form(int form) {
+  if (form != kMathF32 && form != kMathX6) return MSL_ERR_ARG;
+  g_f32_form = form;
+  return MSL_OK;
+}
+
+int msl_conv_f32_form(void) { return g_f32_form; }
 
 const char* msl_status_string(int status) {
   switch (status) {
@@ -395,7 +419,7 @@ int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float*
   if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<false>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
+  return fwd_f32(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
@@ -410,7 +434,7 @@ int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int n
   if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<false>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
@@ -425,7 +449,7 @@ int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, in
   if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_wgrad<false>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
+  return wgrad_f32(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
                       ws_bytes, as_stream(stream));
 }
 
@@ -449,7 +473,7 @@ size_t msl_pconv_fwd_workspace(int cin, int cout, int p) {
 int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
                   int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return launch_fwd_form<false>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
+  return fwd_f32(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
                          ws_bytes, as_stream(stream));
 }
 
@@ -461,7 +485,7 @@ size_t msl_pconv_dgrad_workspace(int cin, int cout, int p) {
 int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return launch_fwd_form<false>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
                          ws, ws_bytes, as_stream(stream));
 }
 
@@ -473,7 +497,7 @@ size_t msl_pconv_wgrad_workspace(int cin, int cout, int p) {
 int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,
                     int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
-  return launch_wgrad<false>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+  return wgrad_f32(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
                       as_stream(stream));
 }
 
@@ -487,7 +511,7 @@ int msl_dconv_fwd_bf16(const float* x, const float* packed, const float* bias, f
   if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<true>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
+  return launch_fwd_form<kMathBf16>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
@@ -497,7 +521,7 @@ int msl_dconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, 
   if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<true>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+  return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
@@ -507,28 +531,28 @@ int msl_dconv_wgrad_bf16(const float* x, const float* dy, float* dw, float* dbia
   if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_wgrad<true>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
+  return launch_wgrad<kMathBf16>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
                       ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_fwd_bf16(const float* x, const float* packed, float* y, int cin, int cout, int p,
                   int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return launch_fwd_form<true>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
+  return launch_fwd_form<kMathBf16>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
                          ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return launch_fwd_form<true>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
+  return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
                          ws, ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, int cout, int p,
                     int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
-  return launch_wgrad<true>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+  return launch_wgrad<kMathBf16>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
                       as_stream(stream));
 }
 

@@ -160,6 +160,23 @@ __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, c, 0, 0, 0);
 }
 
+// Operand fragment of a bf16 matrix-core form and its MFMA step (32x32x16: 8 k per lane).
+template <int MT> struct MathFrag { typedef bf16x8 type; };
+template <> struct MathFrag<kMathX6> { typedef Split3 type; };
+
+template <int MT>
+__device__ __forceinline__ void frag_set(typename MathFrag<MT>::type& f, int j, float v) {
+  if constexpr (MT == kMathX6) split3_set(f, j, v);
+  else f[j] = (__bf16)v;
+}
+
+template <int MT>
+__device__ __forceinline__ f32x16 frag_mma(const typename MathFrag<MT>::type& a,
+                                           const typename MathFrag<MT>::type& b, f32x16 c) {
+  if constexpr (MT == kMathX6) return mfma_x6(a, b, c);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
 // One LDS stage of fp32 operands through mfma_x6 (same operand reads as mfma_stage_bf16).
 template <int BK, int TM, int TN, int LDA_S, int LDB_S, typename F>
 __device__ __forceinline__ void mfma_stage_x6(const float* __restrict__ As, const float* __restrict__ Bs,
@@ -563,7 +580,7 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
   return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
 }
 
-template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, bool BF = false>
+template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0>
 __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -734,8 +751,10 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       auto mid = [&] {
         if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
       };
-      if constexpr (BF)
+      if constexpr (MT == kMathBf16)
         mfma_stage_bf16<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
+      else if constexpr (MT == kMathX6)
+        mfma_stage_x6<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else
         mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -870,12 +889,12 @@ struct WskArgs {
 
 constexpr int kWskBK = 64;
 
-template <int BM, int BN, int STAGES, int WM, int WN, bool BF = false>
+template <int BM, int BN, int STAGES, int WM, int WN, int MT = 0>
 __global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
   static_assert(WM * WN == 4, "4 waves");
-  // row stride: 66 floats for the f32 b64 reads (64 distinct banks); 68 for the bf16 form's
+  // row stride: 66 floats for the f32 b64 reads (64 distinct banks); 68 for the bf16 forms'
   // 16-B aligned b128 reads (4-dword chunks at 4*row: conflict-free per 16-lane group)
-  constexpr int kWskLD = BF ? 68 : 66;
+  constexpr int kWskLD = MT != kMathF32 ? 68 : 66;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(TM >= 1 && TN >= 1, "tiles");
   constexpr int A_STAGE = BM * kWskLD, STAGE = (BM + BN) * kWskLD;
@@ -961,31 +980,27 @@ __global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
       const float* As = smem + (i % STAGES) * STAGE;
       const float* Bs = As + A_STAGE;
       typedef float f32x2 __attribute__((ext_vector_type(2)));
-      if constexpr (BF) {
+      if constexpr (MT != kMathF32) {
         // lane (r, h) of v_mfma_f32_32x32x16_bf16 takes pixels kk*16 + 8h .. +7 of row r
+        typedef typename MathFrag<MT>::type Frag;
 #pragma unroll
         for (int kk = 0; kk < kWskBK / 16; ++kk) {
           const int kc = kk * 16 + 8 * kh;
-          bf16x8 av[TM], bv[TN];
-#pragma unroll
-          for (int ii = 0; ii < TM; ++ii) {
-            const float4* src = reinterpret_cast<const float4*>(As + (wm + ii * 32 + l32) * kWskLD + kc);
+          Frag av[TM], bv[TN];
+          auto rd8 = [&](Frag& f, const float* row) {
+            const float4* src = reinterpret_cast<const float4*>(row + kc);
             const float4 u = src[0], v = src[1];
-            av[ii][0] = (__bf16)u.x; av[ii][1] = (__bf16)u.y; av[ii][2] = (__bf16)u.z; av[ii][3] = (__bf16)u.w;
-            av[ii][4] = (__bf16)v.x; av[ii][5] = (__bf16)v.y; av[ii][6] = (__bf16)v.z; av[ii][7] = (__bf16)v.w;
-          }
+            frag_set<MT>(f, 0, u.x); frag_set<MT>(f, 1, u.y); frag_set<MT>(f, 2, u.z); frag_set<MT>(f, 3, u.w);
+            frag_set<MT>(f, 4, v.x); frag_set<MT>(f, 5, v.y); frag_set<MT>(f, 6, v.z); frag_set<MT>(f, 7, v.w);
+          };
 #pragma unroll
-          for (int jj = 0; jj < TN; ++jj) {
-            const float4* src = reinterpret_cast<const float4*>(Bs + (wn + jj * 32 + l32) * kWskLD + kc);
-            const float4 u = src[0], v = src[1];
-            bv[jj][0] = (__bf16)u.x; bv[jj][1] = (__bf16)u.y; bv[jj][2] = (__bf16)u.z; bv[jj][3] = (__bf16)u.w;
-            bv[jj][4] = (__bf16)v.x; bv[jj][5] = (__bf16)v.y; bv[jj][6] = (__bf16)v.z; bv[jj][7] = (__bf16)v.w;
-          }
+          for (int ii = 0; ii < TM; ++ii) rd8(av[ii], As + (wm + ii * 32 + l32) * kWskLD);
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj) rd8(bv[jj], Bs + (wn + jj * 32 + l32) * kWskLD);
 #pragma unroll
           for (int ii = 0; ii < TM; ++ii)
 #pragma unroll
-            for (int jj = 0; jj < TN; ++jj)
-              acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[ii], bv[jj], acc[ii][jj], 0, 0, 0);
+            for (int jj = 0; jj < TN; ++jj) acc[ii][jj] = frag_mma<MT>(av[ii], bv[jj], acc[ii][jj]);
         }
       } else {
 #pragma unroll

@@ -26,6 +26,28 @@ def set_conv_math(math):
     CONV_MATH = math
 
 
+# Matrix-core form of the fp32 conv math, held process-wide by the library
+# (msl_conv_set_f32_form): "mfma_f32" = v_mfma_f32_32x32x2_f32, an exact fmaf chain; "bf16x6" =
+# each operand split into three bf16 terms, six products per 16-deep K slice on
+# v_mfma_f32_32x32x16_bf16 with fp32 sums (fp32-accurate; csrc/dconv_kernels.h Split3).
+F32_FORMS = {"mfma_f32": 0, "bf16x6": 2}
+
+
+def set_f32_form(form):
+    """Select the fp32 conv form; returns the previous one."""
+    if form not in F32_FORMS:
+        raise ValueError(f"fp32 conv form must be one of {sorted(F32_FORMS)}, got {form!r}")
+    lib = hip.load(require_gpu=False)
+    prev = lib.msl_conv_f32_form()
+    hip.check(lib.msl_conv_set_f32_form(F32_FORMS[form]), "msl_conv_set_f32_form")
+    return {v: k for k, v in F32_FORMS.items()}[prev]
+
+
+def f32_form():
+    lib = hip.load(require_gpu=False)
+    return {v: k for k, v in F32_FORMS.items()}[lib.msl_conv_f32_form()]
+
+
 def _fn(lib, name, math):
     return getattr(lib, name + "_bf16") if math == "bf16" else getattr(lib, name)
 

@@ -78,7 +78,7 @@ float run_fwd_dma(const Shape& sh, const float* x, const float* wp, float* y, fl
   return ms / iters;
 }
 
-template <int BM, int BN, int G, int STAGES, int WM, int WN>
+template <int BM, int BN, int G, int STAGES, int WM, int WN, int MT = 0>
 float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda, int* flags) {
   const int P = sh.h * sh.w;
   FwdArgs a;
@@ -97,7 +97,7 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   CK(hipMemset(flags, 0, 1 << 20));
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, WM, WN>), dim3(NW), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, WM, WN, false, MT>), dim3(NW), dim3(256), 0, 0, a, sk);
     hipLaunchKernelGGL((k_sk_reduce<BM, BN>), dim3(BM * BN / 1024, tiles), dim3(256), 0, 0, a, sk);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
@@ -128,7 +128,7 @@ float run_wgrad(const Shape& sh, const float* x, const float* dy, float* dw, flo
   return ms / iters;
 }
 
-template <int BM, int BN, int ST>
+template <int BM, int BN, int ST, int MT = 0>
 float run_wgrad_sk(const Shape& sh, const float* x, const float* dy, float* dw, float* ws, int NWmax, int iters) {
   const int P = sh.h * sh.w;
   WskArgs a;
@@ -142,7 +142,7 @@ float run_wgrad_sk(const Shape& sh, const float* x, const float* dy, float* dw, 
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((k_wgrad_sk<BM, BN, ST, (BM >= 64 ? 2 : 1), (BM >= 64 ? 2 : 4)>), dim3(a.NW), dim3(256), 0, 0, a);
+    hipLaunchKernelGGL((k_wgrad_sk<BM, BN, ST, (BM >= 64 ? 2 : 1), (BM >= 64 ? 2 : 4), MT>), dim3(a.NW), dim3(256), 0, 0, a);
     hipLaunchKernelGGL((k_wsk_reduce<BM, BN>), dim3(BM * BN * 9 / 256, a.tiles_m * a.tiles_n), dim3(256), 0, 0, a);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
@@ -160,15 +160,81 @@ static double maxdiff(const float* a, const float* b, size_t n, double* scale) {
   return m;
 }
 
+static unsigned lcg(unsigned& s) { s = s * 1664525u + 1013904223u; return s >> 8; }
+
+// fp64 forward reference at sampled (cout, pixel) outputs.  Weights are the tap-major pack:
+// row k = (tap * ncb + ci / 16) * 16 + ci % 16, column cout, stride lda.  Error relative to the
+// sum of |terms| of that output.
+static void err64_fwd(const Shape& sh, const std::vector<float>& hx, const std::vector<float>& hw, int lda,
+                      const float* dev, double* mx, double* rms) {
+  const int P = sh.h * sh.w, ncb = (sh.cin + 15) / 16;
+  std::vector<float> hy((size_t)sh.cout * P);
+  CK(hipMemcpy(hy.data(), dev, hy.size() * 4, hipMemcpyDeviceToHost));
+  unsigned s = 12345;
+  double m = 0, q = 0;
+  const int NS = 3000;
+  for (int i = 0; i < NS; ++i) {
+    const int co = lcg(s) % sh.cout, p = lcg(s) % P;
+    const int py = p / sh.w, px = p % sh.w;
+    double acc = 0, mag = 0;
+    for (int t = 0; t < 9; ++t) {
+      const int yy = py + (t / 3 - 1) * sh.dil, xx = px + (t % 3 - 1) * sh.dil;
+      if (yy < 0 || yy >= sh.h || xx < 0 || xx >= sh.w) continue;
+      for (int ci = 0; ci < sh.cin; ++ci) {
+        const double v = (double)hw[((size_t)(t * ncb + ci / 16) * 16 + ci % 16) * lda + co] *
+                         (double)hx[(size_t)ci * P + yy * sh.w + xx];
+        acc += v;
+        mag += std::fabs(v);
+      }
+    }
+    const double e = std::fabs((double)hy[(size_t)co * P + p] - acc) / (mag > 0 ? mag : 1.0);
+    m = std::max(m, e);
+    q += e * e;
+  }
+  *mx = m;
+  *rms = std::sqrt(q / NS);
+}
+
+// fp64 weight-gradient reference at sampled (cout, cin, tap): dW = sum_p dY[co][p] X[ci][p + shift]
+static void err64_wgrad(const Shape& sh, const std::vector<float>& hx, const std::vector<float>& hdy,
+                        const float* dev, double* mx, double* rms) {
+  const int P = sh.h * sh.w;
+  std::vector<float> hd((size_t)sh.cout * sh.cin * 9);
+  CK(hipMemcpy(hd.data(), dev, hd.size() * 4, hipMemcpyDeviceToHost));
+  unsigned s = 777;
+  double m = 0, q = 0;
+  const int NS = 600;
+  for (int i = 0; i < NS; ++i) {
+    const int co = lcg(s) % sh.cout, ci = lcg(s) % sh.cin, t = lcg(s) % 9;
+    const int dh = (t / 3 - 1) * sh.dil, dw = (t % 3 - 1) * sh.dil;
+    double acc = 0, mag = 0;
+    for (int p = 0; p < P; ++p) {
+      const int yy = p / sh.w + dh, xx = p % sh.w + dw;
+      if (yy < 0 || yy >= sh.h || xx < 0 || xx >= sh.w) continue;
+      const double v = (double)hdy[(size_t)co * P + p] * (double)hx[(size_t)ci * P + yy * sh.w + xx];
+      acc += v;
+      mag += std::fabs(v);
+    }
+    const double e = std::fabs((double)hd[((size_t)co * sh.cin + ci) * 9 + t] - acc) / (mag > 0 ? mag : 1.0);
+    m = std::max(m, e);
+    q += e * e;
+  }
+  *mx = m;
+  *rms = std::sqrt(q / NS);
+}
+
 int main(int argc, char** argv) {
   // "sk": only the library's stream-K configuration on the layer3 shape (profiling runs)
   const bool sk_only = argc > 1 && std::string(argv[1]) == "sk";
   // "fsk": every stream-K row, nothing else
   const bool fsk_only = argc > 1 && std::string(argv[1]) == "fsk";
   const bool wsk_only = argc > 1 && std::string(argv[1]) == "wsk";
+  // "x6": the matrix-core forms (f32, bf16, bf16x6) of the stream-K kernels vs an fp64 reference
+  const bool x6_mode = argc > 1 && std::string(argv[1]) == "x6";
   const int iters = sk_only ? 5 : 20;
   Shape shapes[] = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
   for (const Shape& sh : shapes) {
+    if (x6_mode && (sh.cin != sh.cout || sh.h != 65)) continue;  // the model's layer3 / layer4 shapes
     const int P = sh.h * sh.w;
     const int lda = (sh.cout + 127) / 128 * 128;
     const long long kp = (long long)((sh.cin + 15) / 16) * 9 * 16;
@@ -204,6 +270,22 @@ int main(int argc, char** argv) {
 #define WSK(BM, BN, ST, NW) { float ms = run_wgrad_sk<BM, BN, ST>(sh, x, dy, dw, ws, NW, iters); \
       double md = maxdiff(dw, dwref, (size_t)sh.cout * sh.cin * 9, &sc); \
       printf("wsk   BM %3d BN %3d ST %d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, ST, NW, ms * 1e3, gf / ms, md, sc); }
+    if (x6_mode) {
+      double mx, rms;
+#define FSKE(BM, BN, G, ST, WM, WN, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_fwd_sk<BM, BN, G, ST, WM, WN, MT>(sh, x, wp, y, ws, NW, iters, lda, flags); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms); \
+      printf("fsk  MT %d BM %3d BN %3d G %d ST %d NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, BN, G, ST, NW, ms * 1e3, gf / ms, mx, rms); }
+#define WSKE(BM, BN, ST, NW, MT) { float ms = run_wgrad_sk<BM, BN, ST, MT>(sh, x, dy, dw, ws, NW, iters); \
+      err64_wgrad(sh, hx, hdy, dw, &mx, &rms); \
+      printf("wsk  MT %d BM %3d BN %3d ST %d NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, BN, ST, NW, ms * 1e3, gf / ms, mx, rms); }
+      FSKE(128, 128, 2, 2, 2, 2, 512, 0) FSKE(128, 128, 2, 2, 2, 2, 512, 1) FSKE(128, 128, 2, 2, 2, 2, 512, 2)
+      FSKE(128, 128, 2, 2, 2, 2, 256, 2) FSKE(128, 128, 1, 3, 2, 2, 512, 2) FSKE(128, 128, 2, 3, 2, 2, 256, 2)
+      FSKE(128, 128, 4, 2, 2, 2, 256, 2) FSKE(64, 128, 2, 2, 2, 2, 768, 2)
+      WSKE(64, 64, 2, 512, 0) WSKE(64, 64, 2, 512, 1) WSKE(64, 64, 2, 512, 2)
+      WSKE(128, 128, 2, 256, 0) WSKE(128, 128, 2, 256, 2) WSKE(64, 128, 2, 512, 2)
+      continue;
+    }
     if (wsk_only) {
       run_wgrad<64, 128, 32, 2, 2>(sh, x, dy, dwref, ws, 1, 1);
       WGR(64, 128, 32, 2, 2, 8)

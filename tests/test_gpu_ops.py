@@ -17,6 +17,14 @@ from maxsquareloss_amd import ops  # noqa: E402
 DEV = "cuda"
 
 
+@pytest.fixture(params=["mfma_f32", "bf16x6"])
+def f32_form(request):
+    """Both matrix-core forms of the fp32 convs are held to the same fp64 tolerance."""
+    prev = ops.set_f32_form(request.param)
+    yield request.param
+    ops.set_f32_form(prev)
+
+
 def _rel(a, b):
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()
@@ -30,7 +38,7 @@ def _conv_ref(x, w, d, bias=None):
 @pytest.mark.parametrize("cin,cout,h,w,d", [
     (256, 256, 17, 33, 2), (512, 512, 17, 33, 4), (64, 64, 33, 65, 1), (32, 48, 9, 13, 2),
     (256, 256, 65, 129, 2)])
-def test_dconv_fwd_bwd(cin, cout, h, w, d):
+def test_dconv_fwd_bwd(cin, cout, h, w, d, f32_form):
     g = torch.Generator().manual_seed(cin * 7 + h)
     x = torch.randn(1, cin, h, w, generator=g)
     wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.05
@@ -52,7 +60,7 @@ def test_dconv_fwd_bwd(cin, cout, h, w, d):
 @pytest.mark.parametrize("cin,cout,h,w", [
     (64, 256, 33, 65), (256, 64, 33, 65), (1024, 256, 17, 33), (48, 160, 9, 13), (512, 2048, 17, 33),
     (2048, 512, 65, 129), (256, 1024, 65, 129)])
-def test_pconv_fwd_bwd(cin, cout, h, w):
+def test_pconv_fwd_bwd(cin, cout, h, w, f32_form):
     g = torch.Generator().manual_seed(cin * 3 + cout)
     x = torch.randn(1, cin, h, w, generator=g)
     wt = torch.randn(cout, cin, 1, 1, generator=g) * 0.05
@@ -99,7 +107,7 @@ def test_conv1x1_library_gemms(cin, cout, h, w):
 
 
 @pytest.mark.parametrize("cin,c,h,w", [(1024, 19, 17, 33), (2048, 19, 33, 65), (96, 16, 9, 17), (64, 13, 65, 129)])
-def test_aspp2_fwd_bwd(cin, c, h, w):
+def test_aspp2_fwd_bwd(cin, c, h, w, f32_form):
     g = torch.Generator().manual_seed(cin + c)
     x = torch.randn(1, cin, h, w, generator=g)
     w0 = torch.randn(c, cin, 3, 3, generator=g) * 0.01
