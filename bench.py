@@ -134,13 +134,17 @@ def main():
             traffic = json.load(open(a.pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    peak = BF16_MFMA_PEAK_TFLOPS if a.conv_math == "bf16" else FP32_MFMA_PEAK_TFLOPS
-    if a.conv_math != "fp32":
-        traffic = None  # the committed PMC figure is for the fp32 kernel
+    form = ops.f32_form() if a.conv_math == "fp32" else "bf16"
+    # the bound of the kernel's own arithmetic: FP32 MFMA, BF16 MFMA, or BF16 MFMA at six
+    # products per fp32 product (the bf16x6 form): 2500 / 6 = 416.7 fp32-equivalent TFLOP/s
+    peak = {"mfma_f32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
+            "bf16x6": round(BF16_MFMA_PEAK_TFLOPS / 6, 1)}[form]
+    if traffic is not None and json.load(open(a.pmc)).get("form", "mfma_f32") != form:
+        traffic = None  # the committed PMC figure belongs to another form of the kernel
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": "dconv3x3 fwd layer3 d=2 (stream-K k_igemm_fwd_sk + k_sk_reduce, one op call)",
-                "kernel_ms": round(kern_ms, 4), "launches": len(probes),
+                "form": form, "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
 
     cpu = None

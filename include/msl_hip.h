@@ -47,9 +47,9 @@ const char* msl_status_string(int status);
 int msl_counter_elems(void);
 
 /* Matrix-core form of the fp32 conv entry points (msl_dconv_* / msl_pconv_* without _bf16),
- * process-wide: 0 = v_mfma_f32_32x32x2_f32 (exact fmaf chain, the default), 2 = each fp32
- * operand split into three bf16 terms, six products per 16-deep K slice on
- * v_mfma_f32_32x32x16_bf16 with fp32 accumulation (fp32-accurate).  Returns MSL_ERR_ARG for
+ * process-wide: 0 = v_mfma_f32_32x32x2_f32 (exact fmaf chain), 2 = each fp32 operand split
+ * into three bf16 terms, six products per 16-deep K slice on v_mfma_f32_32x32x16_bf16 with fp32
+ * accumulation (fp32-accurate; the default).  Returns MSL_ERR_ARG for
  * any other value.  Replaces nothing in the reference (its convs are cuDNN fp32). */
 int msl_conv_set_f32_form(int form);
 int msl_conv_f32_form(void);

@@ -155,9 +155,13 @@ struct WgradPlan {
   long long T;
 };
 
-static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P) {
+static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, bool x6 = false) {
   WgradPlan pl;
-  if (cout <= 32) {
+  if (x6 && cout >= 128 && cin >= 128) {
+    // x6: 128x128 tiles (2 x 2 fragments per wave amortise the operand splits); 110 vs 130 us
+    // on layer3, 390 vs 428 on layer4 (scripts/tune_dconv.hip x6)
+    pl.bm = 128; pl.bn = 128; pl.nw = 256;
+  } else if (cout <= 32) {
     pl.bm = 32; pl.bn = 128; pl.nw = 256;
   } else if (cout >= 512 && cin >= 512) {
     pl.bm = 128; pl.bn = 128; pl.nw = 256;
@@ -189,6 +193,15 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
                            int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st) {
   const int P = h * w;
   FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
+  // The x6 form runs one K-step per stage, three stages deep (scripts/tune_dconv.hip x6, layer3:
+  // 87 us vs 115 with two K-steps per stage; f32 is indifferent); its 64- and 32-row tiles stay
+  // on exact f32 MFMA (no gain measured there).
+  constexpr int MS = MT == kMathX6 ? kMathF32 : MT;
+  if (MT == kMathX6 && pl.sk && pl.bm == 128) {
+    pl.G = 1;
+    pl.bk = kCB;
+    pl.kps = pl.ksteps;
+  }
   if (ws_bytes < fwd_ws_bytes(pl, M, P)) return MSL_ERR_WORKSPACE;
   FwdArgs a;
   a.A = packed;
@@ -239,13 +252,13 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
       hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
       if (pl.G == 2)
-        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2, false, MT>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2, false, MS>), grid, block, 0, st, a, sk);
       else
-        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2, false, MT>), grid, block, 0, st, a, sk);
+        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2, false, MS>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
     } else {
-      hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4, false, MT>), grid, block, 0, st, a, sk);
+      hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4, false, MS>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
     }
@@ -292,8 +305,13 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
 }
 
 static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P) {
-  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P);
-  return (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float);
+  // large enough for either fp32 form
+  size_t b = 0;
+  for (int x6 = 0; x6 < 2; ++x6) {
+    WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, x6 != 0);
+    b = std::max(b, (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float));
+  }
+  return b;
 }
 
 template <int MT>
@@ -301,7 +319,8 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
                         int taps, int cin, int cout, int h, int w, int dil0, int dil1,
                         int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
   const int P = h * w;
-  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P);
+  constexpr int MS = MT == kMathX6 ? kMathF32 : MT;  // x6 only on 128x128 tiles (plan_wgrad)
+  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, MT == kMathX6);
   if (ws_bytes < wgrad_ws_bytes(nbranch, taps, cin, cout, P)) return MSL_ERR_WORKSPACE;
   if (pl.T * pl.nw >= (1LL << 31) || (long long)pl.nw * pl.slots * pl.bm * pl.bn * 4 >= (1LL << 31) || (long long)std::max(cin, cout) * P >= (1LL << 29) ||
       (long long)P + kWskBK >= (1LL << 22))
@@ -335,11 +354,11 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
   } else if (pl.bm == 64) {
-    hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2, MT>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2, MS>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<64, 64>), rgrid, rblock, 0, st, a);
   } else {
-    hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4, MT>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4, MS>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<32, 128>), rgrid, rblock, 0, st, a);
   }
@@ -354,8 +373,9 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
 
 // Matrix-core form of the fp32 entry points (msl_conv_set_f32_form): kMathF32 runs
 // v_mfma_f32_32x32x2_f32 (an exact fmaf chain), kMathX6 the three-way bf16 split on the BF16
-// matrix cores (fp32-accurate, dconv_kernels.h).  Process-wide.
-static int g_f32_form = kMathF32;
+// matrix cores (fp32-accurate, dconv_kernels.h; the default: layer3 fwd 78 vs 102 us in the
+// step, err vs fp64 4e-8 vs 6e-8 relative to sum|terms|).  Process-wide.
+static int g_f32_form = kMathX6;
 
 template <typename... Args>
 static int fwd_f32(Args... args) {

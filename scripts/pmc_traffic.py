@@ -10,6 +10,7 @@ import json
 import sys
 
 fetch_csv, write_csv, kernels, out = sys.argv[1:5]
+form = sys.argv[5] if len(sys.argv) > 5 else "bf16x6"  # the fp32 form the profiled run used
 
 
 def per_launch(path, counter, name):
@@ -25,7 +26,7 @@ fs = [per_launch(fetch_csv, "FETCH_SIZE", n) for n in names]
 ws = [per_launch(write_csv, "WRITE_SIZE", n) for n in names]
 f, nf = sum(v for v, _ in fs), [n for _, n in fs]
 w, nw = sum(v for v, _ in ws), [n for _, n in ws]
-res = {"kernel": kernels, "launches": [nf, nw], "fetch_size_kib": f, "write_size_kib": w,
+res = {"kernel": kernels, "form": form, "launches": [nf, nw], "fetch_size_kib": f, "write_size_kib": w,
        "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024),
        "note": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), gfx950 FETCH_SIZE correction; "
                "per-launch figures of the listed kernels summed"}
