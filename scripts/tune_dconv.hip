@@ -108,6 +108,32 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   return ms / iters;
 }
 
+template <int BM, int MT>
+float run_rg(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda) {
+  const int P = sh.h * sh.w;
+  FwdArgs a;
+  a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
+  a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
+  a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
+  a.ksteps = a.ncb * 9; a.kps = a.ksteps; a.slab = 0; a.taps = 9;
+  SkArgs sk;
+  sk.part = ws; sk.flags = nullptr;
+  sk.tiles_m = (sh.cout + BM - 1) / BM; sk.tiles_n = (P + 127) / 128; sk.KS = a.ncb * 3;
+  sk.T = sk.tiles_m * sk.tiles_n * sk.KS;
+  sk.NW = std::min(NW, sk.T);
+  const int tiles = sk.tiles_m * sk.tiles_n;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_conv_rg<BM, 128, 2, 2, MT>), dim3(sk.NW), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_sk_reduce<BM, 128>), dim3(BM * 128 / 1024, tiles), dim3(256), 0, 0, a, sk);
+  }
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
 template <int BM, int BN, int BK, int WM, int WN>
 float run_wgrad(const Shape& sh, const float* x, const float* dy, float* dw, float* ws, int S, int iters) {
   const int P = sh.h * sh.w;
@@ -231,10 +257,12 @@ int main(int argc, char** argv) {
   const bool wsk_only = argc > 1 && std::string(argv[1]) == "wsk";
   // "x6": the matrix-core forms (f32, bf16, bf16x6) of the stream-K kernels vs an fp64 reference
   const bool x6_mode = argc > 1 && std::string(argv[1]) == "x6";
+  // "rg": the row-grouped forward kernel (k_conv_rg) vs the stream-K one, every form, vs fp64
+  const bool rg_mode = argc > 1 && std::string(argv[1]) == "rg";
   const int iters = sk_only ? 5 : 20;
   Shape shapes[] = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
   for (const Shape& sh : shapes) {
-    if (x6_mode && (sh.cin != sh.cout || sh.h != 65)) continue;  // the model's layer3 / layer4 shapes
+    if ((x6_mode || rg_mode) && (sh.cin != sh.cout || sh.h != 65)) continue;  // the model's layer3 / layer4 shapes
     const int P = sh.h * sh.w;
     const int lda = (sh.cout + 127) / 128 * 128;
     const long long kp = (long long)((sh.cin + 15) / 16) * 9 * 16;
@@ -270,6 +298,23 @@ int main(int argc, char** argv) {
 #define WSK(BM, BN, ST, NW) { float ms = run_wgrad_sk<BM, BN, ST>(sh, x, dy, dw, ws, NW, iters); \
       double md = maxdiff(dw, dwref, (size_t)sh.cout * sh.cin * 9, &sc); \
       printf("wsk   BM %3d BN %3d ST %d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, ST, NW, ms * 1e3, gf / ms, md, sc); }
+#define FSKE(BM, BN, G, ST, WM, WN, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_fwd_sk<BM, BN, G, ST, WM, WN, MT>(sh, x, wp, y, ws, NW, iters, lda, flags); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms); \
+      printf("fsk  MT %d BM %3d BN %3d G %d ST %d NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, BN, G, ST, NW, ms * 1e3, gf / ms, mx, rms); }
+#define WSKE(BM, BN, ST, NW, MT) { float ms = run_wgrad_sk<BM, BN, ST, MT>(sh, x, dy, dw, ws, NW, iters); \
+      err64_wgrad(sh, hx, hdy, dw, &mx, &rms); \
+      printf("wsk  MT %d BM %3d BN %3d ST %d NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, BN, ST, NW, ms * 1e3, gf / ms, mx, rms); }
+    if (rg_mode) {
+      double mx, rms;
+#define RGE(BM, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_rg<BM, MT>(sh, x, wp, y, ws, NW, iters, lda); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms); \
+      printf("rg   MT %d BM %3d         NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, NW, ms * 1e3, gf / ms, mx, rms); }
+      FSKE(128, 128, 2, 2, 2, 2, 512, 0) FSKE(128, 128, 1, 3, 2, 2, 512, 2) FSKE(128, 128, 2, 2, 2, 2, 512, 1)
+      RGE(128, 512, 0) RGE(128, 256, 0) RGE(128, 512, 2) RGE(128, 256, 2) RGE(128, 512, 1) RGE(64, 768, 0) RGE(64, 512, 2)
+      continue;
+    }
     if (x6_mode) {
       double mx, rms;
 #define FSKE(BM, BN, G, ST, WM, WN, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 #include "dconv_kernels.h"
 
@@ -41,7 +42,7 @@ static double maxdiff(const float* a, const float* b, size_t n, double* scale) {
 
 struct Shape { int cimg, M, P; };
 
-template <int BM, int BN, int G, int STAGES, bool PW>
+template <int BM, int BN, int G, int STAGES, bool PW, int MT = 0>
 float run_sk(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int* flags, int NW, int iters, int lda) {
   FwdArgs a;
   a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
@@ -59,7 +60,8 @@ float run_sk(const Shape& sh, const float* x, const float* wp, float* y, float* 
   CK(hipMemset(flags, 0, 1 << 20));
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, 2, 2, PW>), dim3(sk.NW), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, 2, 2, PW, MT>), dim3(sk.NW), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_sk_reduce<BM, BN>), dim3(BM * BN / 1024, sk.tiles_m * sk.tiles_n), dim3(256), 0, 0, a, sk);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -67,7 +69,9 @@ float run_sk(const Shape& sh, const float* x, const float* wp, float* y, float* 
 }
 
 int main(int argc, char** argv) {
-  const bool big_only = argc > 1;
+  // "x6": the current library configuration (f32, G2 ST2 NW512) against the bf16x6 form
+  const bool x6_mode = argc > 1 && std::string(argv[1]) == "x6";
+  const bool big_only = argc > 1 && !x6_mode;
   const int iters = 20;
   // (cimg, M, P): fwd of conv1/conv3/downsample and the dgrad forms (cimg = cout, M = cin)
   Shape shapes[] = {{4096, 4096, 4096}, {1024, 256, 8385}, {256, 1024, 8385}, {512, 1024, 8385}, {2048, 512, 8385},
@@ -93,6 +97,19 @@ int main(int argc, char** argv) {
       float ms = run_sk<BM, BN, G, ST, PW>(sh, x, wp, y, ws, flags, NW, iters, lda); \
       double md = maxdiff(y, yref, (size_t)sh.M * sh.P, &sc); \
       printf("sk BM %3d BN %3d G %d ST %d PW %d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", BM, BN, G, ST, (int)PW, NW, ms * 1e3, gf / ms, md, sc); }
+#define SKM(BM, G, ST, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.M * sh.P * 4)); \
+      float ms = run_sk<BM, 128, G, ST, false, MT>(sh, x, wp, y, ws, flags, NW, iters, lda); \
+      double md = maxdiff(y, yref, (size_t)sh.M * sh.P, &sc); \
+      printf("sk MT %d BM %3d G %d ST %d NW %4d : %8.1f us %7.1f TF  maxdiff %.2e/%.2e\n", MT, BM, G, ST, NW, ms * 1e3, gf / ms, md, sc); }
+    if (x6_mode) {
+      if (sh.P == 4096) continue;
+      if (sh.M >= 128) {
+        SKM(128, 2, 2, 512, 0) SKM(128, 1, 3, 512, 2) SKM(128, 1, 3, 256, 2) SKM(128, 2, 2, 512, 2) SKM(128, 1, 4, 512, 2)
+      } else {
+        SKM(64, 2, 2, 512, 0) SKM(64, 1, 3, 512, 2)
+      }
+      continue;
+    }
     if (sh.M >= 128) {
       SK(128, 128, 2, 2, false, 512) SK(128, 128, 2, 2, true, 512) SK(128, 128, 2, 3, true, 256)
       SK(128, 128, 4, 2, true, 256) SK(128, 128, 2, 2, true, 256) SK(128, 128, 1, 3, true, 512)
