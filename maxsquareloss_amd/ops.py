@@ -277,7 +277,8 @@ class _Conv1x1(Function):
     """1x1, stride-1, bias-free conv as three plain GEMMs, each on the library that is fastest for
     it on MI355X (scripts/bench_mm.py, profiles/r01_gemm_libraries.txt):
       y  = W x        MIOpen (rocBLAS kernels)
-      dx = W^T dy     hipBLASLt (torch.mm) when cout > cin, else MIOpen
+      dx = W^T dy     the HIP bf16x6 pointwise dgrad when cout > cin >= 128 at <= 16k pixels
+                      (that form only), else hipBLASLt (torch.mm) when cout > cin, else MIOpen
       dW += dy x^T    hipBLASLt addmm straight into the flat gradient buffer (beta = 1), or the
                       HIP pointwise wgrad at the 33k-pixel layer1 maps where it is the fastest.
     """
@@ -301,7 +302,18 @@ class _Conv1x1(Function):
         w2 = weight.view(cout, cin)
         dx = None
         if ctx.needs_input_grad[0]:
-            if cout > cin:
+            if cout > cin and cin >= 128 and p <= 16384 and f32_form() == "bf16x6":
+                # HIP x6 pointwise dgrad (layer3 conv3 256<-1024: 48.6 vs 65.2 us on hipBLASLt,
+                # profiles/r01_tune_pconv_x6.txt; layer4 conv3 512<-2048: 154.6 vs 166.7)
+                lib = hip.load()
+                packed_d = ctx.cache.get([weight], cin, cout, 1)
+                dx = torch.empty_like(x)
+                wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
+                ws = hip.workspace(wsb, x.device)
+                hip.check(lib.msl_pconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
+                                              hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                                              hip.stream_ptr()), "msl_pconv_dgrad")
+            elif cout > cin:
                 dx = torch.mm(w2.t(), g2).view(1, cin, h, w)
             else:
                 dx = torch.ops.aten.convolution_backward(gy, x, weight, None, (1, 1), (0, 0), (1, 1), False,
