@@ -182,8 +182,13 @@ static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, boo
 // stream-K workspace: the published pieces, NW x 2 x BM*BN floats.  The arrival counters live in
 // a caller-owned, persistent int[kMaxCounters] that is zero on entry and left zero on exit (the
 // finishing workgroup of each tile re-arms its counter), so no per-call memset is needed.
+// bytes of the pre-split A planes the x6 form stages its weights from (k_split_pack)
+static size_t x6_planes_bytes(const FwdPlan& pl, int M) {
+  return pl.sk && pl.bm == 128 ? (size_t)pl.ksteps * 6 * pad_to(M, kPackPad) * 16 : 0;
+}
+
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
-  if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float);
+  if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float) + x6_planes_bytes(pl, M);
   return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
 }
 
@@ -204,6 +209,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   }
   if (ws_bytes < fwd_ws_bytes(pl, M, P)) return MSL_ERR_WORKSPACE;
   FwdArgs a;
+  a.Ax6 = nullptr;
   a.A = packed;
   a.B = img;
   a.C = pl.S > 1 ? (float*)ws : out;
@@ -243,7 +249,18 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     a.bias = bias;
     const dim3 grid(sk.NW), block(256);
     const dim3 rgrid(pl.bm * kSkBN / 1024, pl.tiles_m * pl.tiles_n);
-    if (pl.bm == 128) {
+    if (MT == kMathX6 && pl.bm == 128) {
+      // weights split into bf16 planes once per call, then the x6 kernel stages them directly
+      __bf16* planes = (__bf16*)((char*)ws + (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float));
+      const long long n = (long long)pl.ksteps * kCB * a.lda;
+      hipLaunchKernelGGL(k_split_pack, dim3((int)std::min<long long>(cdiv(n, 256), 4096)), block, 0, st,
+                         packed, pl.ksteps, a.lda, planes);
+      MSL_CHECK_LAUNCH();
+      a.Ax6 = planes;
+      hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 4, 2, 2, false, kMathX6P>), grid, block, 0, st, a, sk);
+      MSL_CHECK_LAUNCH();
+      hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
+    } else if (pl.bm == 128) {
       if (pl.G == 2)
         hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2, false, MT>), grid, block, 0, st, a, sk);
       else

@@ -21,6 +21,7 @@ struct FwdArgs {
   int M, lda, H, W, P, cimg, ncb, dil0, dil1, ksteps, kps;  // ksteps counts BK-deep steps
   int taps;           // 9 (3x3) or 1 (pointwise: dil0 = 0, so the single tap has no shift)
   long long slab;
+  const void* Ax6;    // kMathX6P: A split into bf16 planes [ks][plane][k half][lda][8] (k_split_pack)
 };
 
 struct WgradArgs {
@@ -140,7 +141,9 @@ struct Split3 {
 };
 
 // matrix-core form of a conv kernel (template argument MT)
-constexpr int kMathF32 = 0, kMathBf16 = 1, kMathX6 = 2;
+// kMathX6P: the x6 form with the A operand (packed weights) split once per call by
+// k_split_pack instead of per read (fwd form only)
+constexpr int kMathF32 = 0, kMathBf16 = 1, kMathX6 = 2, kMathX6P = 3;
 
 __device__ __forceinline__ void split3_set(Split3& s, int j, float v) {
   const __bf16 h = (__bf16)v;
@@ -190,6 +193,62 @@ __device__ __forceinline__ void mfma_stage_x6(const float* __restrict__ As, cons
       const int kr = kk * 16 + 8 * h + j;
 #pragma unroll
       for (int i = 0; i < TM; ++i) split3_set(av[i], j, As[kr * LDA_S + wm + i * 32 + l32]);
+#pragma unroll
+      for (int t = 0; t < TN; ++t) split3_set(bv[t], j, Bs[kr * LDB_S + wn + t * 32 + l32]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) acc[i][t] = mfma_x6(av[i], bv[t], acc[i][t]);
+    if (kk == 0) mid();
+  }
+}
+
+// The fwd-form A operand [ks*16 + k][lda] fp32 split into its three bf16 terms, laid out for
+// the x6 stage's operand reads: planes[((ks*3 + q)*2 + h)*lda + m][j] = term q of
+// A[ks*16 + 8h + j][m] - one 16-B ds_read_b128 per (plane, fragment), 16-B rows per m so a
+// 16-lane group of reads covers 64 distinct banks, and every 64 rows of one (ks, q, h) are one
+// contiguous 1 KB LDS-DMA piece.
+__global__ void __launch_bounds__(256) k_split_pack(const float* __restrict__ A, int ksteps, int lda,
+                                                    __bf16* __restrict__ planes) {
+  // one thread per (ks, half h, m): reads A[ks*16 + 8h + j][m], j < 8 (coalesced over m), writes
+  // the three 16-B plane rows of that (ks, h, m) (coalesced over m)
+  const long long n = (long long)ksteps * 2 * lda;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const int m = (int)(e % lda);
+    const long long kh = e / lda;
+    const int h = (int)(kh & 1), ks = (int)(kh >> 1);
+    Split3 sp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_set(sp, j, A[((long long)ks * kCB + 8 * h + j) * lda + m]);
+    bf16x8* out = reinterpret_cast<bf16x8*>(planes);
+    const long long row = ((long long)(ks * 3) * 2 + h) * lda + m;  // plane 0
+    out[row] = sp.hi;
+    out[row + 2LL * lda] = sp.mid;
+    out[row + 4LL * lda] = sp.lo;
+  }
+}
+
+// x6 stage with the A fragments read as pre-split bf16 planes (one LDS stage = G K-steps of
+// [plane][half][BM][8] bf16, 24*BM floats each) and the B fragments split as they are read.
+template <int G, int TM, int TN, int BM, int LDB_S, typename F>
+__device__ __forceinline__ void mfma_stage_x6p(const float* __restrict__ As, const float* __restrict__ Bs,
+                                               int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int kk = 0; kk < G; ++kk) {
+    const bf16x8* Ab = reinterpret_cast<const bf16x8*>(As + kk * 24 * BM);
+    Split3 av[TM], bv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = wm + i * 32 + l32;
+      av[i].hi = Ab[(0 * 2 + h) * BM + m];
+      av[i].mid = Ab[(1 * 2 + h) * BM + m];
+      av[i].lo = Ab[(2 * 2 + h) * BM + m];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kr = kk * 16 + 8 * h + j;
 #pragma unroll
       for (int t = 0; t < TN; ++t) split3_set(bv[t], j, Bs[kr * LDB_S + wn + t * 32 + l32]);
     }
@@ -589,9 +648,11 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   static_assert(BN % 64 == 0 && BM % 32 == 0, "tiles");
-  constexpr int A_STAGE = BK * BM, STAGE = A_STAGE + BK * BN;
+  constexpr bool APRE = MT == kMathX6P;  // A from the pre-split bf16 planes (1 KB DMA pieces)
+  static_assert(!APRE || BM % 64 == 0, "pre-split A: 64-row DMA pieces");
+  constexpr int A_STAGE = APRE ? G * 24 * BM : BK * BM, STAGE = A_STAGE + BK * BN;
   constexpr int A_ROWS_PER_INST = 256 / BM;
-  constexpr int A_INST = BK / A_ROWS_PER_INST;
+  constexpr int A_INST = APRE ? G * 6 * (BM / 64) : BK / A_ROWS_PER_INST;
   constexpr int A_INST_W = A_INST / 4;
   constexpr int NH = BN / 64;
 #ifdef MSL_SK_FAKEX4
@@ -621,6 +682,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       (void*)a.A, (short)0, (int)min(0x7fffffffLL, (long long)sk.KS * BK * a.lda * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * 6 * a.lda * 16), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
   const unsigned chan_bytes = (unsigned)a.P * 4u;
 
@@ -681,11 +744,23 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 #endif
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
-      const unsigned a_base = (unsigned)s * a_stage_bytes;
+      if constexpr (APRE) {
+        // piece inst = (g, plane*2 + half, 64-row block): planes row ((ks*3+q)*2+h)*lda + m
 #pragma unroll
-      for (int i = 0; i < A_INST_W; ++i) {
-        const int inst = wid * A_INST_W + i;
-        dma_b128(ra, As + inst * 256, a_off[i] + a_base);
+        for (int i = 0; i < A_INST_W; ++i) {
+          const int inst = wid * A_INST_W + i;
+          const int g = inst / (6 * (BM / 64)), r = inst % (6 * (BM / 64));
+          const int qh = r / (BM / 64), mb = (r % (BM / 64)) * 64;
+          const int ks = s * G + g;
+          dma_b128(rx, As + inst * 256, (unsigned)(((ks * 6 + qh) * a.lda + m0 + mb + lane) * 16));
+        }
+      } else {
+        const unsigned a_base = (unsigned)s * a_stage_bytes;
+#pragma unroll
+        for (int i = 0; i < A_INST_W; ++i) {
+          const int inst = wid * A_INST_W + i;
+          dma_b128(ra, As + inst * 256, a_off[i] + a_base);
+        }
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -755,6 +830,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
         mfma_stage_bf16<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (MT == kMathX6)
         mfma_stage_x6<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
+      else if constexpr (MT == kMathX6P)
+        mfma_stage_x6p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else
         mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
