@@ -21,7 +21,8 @@ struct FwdArgs {
   int M, lda, H, W, P, cimg, ncb, dil0, dil1, ksteps, kps;  // ksteps counts BK-deep steps
   int taps;           // 9 (3x3) or 1 (pointwise: dil0 = 0, so the single tap has no shift)
   long long slab;
-  const void* Ax6;    // kMathX6P: A split into bf16 planes [ks][plane][k half][lda][8] (k_split_pack)
+  const void* Ax6;    // kMathX6P/PP: A split into bf16 planes [ks][plane][k half][lda][8] (k_split_pack)
+  const void* Bx6;    // kMathX6PP: B split into bf16 planes [cb][plane][k half][P][8] (k_split_act)
 };
 
 struct WgradArgs {
@@ -143,7 +144,8 @@ struct Split3 {
 // matrix-core form of a conv kernel (template argument MT)
 // kMathX6P: the x6 form with the A operand (packed weights) split once per call by
 // k_split_pack instead of per read (fwd form only)
-constexpr int kMathF32 = 0, kMathBf16 = 1, kMathX6 = 2, kMathX6P = 3;
+// by k_split_pack instead of per read; kMathX6PP: both operands pre-split (k_split_act for B)
+constexpr int kMathF32 = 0, kMathBf16 = 1, kMathX6 = 2, kMathX6P = 3, kMathX6PP = 4;
 
 __device__ __forceinline__ void split3_set(Split3& s, int j, float v) {
   const __bf16 h = (__bf16)v;
@@ -226,6 +228,63 @@ __global__ void __launch_bounds__(256) k_split_pack(const float* __restrict__ A,
     out[row] = sp.hi;
     out[row + 2LL * lda] = sp.mid;
     out[row + 4LL * lda] = sp.lo;
+  }
+}
+
+// The fwd-form B operand (image [cimg][P] fp32) split into bf16 planes
+// planes[((cb*3 + q)*2 + h)*P + p][j] = term q of image[cb*16 + 8h + j][p] (0 past cimg): a tap's
+// B tile is then one 16-B DMA piece per (pixel, plane, half) - per-lane, so shifted pixels that
+// leave the image still get an out-of-range offset - and one ds_read_b128 per fragment and plane.
+__global__ void __launch_bounds__(256) k_split_act(const float* __restrict__ x, int cimg, int ncb, int P,
+                                                   __bf16* __restrict__ planes) {
+  const long long n = (long long)ncb * 2 * P;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const int p = (int)(e % P);
+    const long long kh = e / P;
+    const int h = (int)(kh & 1), cb = (int)(kh >> 1);
+    Split3 sp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cb * kCB + 8 * h + j;
+      split3_set(sp, j, c < cimg ? x[(long long)c * P + p] : 0.f);
+    }
+    bf16x8* out = reinterpret_cast<bf16x8*>(planes);
+    const long long row = ((long long)(cb * 3) * 2 + h) * P + p;  // plane 0
+    out[row] = sp.hi;
+    out[row + 2LL * P] = sp.mid;
+    out[row + 4LL * P] = sp.lo;
+  }
+}
+
+// x6 stage with both operands read as pre-split bf16 planes: no split work in the loop.
+template <int G, int TM, int TN, int BM, int BN, typename F>
+__device__ __forceinline__ void mfma_stage_x6pp(const float* __restrict__ As, const float* __restrict__ Bs,
+                                                int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int kk = 0; kk < G; ++kk) {
+    const bf16x8* Ab = reinterpret_cast<const bf16x8*>(As + kk * 24 * BM);
+    const bf16x8* Bb = reinterpret_cast<const bf16x8*>(Bs + kk * 24 * BN);
+    Split3 av[TM], bv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = wm + i * 32 + l32;
+      av[i].hi = Ab[h * BM + m];
+      av[i].mid = Ab[(2 + h) * BM + m];
+      av[i].lo = Ab[(4 + h) * BM + m];
+    }
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const int n = wn + t * 32 + l32;
+      bv[t].hi = Bb[h * BN + n];
+      bv[t].mid = Bb[(2 + h) * BN + n];
+      bv[t].lo = Bb[(4 + h) * BN + n];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) acc[i][t] = mfma_x6(av[i], bv[t], acc[i][t]);
+    if (kk == 0) mid();
   }
 }
 
@@ -648,9 +707,12 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   static_assert(BN % 64 == 0 && BM % 32 == 0, "tiles");
-  constexpr bool APRE = MT == kMathX6P;  // A from the pre-split bf16 planes (1 KB DMA pieces)
+  constexpr bool APRE = MT == kMathX6P || MT == kMathX6PP;  // A from pre-split bf16 planes
+  constexpr bool BPRE = MT == kMathX6PP;                      // B from pre-split bf16 planes
   static_assert(!APRE || BM % 64 == 0, "pre-split A: 64-row DMA pieces");
-  constexpr int A_STAGE = APRE ? G * 24 * BM : BK * BM, STAGE = A_STAGE + BK * BN;
+  static_assert(!BPRE || (!PW && BN % 64 == 0), "pre-split B: 64-pixel DMA pieces");
+  constexpr int A_STAGE = APRE ? G * 24 * BM : BK * BM;
+  constexpr int STAGE = A_STAGE + (BPRE ? G * 24 * BN : BK * BN);
   constexpr int A_ROWS_PER_INST = 256 / BM;
   constexpr int A_INST = APRE ? G * 6 * (BM / 64) : BK / A_ROWS_PER_INST;
   constexpr int A_INST_W = A_INST / 4;
@@ -658,7 +720,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 #ifdef MSL_SK_FAKEX4
   constexpr int BG_INST_W = kCB * BN / 256 / 4;
 #else
-  constexpr int BG_INST_W = PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B instructions per wave per K-step
+  constexpr int BG_INST_W = BPRE ? 6 * NH / 4 : PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B DMAs per wave per K-step
 #endif
   static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
   constexpr int INST_W = A_INST_W + G * BG_INST_W;
@@ -684,6 +746,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * 6 * a.lda * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.Bx6, (short)0, (int)min(0x7fffffffLL, (long long)a.ncb * 6 * a.P * 16), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
   const unsigned chan_bytes = (unsigned)a.P * 4u;
 
@@ -734,7 +798,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const bool v = pin[h] && (unsigned)(py[h] + dh) < (unsigned)a.H && (unsigned)(px[h] + dw) < (unsigned)a.W;
-        vrow[h] = v ? (unsigned)((n0 + h * 64 + lane + shift) * 4) : OOB;
+        vrow[h] = v ? (unsigned)((n0 + h * 64 + lane + shift) * (BPRE ? 16 : 4)) : OOB;
       }
     };
     set_tap(c_tap);
@@ -765,6 +829,16 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int cb16 = c_cb * kCB;
+        if constexpr (BPRE) {
+          // piece (plane*2 + k half, 64-pixel half): lane = pixel, 16 B = 8 channels of a plane
+#pragma unroll
+          for (int j = 0; j < BG_INST_W; ++j) {
+            const int inst = wid * BG_INST_W + j;
+            const int qh = inst / NH, h = inst % NH;  // wave-uniform
+            const unsigned rowb = (unsigned)((c_cb * 6 + qh) * a.P) * 16u;
+            dma_b128(rbx, Bs + g * 24 * BN + (qh * BN + h * 64) * 4, vrow[h] + rowb);
+          }
+        } else
 #ifdef MSL_SK_FAKEX4  // tuning-harness experiment only: dwordx4 B loads of unshifted rows (wrong results)
         if constexpr (true) {
 #else
@@ -832,6 +906,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
         mfma_stage_x6<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (MT == kMathX6P)
         mfma_stage_x6p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
+      else if constexpr (MT == kMathX6PP)
+        mfma_stage_x6pp<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else
         mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -97,9 +97,13 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   CK(hipMemset(flags, 0, 1 << 20));
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    if (MT == kMathX6P) {  // the split of the weights is part of every call
+    if (MT == kMathX6P || MT == kMathX6PP) {  // the splits are part of every call
       a.Ax6 = ws + (size_t)NW * 2 * BM * BN;
       hipLaunchKernelGGL(k_split_pack, dim3(2048), dim3(256), 0, 0, wp, a.ksteps, lda, (__bf16*)a.Ax6);
+    }
+    if (MT == kMathX6PP) {
+      a.Bx6 = ws + (size_t)NW * 2 * BM * BN + (size_t)a.ksteps * 6 * lda * 4;
+      hipLaunchKernelGGL(k_split_act, dim3(2048), dim3(256), 0, 0, x, a.cimg, a.ncb, P, (__bf16*)a.Bx6);
     }
     hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, WM, WN, false, MT>), dim3(NW), dim3(256), 0, 0, a, sk);
     hipLaunchKernelGGL((k_sk_reduce<BM, BN>), dim3(BM * BN / 1024, tiles), dim3(256), 0, 0, a, sk);
@@ -331,8 +335,8 @@ int main(int argc, char** argv) {
       FSKE(128, 128, 2, 2, 2, 2, 512, 0) FSKE(128, 128, 2, 2, 2, 2, 512, 1) FSKE(128, 128, 2, 2, 2, 2, 512, 2)
       FSKE(128, 128, 2, 2, 2, 2, 256, 2) FSKE(128, 128, 1, 3, 2, 2, 512, 2) FSKE(128, 128, 2, 3, 2, 2, 256, 2)
       FSKE(128, 128, 4, 2, 2, 2, 256, 2) FSKE(64, 128, 2, 2, 2, 2, 768, 2)
-      FSKE(128, 128, 1, 3, 2, 2, 512, 3) FSKE(128, 128, 1, 4, 2, 2, 512, 3) FSKE(128, 128, 2, 2, 2, 2, 512, 3)
-      FSKE(128, 128, 1, 3, 2, 2, 256, 3)
+      FSKE(128, 128, 1, 4, 2, 2, 512, 3) FSKE(128, 128, 1, 4, 2, 2, 512, 4) FSKE(128, 128, 1, 3, 2, 2, 512, 4)
+      FSKE(128, 128, 2, 2, 2, 2, 512, 4) FSKE(128, 128, 2, 3, 2, 2, 512, 4) FSKE(128, 128, 1, 4, 2, 2, 256, 4)
       WSKE(64, 64, 2, 512, 0) WSKE(64, 64, 2, 512, 1) WSKE(64, 64, 2, 512, 2)
       WSKE(128, 128, 2, 256, 0) WSKE(128, 128, 2, 256, 2) WSKE(64, 128, 2, 512, 2)
       continue;
