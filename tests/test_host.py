@@ -61,6 +61,11 @@ def test_pure_host_entry_points():
     off = np.zeros(8, np.int64)
     n = lib.msl_sgd_plan(numels.ctypes.data, 4, ent.ctypes.data, off.ctypes.data, 8)
     assert n == 4 and list(ent[:4]) == [0, 1, 2, 2] and list(off[:4]) == [0, 0, 0, be]
+    # matrix-core form of the fp32 convs: bf16x6 (2) by default, f32 MFMA (0) selectable, others refused
+    assert lib.msl_conv_f32_form() == 2
+    assert lib.msl_conv_set_f32_form(1) == -3 and lib.msl_conv_set_f32_form(7) == -3
+    assert lib.msl_conv_set_f32_form(0) == 0 and lib.msl_conv_f32_form() == 0
+    assert lib.msl_conv_set_f32_form(2) == 0 and lib.msl_conv_f32_form() == 2
 
 
 def test_compute_calls_fail_loudly_without_gpu():
