@@ -993,15 +993,17 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
       return part[(long long)(wc * 2 + slot) * (PSZ / 4) + g];
     };
     auto add = [](float4& acc, const float4& v) { acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w; };
-    // two loads in flight per step (the sum stays in worker order)
+    // four loads in flight per step (the sum stays in worker order)
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int wc = w_lo;
-    for (; wc + 1 <= w_hi; wc += 2) {
-      const float4 p0 = piece(wc), p1 = piece(wc + 1);
+    for (; wc + 3 <= w_hi; wc += 4) {
+      const float4 p0 = piece(wc), p1 = piece(wc + 1), p2 = piece(wc + 2), p3 = piece(wc + 3);
       add(acc, p0);
       add(acc, p1);
+      add(acc, p2);
+      add(acc, p3);
     }
-    if (wc <= w_hi) add(acc, piece(wc));
+    for (; wc <= w_hi; ++wc) add(acc, piece(wc));
     const int m = m0 + (g * 4) / BN, n = n0 + (g * 4) % BN;
     if (m >= a.M) continue;
     float bsum = 0.f;
