@@ -884,7 +884,18 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       if (k < nst) issue(k_a + k, k);
     for (int i = 0; i < nst; ++i) {
       const int younger = min(STAGES - 2, nst - 1 - i);
-      if constexpr (STAGES >= 4) {
+      if constexpr (STAGES >= 6) {
+        if (younger >= 4) wait_vmcnt<4 * INST_W>();
+        else if (younger == 3) wait_vmcnt<3 * INST_W>();
+        else if (younger == 2) wait_vmcnt<2 * INST_W>();
+        else if (younger == 1) wait_vmcnt<INST_W>();
+        else wait_vmcnt<0>();
+      } else if constexpr (STAGES == 5) {
+        if (younger >= 3) wait_vmcnt<3 * INST_W>();
+        else if (younger == 2) wait_vmcnt<2 * INST_W>();
+        else if (younger == 1) wait_vmcnt<INST_W>();
+        else wait_vmcnt<0>();
+      } else if constexpr (STAGES >= 4) {
         if (younger >= 2) wait_vmcnt<2 * INST_W>();
         else if (younger == 1) wait_vmcnt<INST_W>();
         else wait_vmcnt<0>();

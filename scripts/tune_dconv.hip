@@ -335,8 +335,9 @@ int main(int argc, char** argv) {
       FSKE(128, 128, 2, 2, 2, 2, 512, 0) FSKE(128, 128, 2, 2, 2, 2, 512, 1) FSKE(128, 128, 2, 2, 2, 2, 512, 2)
       FSKE(128, 128, 2, 2, 2, 2, 256, 2) FSKE(128, 128, 1, 3, 2, 2, 512, 2) FSKE(128, 128, 2, 3, 2, 2, 256, 2)
       FSKE(128, 128, 4, 2, 2, 2, 256, 2) FSKE(64, 128, 2, 2, 2, 2, 768, 2)
-      FSKE(128, 128, 1, 4, 2, 2, 512, 3) FSKE(128, 128, 1, 4, 2, 2, 512, 4) FSKE(128, 128, 1, 3, 2, 2, 512, 4)
-      FSKE(128, 128, 2, 2, 2, 2, 512, 4) FSKE(128, 128, 2, 3, 2, 2, 512, 4) FSKE(128, 128, 1, 4, 2, 2, 256, 4)
+      FSKE(128, 128, 1, 4, 2, 2, 512, 3) FSKE(128, 128, 1, 5, 2, 2, 256, 3) FSKE(128, 128, 1, 6, 2, 2, 256, 3)
+      FSKE(128, 128, 1, 7, 2, 2, 256, 3) FSKE(128, 128, 2, 4, 2, 2, 256, 3) FSKE(128, 128, 1, 3, 2, 2, 512, 4)
+      FSKE(128, 128, 1, 5, 2, 2, 256, 4)
       WSKE(64, 64, 2, 512, 0) WSKE(64, 64, 2, 512, 1) WSKE(64, 64, 2, 512, 2)
       WSKE(128, 128, 2, 256, 0) WSKE(128, 128, 2, 256, 2) WSKE(64, 128, 2, 512, 2)
       continue;
