@@ -8,7 +8,8 @@
 // statistics are accumulated in fp64 around a per-channel shift (its first element), which
 // is at least as accurate as the CPU's two-pass fp32 sums.
 //
-// Layout [C][P] (N = 1).  Forward: stats kernel (grid C x S partial fp64 sums per channel) +
+// Layout [C][P] (N = 1).  Train mode on maps of <= 16384 px: one fused launch per call (see
+// k_bn_fwd_fused).  Otherwise: forward: stats kernel (grid C x S partial fp64 sums per channel) +
 // a flat apply kernel over the whole tensor in float4s (each block folds the partials of the
 // channels it touches).  Backward: per-channel reduce (sum g, sum g*xhat with g = dy masked by
 // y > 0 when ReLU) + flat apply (dx, d residual, dgamma, dbeta).  HBM-bound: fwd reads x twice,
@@ -284,6 +285,148 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
       });
 }
 
+// ---------------------------------------------------------------- fused one-block-per-channel form
+// Train mode with P <= kBnFusedMaxP (layers 2-4 at every BASELINE crop): one 1024-thread block
+// per channel keeps the channel's operands in registers (EPT elements per lane, lane-strided so
+// every wave load is 256 contiguous bytes), reduces the fp64 sums in the block and applies in the
+// same launch.  Forward: x (+ residual) read once, y written once — 2 (3) tensor passes instead
+// of 3 (4) and one launch instead of two.  Backward: dy, x, y read once, dx (+ dres) written —
+// 4 (5) passes instead of 7 (8).  Same per-element formulas as the flat kernels above.
+constexpr int kBnFusedThreads = 1024;
+constexpr int kBnFusedMaxP = 16 * kBnFusedThreads;
+static int g_bn_fused = 1;  // msl_bn_set_fused
+static bool bn_fused_enabled() { return g_bn_fused != 0; }
+
+__device__ __forceinline__ void block_sum2_d16(double& a, double& b, double* red) {
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * w] = a;
+    red[2 * w + 1] = b;
+  }
+  __syncthreads();
+  a = 0.0;
+  b = 0.0;
+#pragma unroll
+  for (int i = 0; i < kBnFusedThreads / 64; ++i) {  // fixed order: deterministic
+    a += red[2 * i];
+    b += red[2 * i + 1];
+  }
+}
+
+template <int EPT>
+__global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
+  __shared__ double red[2 * kBnFusedThreads / 64];
+  const int c = blockIdx.x, t = threadIdx.x, P = a.P;
+  const long long base = (long long)c * P;
+  const float* xc = a.x + base;
+  float xv[EPT], rv[EPT];
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    xv[j] = e < P ? xc[e] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    rv[j] = (a.residual && e < P) ? a.residual[base + e] : 0.f;
+  }
+  const double shift = (double)xc[0];
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    if (j * kBnFusedThreads + t < P) {
+      const double d = (double)xv[j] - shift;
+      s1 += d;
+      s2 += d * d;
+    }
+  }
+  block_sum2_d16(s1, s2, red);
+  const double n = (double)P;
+  const double dm = s1 / n;
+  double var = s2 / n - dm * dm;
+  if (var < 0.0) var = 0.0;
+  const float mean = (float)(shift + dm);
+  const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+  if (t == 0) {
+    if (a.update_running) {
+      const float m = a.momentum;
+      const float unbiased = (float)(P > 1 ? var * n / (n - 1.0) : var);
+      a.running_mean[c] = (1.f - m) * a.running_mean[c] + m * mean;
+      a.running_var[c] = (1.f - m) * a.running_var[c] + m * unbiased;
+      if (c == 0 && a.num_batches) a.num_batches[0] += 1;
+    }
+    a.save_mean[c] = mean;
+    a.save_invstd[c] = invstd;
+  }
+  const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
+  const float bsh = (a.beta ? a.beta[c] : 0.f) - mean * alpha;
+  float* yc = a.y + base;
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    if (e < P) {
+      float v = xv[j] * alpha + bsh;
+      v += rv[j];
+      yc[e] = a.relu ? fmaxf(v, 0.f) : v;
+    }
+  }
+}
+
+template <int EPT>
+__global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
+  __shared__ double red[2 * kBnFusedThreads / 64];
+  const int c = blockIdx.x, t = threadIdx.x, P = a.P;
+  const long long base = (long long)c * P;
+  const float mean = a.save_mean[c], invstd = a.save_invstd[c];
+  float g[EPT], xv[EPT];
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    g[j] = e < P ? a.dy[base + e] : 0.f;
+    xv[j] = e < P ? a.x[base + e] : 0.f;
+  }
+  if (a.relu) {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = j * kBnFusedThreads + t;
+      if (e < P && !(a.y[base + e] > 0.f)) g[j] = 0.f;
+    }
+  }
+  double sg = 0.0, sgx = 0.0;
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const float xh = (xv[j] - mean) * invstd;
+    sg += (double)g[j];  // g = 0 past P
+    sgx += (double)g[j] * (double)xh;
+  }
+  block_sum2_d16(sg, sgx, red);
+  if (t == 0) {
+    if (a.dgamma) a.dgamma[c] = a.accumulate ? a.dgamma[c] + (float)sgx : (float)sgx;
+    if (a.dbeta) a.dbeta[c] = a.accumulate ? a.dbeta[c] + (float)sg : (float)sg;
+  }
+  const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
+  const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    if (e < P) {
+      const float xh = (xv[j] - mean) * invstd;
+      if (a.dres) a.dres[base + e] = g[j];
+      if (a.dx) a.dx[base + e] = (g[j] - m1 - xh * m2) * w;
+    }
+  }
+}
+
+template <typename K, typename A>
+static int bn_launch_fused(K k4, K k9, K k16, int c, int p, hipStream_t st, const A& a) {
+  K k = p <= 4 * kBnFusedThreads ? k4 : p <= 9 * kBnFusedThreads ? k9 : k16;
+  hipLaunchKernelGGL(k, dim3(c), dim3(kBnFusedThreads), 0, st, a);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace msl
@@ -291,6 +434,14 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 using namespace msl;
 
 extern "C" {
+
+int msl_bn_set_fused(int fused) {
+  if (fused != 0 && fused != 1) return MSL_ERR_ARG;
+  g_bn_fused = fused;
+  return MSL_OK;
+}
+
+int msl_bn_fused(void) { return g_bn_fused; }
 
 size_t msl_bn_workspace(int c, int p) {
   return align_up((size_t)c * bn_splits(p) * 2 * sizeof(double), 256);
@@ -336,6 +487,8 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   a.update_running = update_running;
   a.eps = eps;
   a.momentum = momentum;
+  if (training && p <= kBnFusedMaxP && bn_fused_enabled())
+    return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, c, p, st, a);
   const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
   if (vec)
     hipLaunchKernelGGL(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
@@ -372,6 +525,8 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
   a.relu = relu;
   a.training = training;
   a.accumulate = accumulate_params;
+  if (training && p <= kBnFusedMaxP && bn_fused_enabled())
+    return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
   const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
   if (vec) {

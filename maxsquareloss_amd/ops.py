@@ -43,6 +43,15 @@ def set_f32_form(form):
     return {v: k for k, v in F32_FORMS.items()}[prev]
 
 
+def set_bn_fused(fused):
+    """Select the BN kernel form (msl_bn_set_fused): True = one fused launch per train-mode BN
+    call on maps of <= 16384 px; returns the previous setting."""
+    lib = hip.load(require_gpu=False)
+    prev = bool(lib.msl_bn_fused())
+    hip.check(lib.msl_bn_set_fused(int(bool(fused))), "msl_bn_set_fused")
+    return prev
+
+
 def f32_form():
     lib = hip.load(require_gpu=False)
     return {v: k for k, v in F32_FORMS.items()}[lib.msl_conv_f32_form()]

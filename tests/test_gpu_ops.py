@@ -272,9 +272,19 @@ def test_sgd_multiplicity_matches_torch_cpu():
         assert _rel(a, b) < 1e-6
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("c,h,w,res,relu,train", [(64, 129, 257, False, True, True), (256, 65, 129, True, True, True),
-                                                  (1024, 33, 65, False, False, True), (64, 17, 33, True, True, False)])
-def test_bn_act(c, h, w, res, relu, train):
+                                                  (1024, 33, 65, False, False, True), (64, 17, 33, True, True, False),
+                                                  (512, 81, 161, False, True, True), (128, 128, 128, True, False, True)])
+def test_bn_act(c, h, w, res, relu, train, fused):
+    prev = ops.set_bn_fused(fused)
+    try:
+        _check_bn_act(c, h, w, res, relu, train)
+    finally:
+        ops.set_bn_fused(prev)
+
+
+def _check_bn_act(c, h, w, res, relu, train):
     g = torch.Generator().manual_seed(c + h)
     x = torch.randn(1, c, h, w, generator=g) * 3 + 40.0  # large mean: the cancellation case
     r = torch.randn(1, c, h, w, generator=g) if res else None

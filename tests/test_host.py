@@ -66,6 +66,9 @@ def test_pure_host_entry_points():
     assert lib.msl_conv_set_f32_form(1) == -3 and lib.msl_conv_set_f32_form(7) == -3
     assert lib.msl_conv_set_f32_form(0) == 0 and lib.msl_conv_f32_form() == 0
     assert lib.msl_conv_set_f32_form(2) == 0 and lib.msl_conv_f32_form() == 2
+    assert lib.msl_bn_fused() == 1 and lib.msl_bn_set_fused(2) == -3
+    assert lib.msl_bn_set_fused(0) == 0 and lib.msl_bn_fused() == 0
+    assert lib.msl_bn_set_fused(1) == 0 and lib.msl_bn_fused() == 1
 
 
 def test_compute_calls_fail_loudly_without_gpu():
