@@ -459,7 +459,8 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   if (training && ws_bytes < msl_bn_workspace(c, p)) return MSL_ERR_WORKSPACE;
   double* part = (double*)ws;
   const bool vec = al16(x) && al16(y) && (!residual || al16(residual));
-  if (training) {
+  const bool fused = training && p <= kBnFusedMaxP && bn_fused_enabled();
+  if (training && !fused) {
     if (vec)
       hipLaunchKernelGGL(k_bn_stats<true>, dim3(c, S), dim3(256), 0, st, x, p, S, part);
     else
@@ -487,8 +488,7 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   a.update_running = update_running;
   a.eps = eps;
   a.momentum = momentum;
-  if (training && p <= kBnFusedMaxP && bn_fused_enabled())
-    return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, c, p, st, a);
+  if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, c, p, st, a);
   const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
   if (vec)
     hipLaunchKernelGGL(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
