@@ -143,7 +143,7 @@ def main():
         traffic = None  # the committed PMC figure belongs to another form of the kernel
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": "dconv3x3 fwd layer3 d=2 (one op call: k_split_pack [bf16x6 form] + stream-K k_igemm_fwd_sk + k_sk_reduce)",
+                "kernel": "dconv3x3 fwd layer3 d=2 (one op call: stream-K k_igemm_fwd_sk + k_sk_reduce; the bf16x6 weight planes are split at pack time, once per SGD step)",
                 "form": form, "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
 

@@ -63,8 +63,10 @@ int msl_conv_f32_form(void);
  * Weights of branch b start at w + b*branch_stride, shape [cout][cin][3][3].
  * ---------------------------------------------------------------------- */
 
-/* Elements of the packed operand produced by msl_dconv_pack (for_dgrad = 0:
- * forward layout, 1: transposed + tap-flipped layout for the data gradient). */
+/* Elements (fp32 units) of the packed operand produced by msl_dconv_pack (for_dgrad = 0:
+ * forward layout, 1: transposed + tap-flipped layout for the data gradient): the fp32 K-major
+ * pack followed by its bf16x6 planes (split once here, read by the bf16x6 fp32 form).  All
+ * nbranch branches are packed by one call (branch b's weights at w + b*branch_stride floats). */
 long long msl_dconv_packed_elems(int nbranch, int cin, int cout, int for_dgrad);
 int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin, int cout,
                    int for_dgrad, float* packed, msl_stream_t stream);

@@ -182,13 +182,8 @@ static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, boo
 // stream-K workspace: the published pieces, NW x 2 x BM*BN floats.  The arrival counters live in
 // a caller-owned, persistent int[kMaxCounters] that is zero on entry and left zero on exit (the
 // finishing workgroup of each tile re-arms its counter), so no per-call memset is needed.
-// bytes of the pre-split A planes the x6 form stages its weights from (k_split_pack)
-static size_t x6_planes_bytes(const FwdPlan& pl, int M) {
-  return pl.sk && pl.bm == 128 ? (size_t)pl.ksteps * 6 * pad_to(M, kPackPad) * 16 : 0;
-}
-
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
-  if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float) + x6_planes_bytes(pl, M);
+  if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float);
   return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
 }
 
@@ -250,13 +245,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     const dim3 grid(sk.NW), block(256);
     const dim3 rgrid(pl.bm * kSkBN / 1024, pl.tiles_m * pl.tiles_n);
     if (MT == kMathX6 && pl.bm == 128) {
-      // weights split into bf16 planes once per call, then the x6 kernel stages them directly
-      __bf16* planes = (__bf16*)((char*)ws + (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float));
-      const long long n = (long long)pl.ksteps * kCB * a.lda;
-      hipLaunchKernelGGL(k_split_pack, dim3((int)std::min<long long>(cdiv(n, 256), 4096)), block, 0, st,
-                         packed, pl.ksteps, a.lda, planes);
-      MSL_CHECK_LAUNCH();
-      a.Ax6 = planes;
+      // the x6 kernel stages its weights from the bf16 planes that pack() split once, behind
+      // the fp32 part of the same buffer (M > 64 <=> 128-row tiles)
+      a.Ax6 = reinterpret_cast<const __bf16*>(packed + (long long)pl.ksteps * kCB * a.lda);
       hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 4, 2, 2, false, kMathX6P>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
@@ -303,21 +294,36 @@ static bool bad_dims(int nbranch, int cin, int cout, int h, int w) {
 }
 
 // ---------------------------------------------------------------- shared by 3x3 and pointwise
-static long long packed_elems(int nbranch, int taps, int cin, int cout, int for_dgrad) {
+// A packed operand is the fp32 K-major pack [ksteps*16][lda] followed by its bf16x6 planes
+// [ks][plane][k half][lda][8] (k_split_pack; 1.5x the fp32 bytes).  The planes are written by
+// pack() when M > 64 - the 128-row tiles of the x6 form, the only reader - so the split runs
+// once per weight update instead of once per conv call.
+static long long packed_f32_elems(int nbranch, int taps, int cin, int cout, int for_dgrad) {
   const int cimg = for_dgrad ? cout : cin;
   const int m = for_dgrad ? cin : cout;
   return (long long)nbranch * cdiv(cimg, kCB) * taps * kCB * pad_to(m, kPackPad);
+}
+
+static long long packed_elems(int nbranch, int taps, int cin, int cout, int for_dgrad) {
+  return packed_f32_elems(nbranch, taps, cin, cout, for_dgrad) * 5 / 2;
 }
 
 static int pack(const float* w, long long branch_stride, int nbranch, int taps, int cin, int cout,
                 int for_dgrad, float* packed, hipStream_t st) {
   const int cimg = for_dgrad ? cout : cin;
   const int m = for_dgrad ? cin : cout;
-  const long long total = packed_elems(nbranch, taps, cin, cout, for_dgrad);
+  const long long total = packed_f32_elems(nbranch, taps, cin, cout, for_dgrad);
   const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
+  const int lda = pad_to(m, kPackPad);
   hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
-                     cdiv(cimg, kCB), pad_to(m, kPackPad), taps, total, packed);
+                     cdiv(cimg, kCB), lda, taps, total, packed);
   MSL_CHECK_LAUNCH();
+  if (m > 64) {
+    const int ksteps = nbranch * cdiv(cimg, kCB) * taps;
+    hipLaunchKernelGGL(k_split_pack, dim3((int)std::min<long long>(cdiv(total, 256), 4096)), dim3(256), 0,
+                       st, packed, ksteps, lda, reinterpret_cast<__bf16*>(packed + total));
+    MSL_CHECK_LAUNCH();
+  }
   return MSL_OK;
 }
 

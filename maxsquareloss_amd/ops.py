@@ -112,20 +112,21 @@ class PackCache:
                 total = lib.msl_pconv_packed_elems(cin, cout, for_dgrad)
             else:
                 total = lib.msl_dconv_packed_elems(nb, cin, cout, for_dgrad)
-            per_branch = total // nb
             buf = self.buf[for_dgrad]
             if buf is None or buf.numel() != total or buf.device != weights[0].device:
                 buf = torch.empty(total, dtype=_f32, device=weights[0].device)
             s = hip.stream_ptr()
-            for b, w in enumerate(weights):
-                wc = w.detach().contiguous()
-                dst = buf.data_ptr() + 4 * b * per_branch
-                if self.pointwise:
-                    hip.check(lib.msl_pconv_pack(wc.data_ptr(), cin, cout, for_dgrad, dst, s),
-                              "msl_pconv_pack")
-                else:
-                    hip.check(lib.msl_dconv_pack(wc.data_ptr(), 0, 1, cin, cout, for_dgrad, dst, s),
-                              "msl_dconv_pack")
+            wc = [w.detach().contiguous() for w in weights]
+            if self.pointwise:
+                hip.check(lib.msl_pconv_pack(wc[0].data_ptr(), cin, cout, for_dgrad, buf.data_ptr(), s),
+                          "msl_pconv_pack")
+            else:
+                # one call packs every branch (and splits the bf16x6 planes behind them)
+                stride = (wc[1].data_ptr() - wc[0].data_ptr()) // 4 if nb == 2 else 0
+                if nb == 2 and (wc[1].data_ptr() - wc[0].data_ptr()) % 4:
+                    raise hip.MSLError("dconv pack: misaligned branch weights")
+                hip.check(lib.msl_dconv_pack(wc[0].data_ptr(), stride, nb, cin, cout, for_dgrad, buf.data_ptr(), s),
+                          "msl_dconv_pack")
             self.buf[for_dgrad] = buf
             self.key[for_dgrad] = key
         return self.buf[for_dgrad]
