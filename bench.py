@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--num-classes", type=int, default=19)
     ap.add_argument("--conv-math", default="fp32", choices=["fp32", "bf16"],
                     help="bf16 = BASELINE config 5's fp16/bf16 MFMA path (fp32 accumulation)")
+    ap.add_argument("--bn-form", default="fused", choices=["fused", "split"],
+                    help="BN kernels: one fused launch per call (default) or split statistics/apply launches")
     ap.add_argument("--f32-form", default=None, choices=["mfma_f32", "bf16x6"],
                     help="matrix-core form of the fp32 convs (default: the library's)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=2, help="0 disables the CPU baseline")
@@ -80,6 +82,7 @@ def main():
     if a.f32_form:
         argv += ["--f32_form", a.f32_form]
     args, _, _ = init_args(build_parser().parse_args(argv))
+    ops.set_bn_fused(a.bn_form == "fused")
     tr = UDATrainer(args, cuda=True)
     rank, dev = tr.rank, tr.device
     init_state = {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()} if rank == 0 else None
@@ -180,7 +183,7 @@ def main():
         "data": "synthetic (counter-generated uint8 images -> BGR-mean, uniform labels; random-init weights)",
         "config": {"workload": f"{'SYNTHIA' if C == 16 else 'GTA5'}->Cityscapes {args.target_mode} UDA step "
                                f"(solve_gta5.py), {W}x{H}, bs=1/GPU",
-                   "conv_math": a.conv_math, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
+                   "conv_math": a.conv_math, "bn_form": a.bn_form, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
                    "target_mode": args.target_mode, "multi": args.multi, "lambda_target": args.lambda_target,
                    "num_classes": C, "global_batch": 2 * world, "parallelism": f"dp{world}"},
         "roofline": roofline, "cpu_baseline": cpu,

@@ -236,8 +236,8 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
                float* dgamma, float* dbeta, int c, int p, int training, int relu,
                int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream);
-/* BN kernel form (process-wide): 1 = train-mode layers with p <= 16384 run one fused
- * statistics+apply launch per call (one block per channel, operands held in registers), 0 =
+/* BN kernel form (process-wide): 1 = train-mode layers with p <= 16384 (or p <= 33792 and
+ * c >= 128) run one fused statistics+apply launch per call (one block per channel, operands held in registers), 0 =
  * the split statistics / flat-apply launches everywhere.  Returns 0, or MSL_ERR_ARG. */
 int msl_bn_set_fused(int fused);
 int msl_bn_fused(void);

@@ -8,7 +8,7 @@
 // statistics are accumulated in fp64 around a per-channel shift (its first element), which
 // is at least as accurate as the CPU's two-pass fp32 sums.
 //
-// Layout [C][P] (N = 1).  Train mode on maps of <= 16384 px: one fused launch per call (see
+// Layout [C][P] (N = 1).  Train mode on layer1-4 maps: one fused launch per call (see
 // k_bn_fwd_fused).  Otherwise: forward: stats kernel (grid C x S partial fp64 sums per channel) +
 // a flat apply kernel over the whole tensor in float4s (each block folds the partials of the
 // channels it touches).  Backward: per-channel reduce (sum g, sum g*xhat with g = dy masked by
@@ -286,16 +286,22 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
 }
 
 // ---------------------------------------------------------------- fused one-block-per-channel form
-// Train mode with P <= kBnFusedMaxP (layers 2-4 at every BASELINE crop): one 1024-thread block
+// Train mode on maps of <= 16384 px (layers 2-4 at every BASELINE crop), or <= 33792 px with
+// >= 128 channels (layer1's 256-channel maps at 1024x512): one 1024-thread block
 // per channel keeps the channel's operands in registers (EPT elements per lane, lane-strided so
 // every wave load is 256 contiguous bytes), reduces the fp64 sums in the block and applies in the
 // same launch.  Forward: x (+ residual) read once, y written once — 2 (3) tensor passes instead
 // of 3 (4) and one launch instead of two.  Backward: dy, x, y read once, dx (+ dres) written —
 // 4 (5) passes instead of 7 (8).  Same per-element formulas as the flat kernels above.
 constexpr int kBnFusedThreads = 1024;
-constexpr int kBnFusedMaxP = 16 * kBnFusedThreads;
+constexpr int kBnFusedMaxP = 33 * kBnFusedThreads;  // layer1 at 1024x512: 257x129 = 33153 px
 static int g_bn_fused = 1;  // msl_bn_set_fused
 static bool bn_fused_enabled() { return g_bn_fused != 0; }
+// beyond 16 elements per lane only with >= 128 channels: at 64 blocks (layer1's 64-channel
+// maps) the split kernels' wider grids win the backward (profiles/r01_bn_forms.txt)
+static bool bn_fused_shape(int c, int p) {
+  return p <= 16 * kBnFusedThreads || (c >= 128 && p <= kBnFusedMaxP);
+}
 
 __device__ __forceinline__ void block_sum2_d16(double& a, double& b, double* red) {
   a = wave_sum_d(a);
@@ -420,8 +426,8 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
 }
 
 template <typename K, typename A>
-static int bn_launch_fused(K k4, K k9, K k16, int c, int p, hipStream_t st, const A& a) {
-  K k = p <= 4 * kBnFusedThreads ? k4 : p <= 9 * kBnFusedThreads ? k9 : k16;
+static int bn_launch_fused(K k4, K k9, K k16, K k33, int c, int p, hipStream_t st, const A& a) {
+  K k = p <= 4 * kBnFusedThreads ? k4 : p <= 9 * kBnFusedThreads ? k9 : p <= 16 * kBnFusedThreads ? k16 : k33;
   hipLaunchKernelGGL(k, dim3(c), dim3(kBnFusedThreads), 0, st, a);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -459,7 +465,7 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   if (training && ws_bytes < msl_bn_workspace(c, p)) return MSL_ERR_WORKSPACE;
   double* part = (double*)ws;
   const bool vec = al16(x) && al16(y) && (!residual || al16(residual));
-  const bool fused = training && p <= kBnFusedMaxP && bn_fused_enabled();
+  const bool fused = training && bn_fused_enabled() && bn_fused_shape(c, p);
   if (training && !fused) {
     if (vec)
       hipLaunchKernelGGL(k_bn_stats<true>, dim3(c, S), dim3(256), 0, st, x, p, S, part);
@@ -488,7 +494,7 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   a.update_running = update_running;
   a.eps = eps;
   a.momentum = momentum;
-  if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, c, p, st, a);
+  if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>, c, p, st, a);
   const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
   if (vec)
     hipLaunchKernelGGL(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
@@ -525,8 +531,8 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
   a.relu = relu;
   a.training = training;
   a.accumulate = accumulate_params;
-  if (training && p <= kBnFusedMaxP && bn_fused_enabled())
-    return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, c, p, st, a);
+  if (training && bn_fused_enabled() && bn_fused_shape(c, p))
+    return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
   const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
   if (vec) {

@@ -45,7 +45,7 @@ def set_f32_form(form):
 
 def set_bn_fused(fused):
     """Select the BN kernel form (msl_bn_set_fused): True = one fused launch per train-mode BN
-    call on maps of <= 16384 px; returns the previous setting."""
+    call on maps of <= 16384 px (<= 33792 px with >= 128 channels); returns the previous setting."""
     lib = hip.load(require_gpu=False)
     prev = bool(lib.msl_bn_fused())
     hip.check(lib.msl_bn_set_fused(int(bool(fused))), "msl_bn_set_fused")

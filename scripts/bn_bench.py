@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from maxsquareloss_amd import ops
 
-SHAPES = [(64, 129, 257, False, True), (256, 65, 129, False, True), (1024, 65, 129, True, True),
+SHAPES = [(64, 129, 257, False, True), (256, 129, 257, True, True), (256, 65, 129, False, True), (1024, 65, 129, True, True),
           (512, 65, 129, False, True), (2048, 65, 129, True, True), (128, 65, 129, False, True)]
 
 

@@ -275,7 +275,8 @@ def test_sgd_multiplicity_matches_torch_cpu():
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("c,h,w,res,relu,train", [(64, 129, 257, False, True, True), (256, 65, 129, True, True, True),
                                                   (1024, 33, 65, False, False, True), (64, 17, 33, True, True, False),
-                                                  (512, 81, 161, False, True, True), (128, 128, 128, True, False, True)])
+                                                  (512, 81, 161, False, True, True), (128, 128, 128, True, False, True),
+                                                  (256, 129, 257, True, True, True)])
 def test_bn_act(c, h, w, res, relu, train, fused):
     prev = ops.set_bn_fused(fused)
     try:
