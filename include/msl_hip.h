@@ -53,6 +53,9 @@ int msl_counter_elems(void);
  * any other value.  Replaces nothing in the reference (its convs are cuDNN fp32). */
 int msl_conv_set_f32_form(int form);
 int msl_conv_f32_form(void);
+/* Weight-pack kernel (process-wide; identical packed bytes either way): 1 = one LDS-transposing
+ * pack+split launch per msl_*_pack call (default), 0 = element-wise gather + separate split. */
+int msl_conv_set_pack_form(int form);
 
 /* ------------------------------------------------------------------------
  * Dilated 3x3 convolution, stride 1, padding = dilation, as an FP32-MFMA

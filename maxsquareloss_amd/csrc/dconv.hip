@@ -93,6 +93,65 @@ __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long 
   }
 }
 
+// The same pack through LDS, with the bf16x6 planes split in the same launch: one block per
+// (16-row m chunk, channel block cb, branch) - 256 blocks for a 256x256 conv.  Both weight
+// layouts read as contiguous runs (fwd: W[m][cb*16..+16][taps] = 16*taps floats per m; dgrad:
+// W[c][m0..m0+16][taps] = 16*taps floats per c), the tile is transposed in LDS, and the writes
+// are 64-B fp32 row segments and 256-B plane runs.  k_pack's per-element gather (a 36-B or
+// cin*36-B lane stride) took 6 us for a 256x256x9 weight; the split was a second 4.6-us launch.
+// (64-row chunks: 64 blocks for that weight, 24 us - too few workgroups.)
+constexpr int kPackTileM = 16;
+
+template <int TAPS>
+__global__ void __launch_bounds__(256) k_pack_split(const float* __restrict__ w, long long branch_stride,
+                                                    int cin, int cout, int for_dgrad, int ncb, int lda,
+                                                    int split, float* __restrict__ out,
+                                                    __bf16* __restrict__ planes) {
+  __shared__ float s[kCB * TAPS][kPackTileM + 1];  // [cl*TAPS + t][ml], t = packed tap index
+  const int m0 = blockIdx.x * kPackTileM, cb = blockIdx.y, b = blockIdx.z;
+  const int cimg = for_dgrad ? cout : cin;
+  const int mreal = for_dgrad ? cin : cout;
+  const float* wb = w + (long long)b * branch_stride;
+  constexpr int N = kCB * TAPS * kPackTileM;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    int ml, cl, tm;  // tm = memory tap
+    if (!for_dgrad) {  // i = (ml*16 + cl)*TAPS + tm: W[m][c][tm] contiguous over (cl, tm)
+      tm = i % TAPS;
+      cl = (i / TAPS) % kCB;
+      ml = i / (TAPS * kCB);
+    } else {  // i = (cl*16 + ml)*TAPS + tm: W[c][m][tm] contiguous over (ml, tm)
+      tm = i % TAPS;
+      ml = (i / TAPS) % kPackTileM;
+      cl = i / (TAPS * kPackTileM);
+    }
+    const int m = m0 + ml, c = cb * kCB + cl;
+    float v = 0.f;
+    if (m < mreal && c < cimg)
+      v = for_dgrad ? wb[((long long)c * cin + m) * TAPS + tm] : wb[((long long)m * cin + c) * TAPS + tm];
+    const int t = for_dgrad ? TAPS - 1 - tm : tm;
+    s[cl * TAPS + t][ml] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += 256) {  // i = (t*16 + cl)*16 + ml
+    const int ml = i % kPackTileM, cl = (i / kPackTileM) % kCB, t = i / (kPackTileM * kCB);
+    const long long k = ((long long)(b * TAPS + t) * ncb + cb) * kCB + cl;
+    out[k * lda + m0 + ml] = s[cl * TAPS + t][ml];
+  }
+  if (!split) return;
+  bf16x8* pl = reinterpret_cast<bf16x8*>(planes);
+  for (int i = threadIdx.x; i < TAPS * 2 * kPackTileM; i += 256) {  // i = (t*2 + h)*16 + ml
+    const int ml = i % kPackTileM, h = (i / kPackTileM) & 1, t = i / (2 * kPackTileM);
+    const long long ks = (long long)(b * TAPS + t) * ncb + cb;
+    Split3 sp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_set(sp, j, s[(8 * h + j) * TAPS + t][ml]);
+    const long long row = ((ks * 3) * 2 + h) * lda + m0 + ml;  // plane 0 (k_split_pack layout)
+    pl[row] = sp.hi;
+    pl[row + 2LL * lda] = sp.mid;
+    pl[row + 4LL * lda] = sp.lo;
+  }
+}
+
 // ---------------------------------------------------------------- planning
 // Forward form (fwd and dgrad) runs stream-K (k_igemm_fwd_sk): 128-pixel tiles of 128, 64 or
 // 32 rows (by M: the ASPP forward has 19 classes), two K-steps per LDS stage, up to 512
@@ -308,22 +367,44 @@ static long long packed_elems(int nbranch, int taps, int cin, int cout, int for_
   return packed_f32_elems(nbranch, taps, cin, cout, for_dgrad) * 5 / 2;
 }
 
+static int g_pack_form = 1;  // msl_conv_set_pack_form: 1 = k_pack_split, 0 = k_pack + k_split_pack
+
 static int pack(const float* w, long long branch_stride, int nbranch, int taps, int cin, int cout,
                 int for_dgrad, float* packed, hipStream_t st) {
   const int cimg = for_dgrad ? cout : cin;
   const int m = for_dgrad ? cin : cout;
   const long long total = packed_f32_elems(nbranch, taps, cin, cout, for_dgrad);
-  const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
   const int lda = pad_to(m, kPackPad);
-  hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
-                     cdiv(cimg, kCB), lda, taps, total, packed);
-  MSL_CHECK_LAUNCH();
-  if (m > 64) {
-    const int ksteps = nbranch * cdiv(cimg, kCB) * taps;
-    hipLaunchKernelGGL(k_split_pack, dim3((int)std::min<long long>(cdiv(total, 256), 4096)), dim3(256), 0,
-                       st, packed, ksteps, lda, reinterpret_cast<__bf16*>(packed + total));
+  const int ncb = cdiv(cimg, kCB);
+  __bf16* planes = reinterpret_cast<__bf16*>(packed + total);
+  // M <= 64 has no planes to split, and its 128-row padding is mostly zeros, which k_pack's
+  // fully coalesced rows write faster (ASPP fwd 2048 -> 19: 5.2 vs 9.5 us)
+  if (g_pack_form == 0 || m <= 64) {  // element-wise gather, then a separate split
+    const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
+    hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
+                       ncb, lda, taps, total, packed);
     MSL_CHECK_LAUNCH();
+    if (m > 64) {
+      const int ksteps = nbranch * ncb * taps;
+      hipLaunchKernelGGL(k_split_pack, dim3((int)std::min<long long>(cdiv(total, 256), 4096)), dim3(256),
+                         0, st, packed, ksteps, lda, planes);
+      MSL_CHECK_LAUNCH();
+    }
+    return MSL_OK;
   }
+  // lda is a multiple of kPackPad (128): the m chunks tile it exactly, zero rows included
+  static_assert(kPackPad % kPackTileM == 0, "pack tiles must cover lda");
+  const dim3 grid(lda / kPackTileM, ncb, nbranch);
+  const int split = m > 64;
+  if (taps == 9)
+    hipLaunchKernelGGL(k_pack_split<9>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
+                       lda, split, packed, planes);
+  else if (taps == 1)
+    hipLaunchKernelGGL(k_pack_split<1>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
+                       lda, split, packed, planes);
+  else
+    return MSL_ERR_ARG;
+  MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
 
@@ -427,6 +508,12 @@ int msl_conv_set_f32_form(int form) {
 }
 
 int msl_conv_f32_form(void) { return g_f32_form; }
+
+int msl_conv_set_pack_form(int form) {
+  if (form != 0 && form != 1) return MSL_ERR_ARG;
+  g_pack_form = form;
+  return MSL_OK;
+}
 
 const char* msl_status_string(int status) {
   switch (status) {

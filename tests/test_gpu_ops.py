@@ -389,3 +389,35 @@ def test_conv_bf16_math(kind, cin, cout, h, w, d):
     conv(_bf(x), wr).backward(_bf(gy))
     assert _rel(xg.grad, dx_ref) < 1e-5
     assert _rel(wg.grad, wr.grad) < 1e-5
+
+
+# ----------------------------------------------------------------------------- weight packs
+@pytest.mark.parametrize("kind,nb,cin,cout,for_dgrad", [
+    ("d", 1, 256, 256, 0), ("d", 1, 256, 256, 1), ("d", 2, 2048, 19, 0), ("d", 2, 2048, 19, 1),
+    ("d", 1, 64, 64, 0), ("d", 1, 40, 200, 1), ("d", 1, 200, 40, 0),
+    ("p", 1, 1024, 256, 0), ("p", 1, 256, 1024, 1), ("p", 1, 130, 70, 0), ("p", 1, 70, 130, 1)])
+def test_pack_forms_identical(kind, nb, cin, cout, for_dgrad):
+    """The LDS-transposing pack+split kernel writes exactly the bytes of the element-wise pack
+    followed by k_split_pack (fp32 pack and bf16x6 planes), incl. padding rows and 2 branches."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    k = 3 if kind == "d" else 1
+    w = torch.randn(nb, cout, cin, k, k, generator=torch.Generator().manual_seed(cin * 7 + cout)).to(DEV)
+    total = lib.msl_dconv_packed_elems(nb, cin, cout, for_dgrad) if kind == "d" else \
+        lib.msl_pconv_packed_elems(cin, cout, for_dgrad)
+    bufs = []
+    try:
+        for form in (0, 1):
+            assert lib.msl_conv_set_pack_form(form) == 0
+            buf = torch.full((total,), float("nan"), device=DEV)
+            if kind == "d":
+                st = lib.msl_dconv_pack(w.data_ptr(), cout * cin * 9, nb, cin, cout, for_dgrad, buf.data_ptr(),
+                                        hip.stream_ptr())
+            else:
+                st = lib.msl_pconv_pack(w.data_ptr(), cin, cout, for_dgrad, buf.data_ptr(), hip.stream_ptr())
+            assert st == 0
+            bufs.append(buf)
+        torch.cuda.synchronize()
+    finally:
+        lib.msl_conv_set_pack_form(1)
+    assert torch.equal(bufs[0].view(torch.int32), bufs[1].view(torch.int32))
