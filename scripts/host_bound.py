@@ -26,5 +26,15 @@ for _ in range(N):
 t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
+print("per-step host enqueue (ms):", " ".join(f"{h*1e3:.1f}" for h in host))
+torch.cuda.synchronize()
+first = []
+for _ in range(3):  # one step from a drained queue: the host cost alone
+    torch.cuda.synchronize()
+    h0 = time.perf_counter()
+    tr.uda_step(*b)
+    first.append(time.perf_counter() - h0)
+torch.cuda.synchronize()
+print("from a drained queue (ms):", " ".join(f"{h*1e3:.1f}" for h in first))
 print(f"host enqueue per step: median {sorted(host)[N//2]*1e3:.2f} ms  (all {N}: {(t1-t0)/N*1e3:.2f} ms/step)"
       f"  wall incl. drain {(t2-t0)/N*1e3:.2f} ms/step  tail drain {(t2-t1)*1e3:.1f} ms")
