@@ -246,6 +246,16 @@ int msl_bn_set_fused(int fused);
 int msl_bn_fused(void);
 
 /* ------------------------------------------------------------------------
+ * Training-time evaluation (tools/train_source.py:280-283 + utils/eval.py:109-118): for one
+ * image's prediction pred[c][p] (fp32, the upsampled logits) and label[p] (int64, pixels outside
+ * [0, c) ignored), confusion[gt * c + argmax] += 1 over the pixels, on the stream;
+ * argmax = np.argmax over classes (lowest index on ties, NaN wins).  argmax_out [p] (int32,
+ * nullable) receives the per-pixel argmax.  c <= 64.  Exact, deterministic counts.
+ * ---------------------------------------------------------------------- */
+int msl_confusion_accumulate(const float* pred, const long long* label, int c, long long p,
+                             unsigned long long* confusion, int* argmax_out, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * SGD step with the reference's duplicated-parameter semantics (quirk Q2):
  * torch.optim.SGD(momentum, weight_decay) single-tensor loop over the
  * optim_parameters() groups (train_source.py:139-144, deeplab_multi.py:132-171),

@@ -62,6 +62,7 @@ SIGNATURES = {
     "msl_maxsquare_prob_bwd": (c_int, [c_p, c_int, c_int, c_p, c_p, c_p]),
     "msl_iw_maxsquare_prob_fwd": (c_int, [c_p, c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "msl_iw_maxsquare_prob_bwd": (c_int, [c_p, c_int, c_int, c_p, c_p, c_p, c_p]),
+    "msl_confusion_accumulate": (c_int, [c_p, c_p, c_int, ctypes.c_longlong, c_p, c_p, c_p]),
     "msl_bn_set_fused": (c_int, [c_int]),
     "msl_bn_fused": (c_int, []),
     "msl_bn_workspace": (c_sz, [c_int, c_int]),

@@ -11,8 +11,9 @@ the training arithmetic:
     replicated and gradients are all-reduced over RCCL (utils/dist.py);
   - loss scalars stay on the device (no per-iteration .cpu().item() sync);
     the NaN check of :277-278 runs on the accumulated value at epoch end;
-  - the per-iteration D2H argmax + Eval confusion matrix (:280-283) and
-    tensorboard logging are out of scope.
+  - the per-iteration argmax + Eval confusion matrix (:280-283) run on the
+    device (utils/eval.py, csrc/eval.hip), no D2H copy of the prediction;
+    tensorboard logging is out of scope.
 """
 import argparse
 import logging
@@ -25,6 +26,7 @@ import torch.distributed as dist
 
 from .. import ops
 from ..utils.dist import GradReducer
+from ..utils.eval import Eval
 from ..utils.loss import CrossEntropyLoss
 from ..utils.optim import SGD
 from ..utils.synthetic import SyntheticDomain, init_weights
@@ -69,6 +71,7 @@ class Trainer:
         self.current_iter = 0
 
         self.loss = CrossEntropyLoss(weight=None, ignore_index=-1)
+        self.Eval = Eval(self.args.num_classes)  # train_source.py:93, confusion matrix on device
         ops.set_conv_math(getattr(self.args, "conv_math", "fp32"))
         if getattr(self.args, "f32_form", None):
             ops.set_f32_form(self.args.f32_form)
@@ -106,6 +109,7 @@ class Trainer:
         self.model.train()
         iter_num = self.dataloader.num_iterations
         loss_sum = torch.zeros((), device=self.device)
+        self.Eval.reset()
         for i in range(iter_num):
             x, y, _ = self.dataloader[i]
             self.poly_lr_scheduler(self.optimizer, init_lr=self.args.lr, iter=self.current_iter,
@@ -113,16 +117,24 @@ class Trainer:
             x = x.to(self.device, non_blocking=True)
             y = y.to(self.device, dtype=torch.long, non_blocking=True)
             loss_sum += self.source_step(x, y).detach()
+            self.Eval.add_batch(y, self.last_pred)  # train_source.py:280-283, argmax on device
             self.current_iter += 1
         mean = float(loss_sum) / max(iter_num, 1)
         if np.isnan(mean):
             raise ValueError("Loss is nan during training...")
         self.logger.info("The average loss of train epoch-%d-:%f", self.current_epoch, mean)
+        self.logger.info("Epoch:%d, PA:%.3f, MPA:%.3f, MIoU:%.3f, FWIoU:%.3f", self.current_epoch,
+                         self.Eval.Pixel_Accuracy(), self.Eval.Mean_Pixel_Accuracy() if not self.Eval.synthia
+                         else self.Eval.Mean_Pixel_Accuracy()[0], self.Eval.Mean_Intersection_over_Union()
+                         if not self.Eval.synthia else self.Eval.Mean_Intersection_over_Union()[0],
+                         self.Eval.Frequency_Weighted_Intersection_over_Union() if not self.Eval.synthia
+                         else self.Eval.Frequency_Weighted_Intersection_over_Union()[0])
 
     def source_step(self, x, y):
         """train_source.py:248-264: CE(x2,y) + lambda_seg*CE(x1,y); zero_grad; backward; step."""
         pred = self.model(x)
         pred, pred_2 = pred if isinstance(pred, tuple) else (pred, None)
+        self.last_pred = pred.detach()
         cur_loss = self.loss(pred, y)
         if self.args.multi:
             cur_loss = cur_loss + self.args.lambda_seg * self.loss(pred_2, y)

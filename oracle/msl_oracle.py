@@ -332,3 +332,49 @@ def source_step(model, opt, x, y, cfg, it):
     cur.backward()
     opt.step()
     return {"loss": cur.item()}
+
+
+# ----------------------------------------------------------------------------- evaluation
+# utils/eval.py:109-115 (__generate_matrix) and :25-98 (the metrics), restated in numpy.
+def confusion(gt, pred_logits, num_class):
+    """np.argmax over classes of pred [C, H, W], then bincount of num_class*gt + argmax over the
+    pixels with 0 <= gt < num_class (utils/eval.py:111-114; train_source.py:280-282)."""
+    arg = np.argmax(pred_logits.reshape(num_class, -1), axis=0)
+    g = gt.reshape(-1)
+    keep = (g >= 0) & (g < num_class)
+    idx = num_class * g[keep].astype(np.int64) + arg[keep]
+    return np.bincount(idx, minlength=num_class ** 2).reshape(num_class, num_class), arg
+
+
+_S16 = [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 15, 17, 18]   # utils/eval.py:9
+_S13 = [0, 1, 2, 6, 7, 8, 10, 11, 12, 13, 15, 17, 18]             # :10
+_S16_13 = [0, 1, 2, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15]           # :11
+
+
+def eval_metrics(cm, out_16_13=False):
+    """PA, MPA, MIoU, FWIoU, Precision of utils/eval.py:25-98 for a [C, C] float matrix (the
+    16-class SYNTHIA case returns (16, 13) pairs as the reference does)."""
+    cm = np.asarray(cm, dtype=np.float64)
+    n = cm.shape[0]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        diag, rows, cols = np.diag(cm), cm.sum(axis=1), cm.sum(axis=0)
+        pa = 0 if cm.sum() == 0 else diag.sum() / cm.sum()
+        mpa, iou, prec = diag / rows, diag / (rows + cols - diag), diag / cols
+        fw = rows * iou
+
+    def mean(v):
+        if n == 16:
+            return np.nanmean(v), np.nanmean(v[_S16_13])
+        if out_16_13:
+            return np.nanmean(v[_S16]), np.nanmean(v[_S13])
+        return np.nanmean(v)
+
+    def fwsum(v):
+        tot = cm.sum()
+        if n == 16:
+            return sum(x for x in v if not np.isnan(x)) / tot, sum(x for x in v[_S16_13] if not np.isnan(x)) / tot
+        if out_16_13:
+            return sum(x for x in v[_S16] if not np.isnan(x)) / tot, sum(x for x in v[_S13] if not np.isnan(x)) / tot
+        return sum(x for x in v if not np.isnan(x)) / tot
+
+    return {"PA": pa, "MPA": mean(mpa), "MIoU": mean(iou), "FWIoU": fwsum(fw), "Precision": mean(prec)}
