@@ -119,6 +119,7 @@ class UDATrainer(Trainer):
     def train_one_epoch(self, epoch=0):
         self.model.eval() if self.args.freeze_bn else self.model.train()
         self.iter_num = self.dataloader.num_iterations
+        self.Eval.reset()  # solve_gta5.py:294 (the UDA loop resets but never fills it)
         self._reset_meters()
         for i in range(self.iter_num):
             x_s, y_s, _ = self.source_dataloader[i % len(self.source_dataloader)]
