@@ -72,3 +72,22 @@ def test_device_confusion_matches_bincount(c, h, w):
     assert np.array_equal(cm.view(c, c).cpu().numpy(), ref0)
     ev.reset()
     assert ev.confusion_matrix.sum() == 0
+
+
+@pytest.mark.gpu
+def test_source_epoch_fills_eval_on_device():
+    """Trainer.train_one_epoch (train_source.py:241-283): every iteration's argmax lands in the
+    device confusion matrix; its total is the epoch's count of labelled pixels."""
+    import argparse
+    from maxsquareloss_amd.tools.train_source import Trainer, add_train_args, init_args
+    argv = ["--crop_size", "256,128", "--target_crop_size", "256,128", "--imagenet_pretrained", "False",
+            "--save_dir", "", "--synthetic_images", "2", "--iter_max", "200000"]
+    args, _, _ = init_args(add_train_args(argparse.ArgumentParser()).parse_args(argv))
+    tr = Trainer(args, cuda=True)
+    tr.train_one_epoch()
+    torch.cuda.synchronize()
+    c = args.num_classes
+    n = sum(int(((y >= 0) & (y < c)).sum()) for y in (tr.dataloader[i][1] for i in range(tr.dataloader.num_iterations)))
+    cm = tr.Eval.confusion_matrix
+    assert cm.shape == (c, c) and cm.sum() == n
+    assert 0.0 <= tr.Eval.Pixel_Accuracy() <= 1.0 and np.isfinite(tr.Eval.Mean_Intersection_over_Union())
