@@ -262,13 +262,16 @@ int main(int argc, char** argv) {
   const bool sk_only = argc > 1 && std::string(argv[1]) == "sk";
   // "fsk": every stream-K row, nothing else
   const bool fsk_only = argc > 1 && std::string(argv[1]) == "fsk";
-  const bool wsk_only = argc > 1 && std::string(argv[1]) == "wsk";
+  // "wsks": the small weight gradients of layers 1-2 (64 / 128 channels) by worker count
+  const bool wsks = argc > 1 && std::string(argv[1]) == "wsks";
+  const bool wsk_only = (argc > 1 && std::string(argv[1]) == "wsk") || wsks;
   // "x6": the matrix-core forms (f32, bf16, bf16x6) of the stream-K kernels vs an fp64 reference
   const bool x6_mode = argc > 1 && std::string(argv[1]) == "x6";
   // "rg": the row-grouped forward kernel (k_conv_rg) vs the stream-K one, every form, vs fp64
   const bool rg_mode = argc > 1 && std::string(argv[1]) == "rg";
   const int iters = sk_only ? 5 : 20;
-  Shape shapes[] = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
+  std::vector<Shape> shapes = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
+  if (wsks) shapes = {{128, 128, 65, 129, 1}, {64, 64, 129, 257, 1}};
   for (const Shape& sh : shapes) {
     if ((x6_mode || rg_mode) && (sh.cin != sh.cout || sh.h != 65)) continue;  // the model's layer3 / layer4 shapes
     const int P = sh.h * sh.w;
@@ -340,6 +343,12 @@ int main(int argc, char** argv) {
       FSKE(128, 128, 1, 5, 2, 2, 256, 4)
       WSKE(64, 64, 2, 512, 0) WSKE(64, 64, 2, 512, 1) WSKE(64, 64, 2, 512, 2)
       WSKE(128, 128, 2, 256, 0) WSKE(128, 128, 2, 256, 2) WSKE(64, 128, 2, 512, 2)
+      continue;
+    }
+    if (wsks) {
+      run_wgrad<64, 128, 32, 2, 2>(sh, x, dy, dwref, ws, 1, 1);
+      WSK(64, 64, 2, 512) WSK(64, 64, 2, 384) WSK(64, 64, 2, 256) WSK(64, 64, 2, 192) WSK(64, 64, 2, 128)
+      WSK(64, 64, 3, 256) WSK(64, 64, 3, 128)
       continue;
     }
     if (wsk_only) {
