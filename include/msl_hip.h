@@ -204,6 +204,13 @@ int msl_multi_ce_up_bwd(const float* logits1, const float* logits2, int c, int h
                         int ho, int wo, float thr, const float* stats, const float* gout,
                         float* dlogits1, void* ws, size_t ws_bytes, msl_stream_t stream);
 
+/* The per-pixel decisions inside the fused losses, written out (parity inspection; argmax1 and
+ * label2 are int32 [ho*wo], either nullable): argmax1 = first-max argmax of softmax(up(logits1))
+ * (torch.max at loss.py:84-86 / the IW histogram's class), label2 = the multi-level guidance
+ * label of msl_multi_ce_up_fwd with logits1 = x1, logits2 = x2 (solve_gta5.py:206-212). */
+int msl_loss_labels_up(const float* logits1, const float* logits2, int c, int hi, int wi, int ho,
+                       int wo, float thr, int32_t* argmax1, int32_t* label2, msl_stream_t stream);
+
 /* Probability-input forms, for callers that hand the loss an explicit prob
  * tensor exactly as the reference API does (loss.py:76, :110).
  * prob is [c][hw]; label (nullable) is int64 [hw]. */
@@ -254,6 +261,22 @@ int msl_bn_fused(void);
  * ---------------------------------------------------------------------- */
 int msl_confusion_accumulate(const float* pred, const long long* label, int c, long long p,
                              unsigned long long* confusion, int* argmax_out, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Input pipeline (the loaders' last host steps, on the device after a uint8 H2D copy; byte-exact):
+ *   msl_image_transform: out[c][y][x] = (float)rgb[y][xs][2 - c] - mean[c] (BGR order, mean =
+ *     IMG_MEAN = {B, G, R}), xs = mirror ? w-1-x : x; rgb is uint8 HWC, out fp32 CHW
+ *     (datasets/cityscapes_Dataset.py:14, 245-251 _img_transform with numpy_transform; the
+ *     random_mirror FLIP_LEFT_RIGHT of _train_sync_transform);
+ *   msl_label_transform: out[y][x] = lut256[ids[y][xs]] as int64 (trainId, -1 = ignore): the
+ *     dataset's id_to_trainid composed with its 16/13-class remap (cityscapes_Dataset.py:124-155,
+ *     260-264 id2trainId / _mask_transform; gta5_Dataset.py:73-75; synthia_Dataset.py:56-62).
+ *     lut256 is a device int32[256] table.
+ * ---------------------------------------------------------------------- */
+int msl_image_transform(const uint8_t* rgb, int h, int w, int mirror, float mean_b, float mean_g,
+                        float mean_r, float* out, msl_stream_t stream);
+int msl_label_transform(const uint8_t* ids, int h, int w, int mirror, const int32_t* lut256,
+                        int64_t* out, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * SGD step with the reference's duplicated-parameter semantics (quirk Q2):

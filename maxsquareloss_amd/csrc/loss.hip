@@ -553,6 +553,36 @@ __global__ void __launch_bounds__(256) k_prob_bwd(const float* __restrict__ prob
   }
 }
 
+// ---------------------------------------------------------------- label inspection
+// The per-pixel decisions the fused losses take internally, written out: arg[px] = first-max
+// argmax of softmax(up(L1)) (the IW histogram's class, loss.py:84-86), label2[px] = the
+// multi-level guidance label with P = softmax(up(L2)), P2 = softmax(up(L1)) (solve_gta5.py:
+// 206-212; -1 = ignored).  Same device functions as k_loss_fwd / pixel_grad.
+template <int CM>
+__global__ void __launch_bounds__(256) k_loss_labels(const float* __restrict__ L1,
+                                                      const float* __restrict__ L2, Geo g,
+                                                      float thr, int32_t* __restrict__ arg,
+                                                      int32_t* __restrict__ label2) {
+  const int npx = g.Ho * g.Wo;
+  for (int px = blockIdx.x * 256 + threadIdx.x; px < npx; px += gridDim.x * 256) {
+    const int oy = px / g.Wo, ox = px - oy * g.Wo;
+    const Lin ly = lin(oy, g.sh, g.Hi), lx = lin(ox, g.sw, g.Wi);
+    float v[CM], p[CM], mx, sum;
+    up_logits<CM>(L1, g, ly, lx, v);
+    softmax<CM>(v, g.C, p, mx, sum);
+    if (arg) {
+      float best;
+      arg[px] = argmax_first<CM>(p, g.C, best);
+    }
+    if (label2) {
+      float v2[CM], P[CM], mx2, sum2;
+      up_logits<CM>(L2, g, ly, lx, v2);
+      softmax<CM>(v2, g.C, P, mx2, sum2);
+      label2[px] = multi_label<CM>(P, p, g.C, thr);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- host helpers
 static bool geo_ok(int c, int hi, int wi, int ho, int wo) {
   return c >= 1 && c <= kMaxC && hi >= 1 && wi >= 1 && ho >= 1 && wo >= 1 &&
@@ -741,6 +771,19 @@ int msl_multi_ce_up_bwd(const float* logits1, const float* logits2, int c, int h
   if (!logits1 || !logits2 || !stats || !gout) return MSL_ERR_ARG;
   return loss_bwd<K_MULTI>(logits1, logits2, nullptr, nullptr, c, hi, wi, ho, wo, thr, stats,
                            gout, dlogits1, ws, ws_bytes, stream);
+}
+
+int msl_loss_labels_up(const float* logits1, const float* logits2, int c, int hi, int wi, int ho,
+                       int wo, float thr, int32_t* argmax1, int32_t* label2, msl_stream_t stream) {
+  if (!geo_ok(c, hi, wi, ho, wo) || !logits1 || (label2 && !logits2)) return MSL_ERR_ARG;
+  if (!argmax1 && !label2) return MSL_OK;
+  const Geo g = make_geo(c, hi, wi, ho, wo);
+  const int nblk = std::min(4096, cdiv((long long)ho * wo, 256));
+  MSL_DISPATCH_C(c, CM,
+                 hipLaunchKernelGGL((k_loss_labels<CM>), dim3(nblk), dim3(256), 0, as_stream(stream),
+                                    logits1, logits2, g, thr, argmax1, label2));
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
 }
 
 int msl_maxsquare_prob_fwd(const float* prob, int c, int hw, float* out, void* ws,

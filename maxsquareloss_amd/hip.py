@@ -58,6 +58,7 @@ SIGNATURES = {
     "msl_iw_maxsquare_up_bwd": (c_int, [c_p] + [c_int] * 5 + [c_p, c_p, c_p, c_p, c_sz, c_p]),
     "msl_multi_ce_up_fwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_f, c_p, c_p, c_p, c_sz, c_p]),
     "msl_multi_ce_up_bwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_f, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "msl_loss_labels_up": (c_int, [c_p, c_p] + [c_int] * 5 + [c_f, c_p, c_p, c_p]),
     "msl_maxsquare_prob_fwd": (c_int, [c_p, c_int, c_int, c_p, c_p, c_sz, c_p]),
     "msl_maxsquare_prob_bwd": (c_int, [c_p, c_int, c_int, c_p, c_p, c_p]),
     "msl_iw_maxsquare_prob_fwd": (c_int, [c_p, c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_sz, c_p]),
@@ -68,6 +69,8 @@ SIGNATURES = {
     "msl_bn_workspace": (c_sz, [c_int, c_int]),
     "msl_bn_fwd": (c_int, [c_p] * 10 + [c_int] * 4 + [c_f, c_f, c_int, c_p, c_sz, c_p]),
     "msl_bn_bwd": (c_int, [c_p] * 10 + [c_int] * 5 + [c_p, c_sz, c_p]),
+    "msl_image_transform": (c_int, [c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p, c_p]),
+    "msl_label_transform": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
     "msl_sgd_block_elems": (c_int, []),
     "msl_sgd_plan": (c_ll, [c_p, c_int, c_p, c_p, c_ll]),
     "msl_sgd_step": (c_int, [c_p, c_p, c_p, c_ll, c_f, c_f, c_f, c_f, c_f, c_p]),

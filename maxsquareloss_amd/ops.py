@@ -390,7 +390,7 @@ def upsample_bilinear(x, size):
     the low-resolution logits instead of re-reading the upsampled tensor.
     """
     y = _Upsample.apply(x, int(size[0]), int(size[1]))
-    y._msl_low = x
+    y._msl_low = (x, y._version, x._version)
     return y
 
 
@@ -538,8 +538,32 @@ class _MultiCEUp(Function):
 
 
 def low_of(pred):
-    """The low-resolution logits behind an upsampled prediction, or None."""
-    return getattr(pred, "_msl_low", None)
+    """The low-resolution logits behind an upsampled prediction, or None when there are none or
+    when either tensor was modified in place since the upsample (then the loss must read `pred`
+    itself: the fused path would silently ignore the edit)."""
+    rec = getattr(pred, "_msl_low", None)
+    if rec is None:
+        return None
+    low, v_pred, v_low = rec
+    if pred._version != v_pred or low._version != v_low:
+        return None
+    return low
+
+
+def loss_labels_up(low1, low2, out_hw, thr=0.95):
+    """(argmax, label2) int32 [ho*wo]: the per-pixel decisions of the fused losses - first-max
+    argmax of softmax(up(low1)) (IW histogram class) and, if low2 is given, the multi-level
+    guidance label with low1 = x1 head, low2 = x2 head (solve_gta5.py:206-212)."""
+    low1 = _check_act(low1.detach(), "loss_labels_up")
+    c, hi, wi, ho, wo = _geom(low1, out_hw)
+    arg = torch.empty(ho * wo, dtype=torch.int32, device=low1.device)
+    lab = None
+    if low2 is not None:
+        low2 = _check_act(low2.detach(), "loss_labels_up")
+        lab = torch.empty(ho * wo, dtype=torch.int32, device=low1.device)
+    hip.check(hip.load().msl_loss_labels_up(low1.data_ptr(), hip.ptr(low2), c, hi, wi, ho, wo, float(thr),
+                                            arg.data_ptr(), hip.ptr(lab), hip.stream_ptr()), "msl_loss_labels_up")
+    return arg, lab
 
 
 def ce_up(low, labels, out_hw):

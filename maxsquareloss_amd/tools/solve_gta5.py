@@ -15,6 +15,7 @@ Style-transfer augmentation (exp_tag source_aug/target_aug) and the
 validation/eval path are out of scope.
 """
 import argparse
+import os
 
 import torch
 
@@ -102,6 +103,20 @@ class UDATrainer(Trainer):
 
     # ---------------------------------------------------------------- loop
     def main(self):
+        """solve_gta5.py:237-267: start from --pretrained_ckpt_file (the source-trained model); the
+        counters restart unless --continue_training, which resumes from --checkpoint_dir; iter_max
+        covers the rounds still to run."""
+        if self.args.pretrained_ckpt_file is not None:
+            path = self.args.pretrained_ckpt_file
+            if os.path.isdir(path):
+                path = self.args.checkpoint_dir
+            self.load_checkpoint(path)
+        if not self.args.continue_training:
+            self.best_MIou = 0
+            self.current_iter = 0
+            self.current_epoch = 0
+        else:
+            self.load_checkpoint(self.args.checkpoint_dir)
         self.args.iter_max = self.current_iter + self.dataloader.num_iterations * \
             self.args.epoch_each_round * self.round_num
         self.optimizer.zero_grad()

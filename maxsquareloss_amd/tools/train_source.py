@@ -26,6 +26,7 @@ import torch.distributed as dist
 
 from .. import ops
 from ..utils.dist import GradReducer
+from ..utils.checkpoint import load_checkpoint, save_checkpoint
 from ..utils.eval import Eval
 from ..utils.loss import CrossEntropyLoss
 from ..utils.optim import SGD
@@ -95,8 +96,12 @@ class Trainer:
 
     # ------------------------------------------------------------------ loop
     def main(self):
-        if self.args.continue_training and self.args.checkpoint_dir:
+        """train_source.py:161-173: restore --checkpoint_dir whenever it is given; the counters
+        restart unless --continue_training."""
+        if self.args.checkpoint_dir is not None:
             self.load_checkpoint(self.args.checkpoint_dir)
+        if not self.args.continue_training:
+            self.current_epoch = 0
         self.train()
 
     def train(self):
@@ -106,7 +111,8 @@ class Trainer:
         self.save_checkpoint(self.train_id + "final.pth")
 
     def train_one_epoch(self, epoch=None):
-        self.model.train()
+        # train_source.py:225-229: --freeze_bn keeps BN on its running statistics
+        self.model.eval() if self.args.freeze_bn else self.model.train()
         iter_num = self.dataloader.num_iterations
         loss_sum = torch.zeros((), device=self.device)
         self.Eval.reset()
@@ -149,29 +155,19 @@ class Trainer:
 
     # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, filename=None):
+        """train_source.py:662-678 (utils/checkpoint.py)."""
         if self.rank != 0 or not self.args.save_dir:
             return
-        os.makedirs(self.args.save_dir, exist_ok=True)
-        filename = os.path.join(self.args.save_dir, filename)
-        state = {"epoch": self.current_epoch + 1, "iteration": self.current_iter,
-                 "state_dict": self.model.state_dict(), "optimizer": self.optimizer.state_dict(),
-                 "best_MIou": self.best_MIou}
-        torch.save(state, filename)
+        save_checkpoint(os.path.join(self.args.save_dir, filename), self.model, self.optimizer,
+                        self.current_epoch + 1, self.current_iter, self.best_MIou)
 
     def load_checkpoint(self, filename):
-        try:
-            checkpoint = torch.load(filename, map_location=self.device, weights_only=True)
-        except OSError:
-            self.logger.info("No checkpoint exists from '%s'. Skipping...", filename)
-            return
-        sd = checkpoint["state_dict"]
-        sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}  # DataParallel prefix
-        self.model.load_state_dict(sd)
-        if "optimizer" in checkpoint:
-            self.optimizer.load_state_dict(checkpoint["optimizer"])
-            self.current_epoch = checkpoint["epoch"]
-            self.current_iter = checkpoint["iteration"]
-            self.best_MIou = checkpoint["best_MIou"]
+        """train_source.py:680-704 (utils/checkpoint.py): weights, then optimizer + counters."""
+        got = load_checkpoint(filename, self.model, self.optimizer, map_location=self.device)
+        if got:
+            self.current_epoch = got["epoch"]
+            self.current_iter = got["iteration"]
+            self.best_MIou = got["best_MIou"]
 
     # ------------------------------------------------------------------ LR
     def poly_lr_scheduler(self, optimizer, init_lr=None, iter=None, max_iter=None, power=None):

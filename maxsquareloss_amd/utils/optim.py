@@ -193,20 +193,29 @@ class SGD:
 
     # -- checkpoints (train_source.py:662-704 stores optimizer.state_dict()) -----------
     def state_dict(self):
-        idx, state, groups = 0, {}, []
+        """torch.optim.Optimizer.state_dict's format: list positions numbered across the groups,
+        every occurrence of a duplicated parameter (Q2) mapped to one position, and one
+        momentum buffer per tensor under that index - what the reference's torch.optim.SGD writes
+        into its checkpoints (train_source.py:672-674)."""
+        first, start, groups = {}, 0, []
         for g in self.param_groups:
-            ids = []
-            for p in g["params"]:
-                ids.append(idx)
-                if p in self.state and "momentum_buffer" in self.state[p]:
-                    state[idx] = {"momentum_buffer": self.state[p]["momentum_buffer"].detach().clone()}
-                idx += 1
+            # torch's pack_group: one dict comprehension per group, so inside a group the LAST
+            # position of a duplicated tensor wins; a tensor seen in an earlier group keeps that one
+            first.update({id(p): i for i, p in enumerate(g["params"], start) if id(p) not in first})
             pg = {k: v for k, v in g.items() if k not in ("params", "_unique")}
-            pg["params"] = ids
+            pg["params"] = [first[id(p)] for p in g["params"]]
+            start += len(g["params"])
             groups.append(pg)
+        state = {}
+        for g in self.param_groups:
+            for p, _ in g["_unique"]:
+                st = self.state.get(p)
+                if st is not None and "momentum_buffer" in st:
+                    state[first[id(p)]] = {"momentum_buffer": st["momentum_buffer"].detach().clone()}
         return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd):
+        """Accepts this class's and torch.optim.SGD's state dicts (same format)."""
         flat = [p for g in self.param_groups for p in g["params"]]
         for i, s in sd["state"].items():
             p = flat[int(i)]
@@ -214,6 +223,6 @@ class SGD:
                 self.state.setdefault(p, {})["momentum_buffer"] = s["momentum_buffer"].to(p.device).clone()
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             for k, v in sg.items():
-                if k != "params":
+                if k in ("lr", "momentum", "weight_decay"):
                     g[k] = v
         self._table_key = None

@@ -72,9 +72,14 @@ def init_weights(model, seed=12345):
     return model
 
 
+def synthetic_rgb(h, w, seed):
+    """(h, w, 3) uint8 RGB, U[0, 255]."""
+    return np.floor(counter_uniform(seed, "image", h * w * 3) * 256.0).astype(np.uint8).reshape(h, w, 3)
+
+
 def synthetic_image(h, w, seed):
-    """(1, 3, h, w) fp32: uint8 RGB -> BGR - IMG_MEAN, CHW."""
-    rgb = np.floor(counter_uniform(seed, "image", h * w * 3) * 256.0).astype(np.uint8).reshape(h, w, 3)
+    """(1, 3, h, w) fp32: uint8 RGB -> BGR - IMG_MEAN, CHW (host form of utils/preprocess.image_transform)."""
+    rgb = synthetic_rgb(h, w, seed)
     img = rgb.astype(np.float32)[:, :, ::-1] - IMG_MEAN
     return torch.from_numpy(img.transpose(2, 0, 1).copy()).unsqueeze(0)
 

@@ -15,6 +15,8 @@ maxsquareloss_amd/ may import it.
                        (train_source.py:139-144; deeplab_multi.py:132-171; quirk Q2)
   uda_step()           tools/solve_gta5.py:335-387
   source_step()        tools/train_source.py:233-264
+  image_transform()    datasets/cityscapes_Dataset.py:14, 245-251 (numpy_transform)
+  label_transform()    datasets/cityscapes_Dataset.py:141-155, 260-264 (id2trainId)
 
 Pinned against the real reference: tests/golden/*.npz are produced by
 oracle/gen_golden.py, which imports the reference's own deeplab_multi.py and
@@ -378,3 +380,28 @@ def eval_metrics(cm, out_16_13=False):
         return sum(x for x in v if not np.isnan(x)) / tot
 
     return {"PA": pa, "MPA": mean(mpa), "MIoU": mean(iou), "FWIoU": fwsum(fw), "Precision": mean(prec)}
+
+
+# ----------------------------------------------------------------------------- input pipeline
+def image_transform(rgb, mean, mirror=False):
+    """cityscapes_Dataset.py:245-251 with numpy_transform: uint8 RGB HWC -> float32, BGR,
+    minus IMG_MEAN (float32), CHW; mirror = Image.FLIP_LEFT_RIGHT first (:182)."""
+    img = np.asarray(rgb[:, ::-1] if mirror else rgb, np.float32)
+    img = img[:, :, ::-1] - np.asarray(mean, np.float32)
+    return img.transpose(2, 0, 1).copy()
+
+
+def label_transform(ids, id_to_trainid, set_16=None, set_13=None, mirror=False):
+    """cityscapes_Dataset.py:141-155: ids -> trainIds (-1 for unlisted ids), then the optional
+    16- or 13-class remap (trainIds outside the set -> -1)."""
+    lab = np.asarray(ids[:, ::-1] if mirror else ids, np.float32)
+    out = np.full(lab.shape, -1, np.float32)
+    for k, v in id_to_trainid.items():
+        out[lab == k] = v
+    for sub in (set_16, set_13):
+        if sub is not None:
+            o2 = np.full(lab.shape, -1, np.float32)
+            for i, t in enumerate(sub):
+                o2[out == t] = i
+            out = o2
+    return out

@@ -195,3 +195,32 @@ def test_step_goldens_cfg1():
         x, y = synthetic_image(h, w, 100 + it), synthetic_labels(h, w, 19, 100 + it)
         out = orc.source_step(model, opt, x, y, cfg, it)
         assert out["loss"] == pytest.approx(float(g[f"src_it{it}_loss"]), rel=1e-4)
+
+
+def test_preprocess_kat():
+    """The oracle's loader transforms and the product's id->trainId tables (utils/preprocess.py,
+    host side) reproduce the reference's own _img_transform / id2trainId outputs
+    (preprocess_kat.npz, written by oracle/gen_golden_preprocess.py)."""
+    from maxsquareloss_amd.utils import preprocess as pp
+    g = gold("preprocess_kat.npz")
+    tables = {"cityscapes": pp.CITYSCAPES_ID_TO_TRAINID, "gta5": pp.GTA5_ID_TO_TRAINID,
+              "synthia": pp.SYNTHIA_ID_TO_TRAINID}
+    n = 0
+    for tag in ("a", "b", "c"):
+        rgb, ids = g[f"{tag}_rgb"], g[f"{tag}_ids"]
+        for m in (0, 1):
+            assert np.array_equal(orc.image_transform(rgb, g["img_mean"], bool(m)), g[f"{tag}_m{m}_img"])
+            for ds, table in tables.items():
+                for cls in ("19", "16", "13"):
+                    key = f"{tag}_m{m}_{ds}_{cls}"
+                    if key not in g.files:
+                        continue
+                    s16 = pp.SET_16 if cls == "16" else None
+                    s13 = pp.SET_13 if cls == "13" else None
+                    want = g[key]
+                    assert np.array_equal(orc.label_transform(ids, table, s16, s13, bool(m)), want), key
+                    lut = pp.build_lut(ds, cls == "16", cls == "13")
+                    d = ids[:, ::-1] if m else ids
+                    assert np.array_equal(lut[d].astype(np.float32), want), key
+                    n += 1
+    assert n == 3 * 2 * 8
