@@ -64,6 +64,8 @@ def parse():
                     help="BN kernels: one fused launch per call (default) or split statistics/apply launches")
     ap.add_argument("--f32-form", default=None, choices=["mfma_f32", "bf16x6"],
                     help="matrix-core form of the fp32 convs (default: the library's)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: iterations after the first replay one captured hipGraph (single process); 0: eager")
     ap.add_argument("--cpu-baseline-iters", type=int, default=2, help="0 disables the CPU baseline")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM traffic per launch of the dominant kernel (from a rocprofv3 --pmc run)")
@@ -78,7 +80,7 @@ def main():
     argv = ["--crop_size", f"{a.width},{a.height}", "--target_crop_size", f"{a.width},{a.height}",
             "--imagenet_pretrained", "False", "--save_dir", "", "--num_classes", str(a.num_classes),
             "--target_mode", a.target_mode, "--multi", a.multi, "--lambda_target", str(a.lambda_target),
-            "--iter_max", "200000", "--conv_math", a.conv_math]
+            "--iter_max", "200000", "--conv_math", a.conv_math, "--graph", str(bool(a.graph and world == 1))]
     if a.f32_form:
         argv += ["--f32_form", a.f32_form]
     args, _, _ = init_args(build_parser().parse_args(argv))
@@ -96,16 +98,24 @@ def main():
                         synthetic_image(H, W, 500 + seed).to(dev)))
     torch.cuda.synchronize()
 
+    h3, w3 = feat_hw(H), feat_hw(W)
+    key = (1, 256, 256, h3, w3, 2)
+    graphed = bool(tr.use_graph)
+    if graphed:
+        # the dominant kernel's HIP events are recorded into the captured graph (capture happens in
+        # the first call) and re-recorded by every replay: their times are those of the last step
+        ops.PROBE[key] = []
     first_losses = None
-    for i in range(a.warmup):
+    n_probe_eager = 0
+    for i in range(max(a.warmup, 1 if graphed else 0)):
         tr.uda_step(*batches[i % 2])
         if i == 0:
             first_losses = {"loss_seg": tr.loss_val.detach().clone(), "loss_target": tr.loss_target.detach().clone()}
+            if graphed:
+                n_probe_eager = len(ops.PROBE[key]) // 2  # eager iteration 0, then the capture
     torch.cuda.synchronize()
-
-    h3, w3 = feat_hw(H), feat_hw(W)
-    key = (1, 256, 256, h3, w3, 2)
-    ops.PROBE[key] = []
+    if not graphed:
+        ops.PROBE[key] = []
 
     if dist.is_initialized():
         dist.barrier()
@@ -118,6 +128,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     probes = ops.PROBE.pop(key)
+    if graphed:
+        probes = probes[n_probe_eager:]  # the captured events, as recorded by the last replay
     kern_ms = sum(s.elapsed_time(e) for s, e in probes) / max(len(probes), 1)
 
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -183,7 +195,7 @@ def main():
         "data": "synthetic (counter-generated uint8 images -> BGR-mean, uniform labels; random-init weights)",
         "config": {"workload": f"{'SYNTHIA' if C == 16 else 'GTA5'}->Cityscapes {args.target_mode} UDA step "
                                f"(solve_gta5.py), {W}x{H}, bs=1/GPU",
-                   "conv_math": a.conv_math, "bn_form": a.bn_form, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
+                   "conv_math": a.conv_math, "bn_form": a.bn_form, "hipgraph": graphed, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
                    "target_mode": args.target_mode, "multi": args.multi, "lambda_target": args.lambda_target,
                    "num_classes": C, "global_batch": 2 * world, "parallelism": f"dp{world}"},
         "roofline": roofline, "cpu_baseline": cpu,

@@ -305,6 +305,12 @@ long long msl_sgd_plan(const long long* numels, int n_entries, int32_t* block_en
 int msl_sgd_step(const msl_sgd_entry* entries, const int32_t* block_entry,
                  const long long* block_offset, long long n_blocks, float lr0, float lr1,
                  float momentum, float weight_decay, float grad_scale, msl_stream_t stream);
+/* The same step with the two group learning rates read from device memory (lr_dev[0] = group 0,
+ * lr_dev[1] = group 1) when the kernel runs, so a captured hipGraph replays the poly schedule
+ * (train_source.py:706-717) by updating lr_dev between replays. */
+int msl_sgd_step_lr_dev(const msl_sgd_entry* entries, const int32_t* block_entry,
+                        const long long* block_offset, long long n_blocks, const float* lr_dev,
+                        float momentum, float weight_decay, float grad_scale, msl_stream_t stream);
 
 #ifdef __cplusplus
 }

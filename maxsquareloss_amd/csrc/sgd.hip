@@ -21,12 +21,14 @@ constexpr int kSgdBlockElems = 4096;
 __global__ void __launch_bounds__(256) k_sgd(const msl_sgd_entry* __restrict__ entries,
                                               const int32_t* __restrict__ block_entry,
                                               const long long* __restrict__ block_offset,
-                                              float lr0, float lr1, float mom, float wd,
-                                              float gscale) {
+                                              float lr0, float lr1, const float* __restrict__ lr_dev,
+                                              float mom, float wd, float gscale) {
   const msl_sgd_entry e = entries[block_entry[blockIdx.x]];
   const long long base = block_offset[blockIdx.x];
   const long long end = base + kSgdBlockElems < e.numel ? base + kSgdBlockElems : e.numel;
-  const float lr = e.group ? lr1 : lr0;
+  // the learning rates by value, or from device memory (a replayed hipGraph: the poly schedule
+  // changes them every iteration, train_source.py:706-717)
+  const float lr = lr_dev ? lr_dev[e.group ? 1 : 0] : (e.group ? lr1 : lr0);
   const float nlr = -lr;
   for (long long i = base + threadIdx.x; i < end; i += 256) {
     float p = e.param[i];
@@ -73,7 +75,20 @@ int msl_sgd_step(const msl_sgd_entry* entries, const int32_t* block_entry,
     return MSL_ERR_ARG;
   if (n_blocks == 0) return MSL_OK;
   hipLaunchKernelGGL(k_sgd, dim3((unsigned)n_blocks), dim3(256), 0, as_stream(stream), entries,
-                     block_entry, block_offset, lr0, lr1, momentum, weight_decay, grad_scale);
+                     block_entry, block_offset, lr0, lr1, (const float*)nullptr, momentum, weight_decay,
+                     grad_scale);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+int msl_sgd_step_lr_dev(const msl_sgd_entry* entries, const int32_t* block_entry,
+                        const long long* block_offset, long long n_blocks, const float* lr_dev,
+                        float momentum, float weight_decay, float grad_scale, msl_stream_t stream) {
+  if (!entries || !block_entry || !block_offset || !lr_dev || n_blocks < 0 || n_blocks > 0x7fffffff)
+    return MSL_ERR_ARG;
+  if (n_blocks == 0) return MSL_OK;
+  hipLaunchKernelGGL(k_sgd, dim3((unsigned)n_blocks), dim3(256), 0, as_stream(stream), entries,
+                     block_entry, block_offset, 0.f, 0.f, lr_dev, momentum, weight_decay, grad_scale);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }

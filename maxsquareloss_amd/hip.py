@@ -74,6 +74,7 @@ SIGNATURES = {
     "msl_sgd_block_elems": (c_int, []),
     "msl_sgd_plan": (c_ll, [c_p, c_int, c_p, c_p, c_ll]),
     "msl_sgd_step": (c_int, [c_p, c_p, c_p, c_ll, c_f, c_f, c_f, c_f, c_f, c_p]),
+    "msl_sgd_step_lr_dev": (c_int, [c_p, c_p, c_p, c_ll, c_p, c_f, c_f, c_f, c_p]),
 }
 
 ABI_VERSION = 1

@@ -20,8 +20,9 @@ import os
 import torch
 
 from ..utils.loss import IW_MaxSquareloss, MaxSquareloss, multi_level_guidance_ce
+from ..utils.graph import GraphedStep
 from ..utils.synthetic import SyntheticDomain
-from .train_source import Trainer, add_train_args, init_args
+from .train_source import Trainer, add_train_args, init_args, str2bool
 
 
 class UDATrainer(Trainer):
@@ -48,8 +49,15 @@ class UDATrainer(Trainer):
         self.threshold = self.args.threshold
         self.iter_num = 1
         self._reset_meters()
+        self.use_graph = bool(getattr(self.args, "graph", False))
+        self._graphed = None
 
     def _reset_meters(self):
+        # zeroed in place once they exist: a captured step (utils/graph.py) adds into these tensors
+        if getattr(self, "loss_seg_value", None) is not None:
+            for t in (self.loss_seg_value, self.loss_seg_value_2, self.loss_target_value, self.loss_target_value_2):
+                t.zero_()
+            return
         z = lambda: torch.zeros((), device=self.device)  # noqa: E731
         self.loss_seg_value, self.loss_seg_value_2 = z(), z()
         self.loss_target_value, self.loss_target_value_2 = z(), z()
@@ -89,8 +97,18 @@ class UDATrainer(Trainer):
         self.loss_target_value += self.loss_target.detach() / self.iter_num
 
     def uda_step(self, x_s, y_s, x_t):
-        """One iteration of the hot loop (solve_gta5.py:336-383), inputs already on the device."""
+        """One iteration of the hot loop (solve_gta5.py:336-383), inputs already on the device.
+        With use_graph (single process), iterations after the first replay a captured hipGraph."""
         self.poly_lr_scheduler(optimizer=self.optimizer, init_lr=self.args.lr)
+        if self.use_graph and self.reducer is None:
+            if self._graphed is None:
+                self._graphed = GraphedStep(self, self._uda_body)
+            self._graphed(x_s, y_s, x_t)
+        else:
+            self._uda_body(x_s, y_s, x_t)
+        self.current_iter += 1
+
+    def _uda_body(self, x_s, y_s, x_t):
         pred = self.model(x_s)
         self.train_source(pred, y_s)
         pred = self.model(x_t)
@@ -99,7 +117,6 @@ class UDATrainer(Trainer):
             self.reducer.finish()
         self.optimizer.step()
         self.optimizer.zero_grad()
-        self.current_iter += 1
 
     # ---------------------------------------------------------------- loop
     def main(self):
@@ -159,6 +176,9 @@ def add_UDA_train_args(arg_parser):
     a("--IW_ratio", type=float, default=0.2)
     a("--threshold", type=float, default=0.95)
     a("--target_solo_epoch", type=int, default=0)
+    a("--graph", type=str2bool, default=False,
+      help="replay each iteration after the first as one captured hipGraph (single process; not in the "
+           "reference, whose loop is eager)")
     return arg_parser
 
 

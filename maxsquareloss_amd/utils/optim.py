@@ -124,7 +124,9 @@ class SGD:
         self.grads = FlatGrads(uniq, self.device)
         self._table_key = None
         self._table = None
+        self._last_used = None
         self.grad_scale = 1.0
+        self.lr_dev = None  # device float32[2] learning rates (hipGraph replay), else by value
 
     # -- torch.optim.Optimizer surface ------------------------------------------------
     def zero_grad(self, set_to_none=True):
@@ -152,14 +154,27 @@ class SGD:
                 key.append((rows[-1][0], rows[-1][1], rows[-1][2], rows[-1][6]))
         return rows, tuple(key)
 
-    def step(self, closure=None):
-        if closure is not None:
-            raise NotImplementedError("closure")
-        if self.device.type != "cuda":
-            raise hip.MSLError("SGD.step runs on the HIP path only (no CPU fallback)")
+    def prepare(self, used=None):
+        """Build (and upload) the launch table for the given live-parameter mask now, creating the
+        momentum buffers it needs - so a step captured into a hipGraph afterwards finds it ready
+        (no host-to-device copy and no allocation may happen inside the capture).  `used`
+        defaults to the parameters that received gradients in the last step."""
+        if self._last_used is None:
+            raise hip.MSLError("SGD.prepare(): run one step first (its first-step buffer rule, Q2, differs)")
+        saved = self.grads.used.copy()
+        self.grads.used[:] = self._last_used if used is None else used
+        try:
+            self._ensure_table()
+        finally:
+            self.grads.used[:] = saved
+
+    def _ensure_table(self):
         lib = hip.load()
         rows, key = self._build_table()
         if key != self._table_key:
+            if torch.cuda.is_current_stream_capturing():
+                raise hip.MSLError("SGD: the launch table changed inside a hipGraph capture; call "
+                                   "optimizer.prepare() before capturing")
             ent = np.zeros(len(rows), dtype=_ENTRY)
             for j, r in enumerate(rows):
                 ent[j] = (r[0], r[1], r[2], r[3], r[4], r[5], r[6], 0)
@@ -176,20 +191,38 @@ class SGD:
             self._table = (dev, dev.data_ptr(), dev.data_ptr() + n_ent, dev.data_ptr() + n_ent + n_be,
                            int(nblk_each.sum()))
             self._table_key = key
+
+    def step(self, closure=None):
+        if closure is not None:
+            raise NotImplementedError("closure")
+        if self.device.type != "cuda":
+            raise hip.MSLError("SGD.step runs on the HIP path only (no CPU fallback)")
+        lib = hip.load()
+        self._ensure_table()
+        self._last_used = self.grads.used.copy()
         _dev, p_ent, p_be, p_bo, nblocks = self._table
         mom = float(self.defaults["momentum"])
         wd = float(self.defaults["weight_decay"])
-        lr0 = float(self.param_groups[0]["lr"])
-        lr1 = float(self.param_groups[1]["lr"]) if len(self.param_groups) > 1 else lr0
         # momentum == 0: buffers are written but has_buf stays 0, i.e. buf = d, p -= lr*d
-        hip.check(lib.msl_sgd_step(p_ent, p_be, p_bo, nblocks, lr0, lr1, mom, wd, float(self.grad_scale),
-                                   hip.stream_ptr()), "msl_sgd_step")
+        if self.lr_dev is not None:
+            # learning rates from device memory (set between hipGraph replays, utils/graph.py)
+            hip.check(lib.msl_sgd_step_lr_dev(p_ent, p_be, p_bo, nblocks, self.lr_dev.data_ptr(), mom, wd,
+                                              float(self.grad_scale), hip.stream_ptr()), "msl_sgd_step_lr_dev")
+        else:
+            lr0 = float(self.param_groups[0]["lr"])
+            lr1 = float(self.param_groups[1]["lr"]) if len(self.param_groups) > 1 else lr0
+            hip.check(lib.msl_sgd_step(p_ent, p_be, p_bo, nblocks, lr0, lr1, mom, wd, float(self.grad_scale),
+                                       hip.stream_ptr()), "msl_sgd_step")
         # the kernel wrote the parameters behind autograd's back: bump their version counters
         for g in self.param_groups:
             for p, _ in g["_unique"]:
                 if p.requires_grad and self.grads.used[self.grads.index[id(p)]]:
                     torch.autograd.graph.increment_version(p)
         return None
+
+    def group_lrs(self):
+        lr0 = float(self.param_groups[0]["lr"])
+        return lr0, (float(self.param_groups[1]["lr"]) if len(self.param_groups) > 1 else lr0)
 
     # -- checkpoints (train_source.py:662-704 stores optimizer.state_dict()) -----------
     def state_dict(self):

@@ -42,7 +42,7 @@ def _grads(tr, xs, ys, xt):
     return tr.optimizer.grads.flat.detach().cpu().clone()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, outdir):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                           WORLD_SIZE=str(world), LOCAL_RANK="0")
@@ -63,7 +63,8 @@ def _worker(rank, world, port, q):
         xt = synthetic_image(H, W, 500 + seed).cuda()
         _grads(tr, xs, ys, xt)                    # A: learns the live set
         tr.reducer = None
-        local = _grads(tr, xs, ys, xt)            # B: this rank's own gradient
+        local = _grads(tr, xs, ys, xt)            # B: this rank's own gradient ...
+        again = _grads(tr, xs, ys, xt)            # ... twice: the run-to-run noise of the step
         tr.reducer = red
         log = []
         in_finish = [False]
@@ -79,32 +80,46 @@ def _worker(rank, world, port, q):
             in_finish[0] = False
         red._launch, red.finish = launch, finish
         reduced = _grads(tr, xs, ys, xt)          # C: armed, overlapped exchange
-        q.put((rank, local.numpy(), reduced.numpy(), log, red.has_live, red.live.copy(),
-               list(red.bounds), tr.optimizer.grad_scale, tr.optimizer.grads.offsets.copy()))
+        # the gradient buffers go through files: 2 x 174 MB do not belong in a pipe
+        np.save(os.path.join(outdir, f"local{rank}.npy"), local.numpy())
+        np.save(os.path.join(outdir, f"again{rank}.npy"), again.numpy())
+        np.save(os.path.join(outdir, f"reduced{rank}.npy"), reduced.numpy())
+        q.put((rank, "ok", log, red.has_live, red.live.copy(), list(red.bounds), tr.optimizer.grad_scale,
+               tr.optimizer.grads.offsets.copy()))
         dist.destroy_process_group()
     except Exception as e:  # surface the failure to the parent instead of hanging it
         import traceback
         q.put((rank, "error", traceback.format_exc() + repr(e)))
+        raise
 
 
-def test_grad_reducer_real_model_two_ranks():
+def test_grad_reducer_real_model_two_ranks(tmp_path):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, str(tmp_path))) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
-    for _ in range(world):
-        item = q.get(timeout=300)
-        assert item[1] != "error", item[2]
-        got[item[0]] = item[1:]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    expect = got[0][0].astype(np.float64) + got[1][0].astype(np.float64)
+    try:
+        for _ in range(world):
+            item = q.get(timeout=240)
+            assert item[1] == "ok", item[2]
+            got[item[0]] = item[2:]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:  # never leave a rank behind (it would hold the GPU and the test runner)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    local = [np.load(os.path.join(tmp_path, f"local{r}.npy")) for r in range(world)]
+    again = [np.load(os.path.join(tmp_path, f"again{r}.npy")) for r in range(world)]
+    expect = local[0].astype(np.float64) + local[1].astype(np.float64)
     for r in range(world):
-        local, reduced, log, has_live, live, bounds, gscale, offs = got[r]
+        reduced = np.load(os.path.join(tmp_path, f"reduced{r}.npy"))
+        log, has_live, live, bounds, gscale, offs = got[r]
         assert gscale == pytest.approx(1.0 / world)
         # every bucket with a live parameter was launched exactly once, by the countdown during the
         # target backward (before finish()), in bucket order
@@ -112,11 +127,15 @@ def test_grad_reducer_real_model_two_ranks():
         assert launched == [b for b in range(len(bounds)) if has_live[b]], launched
         assert not any(late for _, late in log), log
         assert len(bounds) > 3 and live.sum() > 300
-        # the reduced buffer = rank-sum of the local gradients (the stem conv's MIOpen weight
-        # gradient is not bit-reproducible run to run: compare per bucket, normwise)
+        # the reduced buffer = rank-sum of the local gradients.  The local gradient itself is not
+        # bit-reproducible run to run (MIOpen's stem / stride-2 convs; amplified through the bs=1
+        # network and the thresholded pseudo-label of the multi-level guidance CE), so the bar per
+        # parameter is 1e-5 of its scale plus 4x the measured run-to-run change of the two ranks.
         assert np.abs(expect).max() > 0
         for i in range(len(offs) - 1):
             lo, hi = int(offs[i]), int(offs[i + 1])
-            e, a = expect[lo:hi], reduced[lo:hi].astype(np.float64)
-            assert np.abs(a - e).max() <= 1e-5 * max(np.abs(e).max(), 1e-30), (i, np.abs(a - e).max(), np.abs(e).max())
-        assert np.abs(reduced.astype(np.float64) - expect).max() <= 1e-5 * np.abs(expect).max()
+            e = expect[lo:hi]
+            a = reduced[lo:hi].astype(np.float64)
+            noise = sum(np.abs(again[k][lo:hi].astype(np.float64) - local[k][lo:hi]).max() for k in range(world))
+            tol = 1e-5 * max(np.abs(e).max(), 1e-30) + 4 * noise
+            assert np.abs(a - e).max() <= tol, (i, np.abs(a - e).max(), np.abs(e).max(), noise)

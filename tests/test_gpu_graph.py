@@ -1,0 +1,74 @@
+"""The captured step (utils/graph.py) against the eager step (GPU only).
+
+Two trainers from the same counter-generated init run the same four UDA iterations (IW-MaxSquare
++ multi-level guidance, different images every iteration), one eagerly, one with every iteration
+after the first replayed from a hipGraph.  Same kernels in the same order: losses, histograms,
+meters, parameters, momentum and BN statistics must agree to rounding (the graph replays the
+poly learning rate from device memory and repacks the weights the previous replay updated).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from maxsquareloss_amd.tools.solve_gta5 import UDATrainer, build_parser  # noqa: E402
+from maxsquareloss_amd.tools.train_source import init_args  # noqa: E402
+from maxsquareloss_amd.utils.synthetic import synthetic_image, synthetic_labels  # noqa: E402
+
+H, W = 256, 512
+
+
+def _trainer(graph):
+    argv = ["--crop_size", f"{W},{H}", "--target_crop_size", f"{W},{H}", "--imagenet_pretrained", "False",
+            "--save_dir", "", "--target_mode", "IW_maxsquare", "--multi", "True", "--lambda_target", "0.09",
+            "--iter_max", "1000", "--graph", str(graph)]
+    args, _, _ = init_args(build_parser().parse_args(argv))
+    tr = UDATrainer(args, cuda=True)
+    tr.optimizer.zero_grad()
+    return tr
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def test_graph_replay_matches_eager():
+    eager, graphed = _trainer(False), _trainer(True)
+    assert graphed.use_graph and not eager.use_graph
+    for it in range(4):
+        xs = synthetic_image(H, W, 40 + it).cuda()
+        ys = synthetic_labels(H, W, 19, 40 + it).cuda()
+        xt = synthetic_image(H, W, 540 + it).cuda()
+        for tr in (eager, graphed):
+            tr.uda_step(xs, ys, xt)
+        torch.cuda.synchronize()
+        assert graphed._graphed is not None and graphed._graphed.replays == max(it, 0)
+        for name in ("loss_val", "loss_target", "loss_target_2"):
+            a, b = getattr(graphed, name).item(), getattr(eager, name).item()
+            assert a == pytest.approx(b, rel=1e-5), (it, name, a, b)
+        assert np.array_equal(graphed.target_loss.last_hist.cpu().numpy(), eager.target_loss.last_hist.cpu().numpy())
+    assert graphed.current_iter == eager.current_iter == 4
+    # the poly learning rate moved every iteration (iter_max 1000): replays used the current one
+    assert eager.optimizer.param_groups[0]["lr"] < 2.5e-4
+    for (n, p), (_, q) in zip(graphed.model.named_parameters(), eager.model.named_parameters()):
+        assert _rel(p, q) < 1e-4, n
+    for (n, b), (_, c) in zip(graphed.model.named_buffers(), eager.model.named_buffers()):
+        if b.is_floating_point():
+            assert _rel(b, c) < 1e-4, n
+        else:
+            assert torch.equal(b, c), n
+    for p, q in zip(graphed.optimizer._uniq, eager.optimizer._uniq):
+        sp, sq = graphed.optimizer.state.get(p), eager.optimizer.state.get(q)
+        assert (sp is None) == (sq is None)
+        if sp is not None:
+            assert _rel(sp["momentum_buffer"], sq["momentum_buffer"]) < 1e-4
+    for name in ("loss_seg_value", "loss_target_value", "loss_target_value_2"):
+        assert getattr(graphed, name).item() == pytest.approx(getattr(eager, name).item(), rel=1e-5)
+    # after replays the packed-weight caches are stale for eager code: the version bump repacks
+    x = synthetic_image(H, W, 77).cuda()
+    with torch.no_grad():
+        a2, a1 = graphed.model(x)
+        b2, b1 = eager.model(x)
+    assert _rel(a2, b2) < 1e-3 and _rel(a1, b1) < 1e-3
