@@ -72,10 +72,20 @@ class GraphedStep:
         torch.cuda.current_stream(self.device).wait_stream(s)
         opt.prepare()  # the table of every later step (buffers exist: has_buf = 1)
         opt.lr_dev = self.lr_dev
+        owners = [self.tr] + [m for m in vars(self.tr).values() if isinstance(m, torch.nn.Module)]
+        before = [{k: v for k, v in vars(o).items() if isinstance(v, torch.Tensor)} for o in owners]
         try:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, stream=s):
                 self.body(*self.static)
         finally:
             opt.lr_dev = None  # eager steps outside the graph keep passing the rates by value
+        # the capture rebound the step's outputs (loss scalars, IW histogram, ...) to tensors the
+        # graph writes but has not written yet: give them iteration 0's values
+        with torch.cuda.stream(s):
+            for o, old in zip(owners, before):
+                for k, v in old.items():
+                    new = getattr(o, k, None)
+                    if isinstance(new, torch.Tensor) and new is not v and new.shape == v.shape:
+                        new.copy_(v)
         torch.cuda.current_stream(self.device).wait_stream(s)
