@@ -6,11 +6,15 @@ one device; the reducer code is backend-agnostic).  The HIP ops report their
 weight gradients through ops.grad_sink -> FlatGrads.notify, not AccumulateGrad
 hooks, so this is the test of that path's bucket countdown:
   - iteration A learns the live set (the first finish() reduces everything);
-  - iteration B computes each rank's local gradient with the reducer detached;
-  - iteration C runs armed: every live bucket must be launched by the countdown
-    during the target backward (before finish()), and the reduced flat buffer
-    must equal the sum of the two ranks' local gradients.
-No optimizer step runs between A, B and C, so the three see the same weights.
+  - iteration B runs armed: every live bucket must be launched by the countdown
+    during the target backward (before finish()), only after every live
+    parameter of the bucket has reported its final gradient, in bucket order;
+    the reduced flat buffer must equal the sum over ranks of each bucket's
+    local contents at its launch (stream-ordered snapshots), exactly.
+The local gradients themselves are not compared across separate iterations: two
+processes sharing one GPU make MIOpen's solver timings (hence its choice) vary, and
+the random-init bs=1 network amplifies a last-bit change of its outputs to
+percent-level gradient changes (see tests/test_gpu_parity.py, configs[0]).
 """
 import os
 import socket
@@ -62,30 +66,33 @@ def _worker(rank, world, port, q, outdir):
         ys = synthetic_labels(H, W, 19, seed).cuda()
         xt = synthetic_image(H, W, 500 + seed).cuda()
         _grads(tr, xs, ys, xt)                    # A: learns the live set
-        tr.reducer = None
-        local = _grads(tr, xs, ys, xt)            # B: this rank's own gradient ...
-        again = _grads(tr, xs, ys, xt)            # ... twice: the run-to-run noise of the step
-        tr.reducer = red
-        log = []
-        in_finish = [False]
+        events = []                               # ("notify", param) / ("launch", bucket, snapshot)
+        flat = tr.optimizer.grads
         orig_launch, orig_finish = red._launch, red.finish
+        in_finish = [False]
+
+        def on_grad(i):
+            events.append(("notify", i))
 
         def launch(b):
-            log.append((b, in_finish[0]))
+            a, e = red._elem_range(b)
+            events.append(("launch", b, flat.flat[a:e].clone(), in_finish[0]))  # stream-ordered copy
             orig_launch(b)
 
         def finish():
             in_finish[0] = True
             orig_finish()
             in_finish[0] = False
+        flat.listeners.insert(0, on_grad)
         red._launch, red.finish = launch, finish
-        reduced = _grads(tr, xs, ys, xt)          # C: armed, overlapped exchange
-        # the gradient buffers go through files: 2 x 174 MB do not belong in a pipe
-        np.save(os.path.join(outdir, f"local{rank}.npy"), local.numpy())
-        np.save(os.path.join(outdir, f"again{rank}.npy"), again.numpy())
+        reduced = _grads(tr, xs, ys, xt)          # B: armed, overlapped exchange
+        flat.listeners.remove(on_grad)
+        log = [(ev[0], ev[1], ev[3]) if ev[0] == "launch" else ev for ev in events]
+        snaps = {ev[1]: ev[2].cpu().numpy() for ev in events if ev[0] == "launch"}
         np.save(os.path.join(outdir, f"reduced{rank}.npy"), reduced.numpy())
+        np.savez(os.path.join(outdir, f"snaps{rank}.npz"), **{str(b): v for b, v in snaps.items()})
         q.put((rank, "ok", log, red.has_live, red.live.copy(), list(red.bounds), tr.optimizer.grad_scale,
-               tr.optimizer.grads.offsets.copy()))
+               [red._elem_range(b) for b in range(len(red.bounds))]))
         dist.destroy_process_group()
     except Exception as e:  # surface the failure to the parent instead of hanging it
         import traceback
@@ -114,28 +121,32 @@ def test_grad_reducer_real_model_two_ranks(tmp_path):
             if p.is_alive():
                 p.kill()
                 p.join(timeout=10)
-    local = [np.load(os.path.join(tmp_path, f"local{r}.npy")) for r in range(world)]
-    again = [np.load(os.path.join(tmp_path, f"again{r}.npy")) for r in range(world)]
-    expect = local[0].astype(np.float64) + local[1].astype(np.float64)
+    snaps = [np.load(os.path.join(tmp_path, f"snaps{r}.npz")) for r in range(world)]
     for r in range(world):
         reduced = np.load(os.path.join(tmp_path, f"reduced{r}.npy"))
-        log, has_live, live, bounds, gscale, offs = got[r]
+        log, has_live, live, bounds, gscale, ranges = got[r]
         assert gscale == pytest.approx(1.0 / world)
-        # every bucket with a live parameter was launched exactly once, by the countdown during the
-        # target backward (before finish()), in bucket order
-        launched = [b for b, _ in log]
-        assert launched == [b for b in range(len(bounds)) if has_live[b]], launched
-        assert not any(late for _, late in log), log
         assert len(bounds) > 3 and live.sum() > 300
-        # the reduced buffer = rank-sum of the local gradients.  The local gradient itself is not
-        # bit-reproducible run to run (MIOpen's stem / stride-2 convs; amplified through the bs=1
-        # network and the thresholded pseudo-label of the multi-level guidance CE), so the bar per
-        # parameter is 1e-5 of its scale plus 4x the measured run-to-run change of the two ranks.
-        assert np.abs(expect).max() > 0
-        for i in range(len(offs) - 1):
-            lo, hi = int(offs[i]), int(offs[i + 1])
-            e = expect[lo:hi]
-            a = reduced[lo:hi].astype(np.float64)
-            noise = sum(np.abs(again[k][lo:hi].astype(np.float64) - local[k][lo:hi]).max() for k in range(world))
-            tol = 1e-5 * max(np.abs(e).max(), 1e-30) + 4 * noise
-            assert np.abs(a - e).max() <= tol, (i, np.abs(a - e).max(), np.abs(e).max(), noise)
+        launches = [e for e in log if e[0] == "launch"]
+        # every bucket with a live parameter launched exactly once, in order, by the countdown
+        # during the target backward (not by finish())
+        assert [e[1] for e in launches] == [b for b in range(len(bounds)) if has_live[b]], launches
+        assert not any(e[2] for e in launches), launches
+        # ... and only after every live parameter of the bucket had reported its gradient
+        seen = set()
+        for e in log:
+            if e[0] == "notify":
+                seen.add(e[1])
+            else:
+                lo, hi = bounds[e[1]]
+                missing = [i for i in range(lo, hi) if live[i] and i not in seen]
+                assert not missing, (e[1], missing)
+        # the reduced buffer = the rank-sum of what each rank held when the bucket launched
+        for b in range(len(bounds)):
+            if not has_live[b]:
+                continue
+            a, e = ranges[b]
+            want = snaps[0][str(b)].astype(np.float64) + snaps[1][str(b)].astype(np.float64)
+            got_b = reduced[a:e].astype(np.float64)
+            assert np.array_equal(got_b, want.astype(np.float32).astype(np.float64)), \
+                (b, np.abs(got_b - want).max(), np.abs(want).max())
