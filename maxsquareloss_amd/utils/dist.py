@@ -69,6 +69,7 @@ class GradReducer:
     def prepare_for_backward(self):
         """Call right before the last backward of the iteration."""
         self.works = []
+        self.flat.new_backward()
         if self.live is None:
             self.armed = False
             return

@@ -55,6 +55,8 @@ class FlatGrads:
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
         self.used = np.zeros(len(self.params), dtype=bool)
         self.listeners = []
+        self.gen = 1                                      # backward-pass generation
+        self.seen = np.zeros(len(self.params), dtype=np.int64)
         for i, p in enumerate(self.params):
             p.grad = self.flat[self.offsets[i]:self.offsets[i + 1]].view_as(p)
             p.register_post_accumulate_grad_hook(self._make_hook(i))
@@ -68,10 +70,20 @@ class FlatGrads:
 
     def notify(self, i):
         """Parameter i's gradient for this backward is complete (AccumulateGrad's hook, or a
-        HIP op that accumulated it directly into the flat buffer)."""
+        HIP op that accumulated it directly into the flat buffer).  Listeners hear it once per
+        backward pass: when an op has accumulated in place and returned None for the parameter,
+        autograd still runs the AccumulateGrad node and fires its post-accumulate hook - a second
+        report that would count a bucket down before its other parameters are final."""
         self.used[i] = True
+        if self.seen[i] == self.gen:
+            return
+        self.seen[i] = self.gen
         for fn in self.listeners:
             fn(i)
+
+    def new_backward(self):
+        """The next reports belong to a new backward pass."""
+        self.gen += 1
 
     def view(self, i):
         return self.flat[self.offsets[i]:self.offsets[i + 1]]
@@ -79,6 +91,7 @@ class FlatGrads:
     def zero_(self):
         self.flat.zero_()
         self.used[:] = False
+        self.new_backward()
 
     def reattach(self):
         """Restore the .grad views (e.g. after someone set grads to None)."""

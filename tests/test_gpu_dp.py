@@ -77,22 +77,32 @@ def _worker(rank, world, port, q, outdir):
         def launch(b):
             a, e = red._elem_range(b)
             events.append(("launch", b, flat.flat[a:e].clone(), in_finish[0]))  # stream-ordered copy
+            if os.environ.get("MSL_DP_SYNC_LAUNCH"):
+                torch.cuda.synchronize()  # diagnostic: hand gloo a settled buffer
             orig_launch(b)
 
         def finish():
             in_finish[0] = True
             orig_finish()
             in_finish[0] = False
+        orig_prepare = red.prepare_for_backward
+
+        def prepare():
+            events.append(("arm", -1))
+            orig_prepare()
         flat.listeners.insert(0, on_grad)
-        red._launch, red.finish = launch, finish
+        red._launch, red.finish, red.prepare_for_backward = launch, finish, prepare
         reduced = _grads(tr, xs, ys, xt)          # B: armed, overlapped exchange
         flat.listeners.remove(on_grad)
+        armed_at = next(k for k, ev in enumerate(events) if ev[0] == "arm")
+        events = events[armed_at + 1:]  # the target backward (the source backward is not armed)
         log = [(ev[0], ev[1], ev[3]) if ev[0] == "launch" else ev for ev in events]
         snaps = {ev[1]: ev[2].cpu().numpy() for ev in events if ev[0] == "launch"}
         np.save(os.path.join(outdir, f"reduced{rank}.npy"), reduced.numpy())
         np.savez(os.path.join(outdir, f"snaps{rank}.npz"), **{str(b): v for b, v in snaps.items()})
+        names = [n for n, p in tr.model.named_parameters() if p.requires_grad][::-1]
         q.put((rank, "ok", log, red.has_live, red.live.copy(), list(red.bounds), tr.optimizer.grad_scale,
-               [red._elem_range(b) for b in range(len(red.bounds))]))
+               [red._elem_range(b) for b in range(len(red.bounds))], list(flat.offsets), names))
         dist.destroy_process_group()
     except Exception as e:  # surface the failure to the parent instead of hanging it
         import traceback
@@ -124,7 +134,7 @@ def test_grad_reducer_real_model_two_ranks(tmp_path):
     snaps = [np.load(os.path.join(tmp_path, f"snaps{r}.npz")) for r in range(world)]
     for r in range(world):
         reduced = np.load(os.path.join(tmp_path, f"reduced{r}.npy"))
-        log, has_live, live, bounds, gscale, ranges = got[r]
+        log, has_live, live, bounds, gscale, ranges, offs, names = got[r]
         assert gscale == pytest.approx(1.0 / world)
         assert len(bounds) > 3 and live.sum() > 300
         launches = [e for e in log if e[0] == "launch"]
@@ -132,6 +142,11 @@ def test_grad_reducer_real_model_two_ranks(tmp_path):
         # during the target backward (not by finish())
         assert [e[1] for e in launches] == [b for b in range(len(bounds)) if has_live[b]], launches
         assert not any(e[2] for e in launches), launches
+        # every live parameter reports exactly once in the armed backward
+        from collections import Counter
+        cnt = Counter(e[1] for e in log if e[0] == "notify")
+        assert all(cnt[i] == 1 for i in range(len(live)) if live[i]), \
+            [(names[i], cnt[i]) for i in range(len(live)) if live[i] and cnt[i] != 1][:10]
         # ... and only after every live parameter of the bucket had reported its gradient
         seen = set()
         for e in log:
@@ -148,5 +163,18 @@ def test_grad_reducer_real_model_two_ranks(tmp_path):
             a, e = ranges[b]
             want = snaps[0][str(b)].astype(np.float64) + snaps[1][str(b)].astype(np.float64)
             got_b = reduced[a:e].astype(np.float64)
-            assert np.array_equal(got_b, want.astype(np.float32).astype(np.float64)), \
-                (b, np.abs(got_b - want).max(), np.abs(want).max())
+            want = want.astype(np.float32).astype(np.float64)
+            if not np.array_equal(got_b, want):
+                lo, hi = bounds[b]
+                detail = [(names[i], float(np.abs(got_b[offs[i] - a:offs[i + 1] - a] - want[offs[i] - a:offs[i + 1] - a]).max()),
+                           float(np.abs(want[offs[i] - a:offs[i + 1] - a]).max())) for i in range(lo, hi)]
+                other = np.load(os.path.join(tmp_path, f"reduced{1 - r}.npy"))[a:e].astype(np.float64)
+                i = next(i for i in range(lo, hi) if detail[i - lo][1] > 0)
+                sl = slice(offs[i] - a, offs[i + 1] - a)
+                d = got_b[sl] - want[sl]
+                s0, s1 = snaps[0][str(b)][sl].astype(np.float64), snaps[1][str(b)][sl].astype(np.float64)
+                k = int(np.abs(d).argmax())
+                raise AssertionError((r, b, [x for x in detail if x[1] > 0], "ranks agree:",
+                                      bool(np.array_equal(got_b[sl], other[sl])), "n differing", int((d != 0).sum()),
+                                      "of", d.size, "at argmax: got", got_b[sl][k], "s0", s0[k], "s1", s1[k],
+                                      "other rank", other[sl][k]))

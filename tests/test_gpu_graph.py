@@ -6,8 +6,12 @@ after the first replayed from a hipGraph (the graph replays the poly learning ra
 memory and repacks the weights the previous replay updated).  Iteration 0 is eager in both:
 bit-identical.  The replays run the same HIP kernels, but the library calls on the path (MIOpen's
 stem / stride-2 convs, hipBLASLt) may pick other kernels under capture, and the random-init bs=1
-network amplifies last-bit changes: later iterations are held to the fp32 rounding envelope
-(losses 1e-4, the thresholded pseudo-label CE 1e-3, parameters and statistics 1e-3).
+network amplifies last-bit changes chaotically from one update to the next (tests/test_gpu_parity.py,
+configs[0]).  So before every later iteration the graphed trainer is re-synced in place to the
+eager one (parameters, momentum, BN statistics: the graph reads them where they live), and each
+replayed iteration is held to the rounding envelope of one iteration: losses 1e-4, the
+thresholded pseudo-label CE 1e-3, IW histogram within 0.1 % of the pixels, the resulting update
+1e-3 normwise.
 """
 import numpy as np
 import pytest
@@ -44,10 +48,13 @@ def test_graph_replay_matches_eager():
         xs = synthetic_image(H, W, 40 + it).cuda()
         ys = synthetic_labels(H, W, 19, 40 + it).cuda()
         xt = synthetic_image(H, W, 540 + it).cuda()
+        if it > 0:
+            _resync(graphed, eager)
+        before = [p.detach().clone() for p in eager.model.parameters()]
         for tr in (eager, graphed):
             tr.uda_step(xs, ys, xt)
         torch.cuda.synchronize()
-        assert graphed._graphed is not None and graphed._graphed.replays == max(it, 0)
+        assert graphed._graphed is not None and graphed._graphed.replays == it
         for name, tol in (("loss_val", 1e-4), ("loss_target", 1e-4), ("loss_target_2", 1e-3)):
             a, b = getattr(graphed, name).item(), getattr(eager, name).item()
             if it == 0:
@@ -55,26 +62,32 @@ def test_graph_replay_matches_eager():
             assert a == pytest.approx(b, rel=tol), (it, name, a, b)
         hg, he = graphed.target_loss.last_hist.cpu().numpy(), eager.target_loss.last_hist.cpu().numpy()
         assert np.abs(hg.astype(np.int64) - he).sum() <= (0 if it == 0 else 2 * 0.001 * H * W), (it, hg, he)
+        # the update this iteration made (SGD inside the graph, poly LR from device memory)
+        for (n, p), q, b in zip(graphed.model.named_parameters(), eager.model.parameters(), before):
+            if p.requires_grad:
+                assert _rel(p - b, q - b) < (1e-5 if it == 0 else 1e-3), (it, n)  # MIOpen's stem wgrad: atomics
     assert graphed.current_iter == eager.current_iter == 4
     # the poly learning rate moved every iteration (iter_max 1000): replays used the current one
     assert eager.optimizer.param_groups[0]["lr"] < 2.5e-4
-    for (n, p), (_, q) in zip(graphed.model.named_parameters(), eager.model.named_parameters()):
-        assert _rel(p, q) < 1e-3, n
-    for (n, b), (_, c) in zip(graphed.model.named_buffers(), eager.model.named_buffers()):
-        if b.is_floating_point():
-            assert _rel(b, c) < 1e-3, n
-        else:
-            assert torch.equal(b, c), n
-    for p, q in zip(graphed.optimizer._uniq, eager.optimizer._uniq):
-        sp, sq = graphed.optimizer.state.get(p), eager.optimizer.state.get(q)
-        assert (sp is None) == (sq is None)
-        if sp is not None:
-            assert _rel(sp["momentum_buffer"], sq["momentum_buffer"]) < 1e-2
     for name in ("loss_seg_value", "loss_target_value", "loss_target_value_2"):
         assert getattr(graphed, name).item() == pytest.approx(getattr(eager, name).item(), rel=1e-3)
     # after replays the packed-weight caches are stale for eager code: the version bump repacks
+    _resync(graphed, eager)
     x = synthetic_image(H, W, 77).cuda()
     with torch.no_grad():
         a2, a1 = graphed.model(x)
         b2, b1 = eager.model(x)
     assert _rel(a2, b2) < 1e-3 and _rel(a1, b1) < 1e-3
+
+
+def _resync(dst, src):
+    """Copy src's parameters, BN buffers and momentum buffers into dst's tensors, in place."""
+    with torch.no_grad():
+        for p, q in zip(dst.model.parameters(), src.model.parameters()):
+            p.copy_(q)
+        for b, c in zip(dst.model.buffers(), src.model.buffers()):
+            b.copy_(c)
+        for p, q in zip(dst.optimizer._uniq, src.optimizer._uniq):
+            sp, sq = dst.optimizer.state.get(p), src.optimizer.state.get(q)
+            if sp is not None and sq is not None:
+                sp["momentum_buffer"].copy_(sq["momentum_buffer"])

@@ -155,27 +155,64 @@ def _free_port():
         return s.getsockname()[1]
 
 
+class _SinkLinear(torch.autograd.Function):
+    """y = x W^T whose backward accumulates dW in place into the flat gradient buffer and returns
+    None for W, as the HIP ops do (ops.grad_sink): autograd then still fires W's
+    post-accumulate hook, a second report the reducer must not count."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, gy):
+        from maxsquareloss_amd import ops
+        x, w = ctx.saved_tensors
+        sink = ops.grad_sink(w)
+        if sink is None:
+            return gy @ w, gy.t() @ x
+        sink[0].add_(gy.t() @ x)
+        sink[1].notify(sink[2])
+        return gy @ w, None
+
+
+class _SinkNet(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.l0 = torch.nn.Linear(8, 16)
+        self.l1 = torch.nn.Linear(16, 16, bias=False)  # weight gradient through the sink
+        self.l2 = torch.nn.Linear(16, 4)
+        self.l3 = torch.nn.Linear(4, 4)  # never used: a "dead" parameter
+
+    def forward(self, x):
+        return self.l2(torch.relu(_SinkLinear.apply(torch.relu(self.l0(x)), self.l1.weight)))
+
+
 def _dp_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     from maxsquareloss_amd.utils.dist import GradReducer
     from maxsquareloss_amd.utils.optim import SGD
-    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4),
-                              torch.nn.Linear(4, 4))  # the last layer is never used: a "dead" param
-    dead = net[3]
+    net = _SinkNet()
+    dead = net.l3
     plist = [p for p in net.parameters()]
     opt = SGD([{"params": plist[:2] + plist[:2], "lr": 0.1}, {"params": plist[2:], "lr": 1.0}],
               lr=0.1, momentum=0.9, weight_decay=5e-4)
     red = GradReducer(opt, bucket_cap_mb=0.0002)  # ~50 floats per bucket -> several buckets
+    reports = []
+    opt.grads.listeners.insert(0, lambda i: reports.append(i))
     results = []
     for it in range(3):
         opt.zero_grad()
         g = torch.Generator().manual_seed(100 * it + rank)
         x1, x2 = torch.randn(5, 8, generator=g), torch.randn(3, 8, generator=g)
-        net[2](net[1](net[0](x1))).pow(2).sum().backward()      # "source" backward: local only
+        net(x1).pow(2).sum().backward()      # "source" backward: local only
         red.prepare_for_backward()
-        net[2](net[1](net[0](x2))).sum().backward()             # "target" backward: overlapped reduce
+        reports.clear()
+        net(x2).sum().backward()             # "target" backward: overlapped reduce
+        assert sorted(reports) == sorted(set(reports)), reports  # one report per parameter
         red.finish()
         results.append([p.grad.detach().numpy().copy() for p in plist] + [opt.grads.used.copy()])
         assert dead.weight.grad.abs().sum() == 0
@@ -196,7 +233,7 @@ def test_grad_reducer_two_ranks_gloo():
         assert p.exitcode == 0
     # expected: the rank-sum of each rank's own (source + target) gradients
     torch.manual_seed(0)
-    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4), torch.nn.Linear(4, 4))
+    net = _SinkNet()
     plist = list(net.parameters())
     for it in range(3):
         total = [torch.zeros_like(p) for p in plist]
@@ -204,8 +241,8 @@ def test_grad_reducer_two_ranks_gloo():
             net.zero_grad()
             g = torch.Generator().manual_seed(100 * it + r)
             x1, x2 = torch.randn(5, 8, generator=g), torch.randn(3, 8, generator=g)
-            net[2](net[1](net[0](x1))).pow(2).sum().backward()
-            net[2](net[1](net[0](x2))).sum().backward()
+            net(x1).pow(2).sum().backward()
+            net(x2).sum().backward()
             for t, p in zip(total, plist):
                 if p.grad is not None:
                     t += p.grad
@@ -216,4 +253,4 @@ def test_grad_reducer_two_ranks_gloo():
     for r in range(world):
         assert got[r][2] == pytest.approx(1.0 / world)
         live = got[r][1]
-        assert live.sum() == 4  # the 2 Linear layers in use (weight, bias each); dead layer excluded
+        assert live.sum() == 5  # l0 (w, b), l1 (w, through the sink), l2 (w, b); the dead l3 excluded
