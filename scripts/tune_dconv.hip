@@ -78,14 +78,15 @@ float run_fwd_dma(const Shape& sh, const float* x, const float* wp, float* y, fl
   return ms / iters;
 }
 
-template <int BM, int BN, int G, int STAGES, int WM, int WN, int MT = 0>
+template <int BM, int BN, int G, int STAGES, int WM, int WN, int MT = 0, bool PW = false>
 float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda, int* flags) {
   const int P = sh.h * sh.w;
+  const int taps = PW ? 1 : 9;
   FwdArgs a;
   a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
-  a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
-  a.ksteps = a.ncb * 9; a.kps = a.ksteps; a.slab = 0; a.taps = 9;
+  a.ncb = (sh.cin + 15) / 16; a.dil0 = PW ? 0 : sh.dil; a.dil1 = 0;
+  a.ksteps = a.ncb * taps; a.kps = a.ksteps; a.slab = 0; a.taps = taps;
   SkArgs sk;
   sk.part = ws; sk.flags = flags;
   sk.tiles_m = (sh.cout + BM - 1) / BM; sk.tiles_n = (P + BN - 1) / BN; sk.KS = a.ksteps / G; sk.NW = NW;
@@ -95,17 +96,17 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   CK(hipMemset(flags, 0, 1 << 20));
+  if (MT == kMathX6P || MT == kMathX6PP) {  // the weight planes are split at pack time (once per SGD step)
+    a.Ax6 = ws + (size_t)NW * 2 * BM * BN;
+    hipLaunchKernelGGL(k_split_pack, dim3(2048), dim3(256), 0, 0, wp, a.ksteps, lda, (__bf16*)a.Ax6);
+  }
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    if (MT == kMathX6P || MT == kMathX6PP) {  // the splits are part of every call
-      a.Ax6 = ws + (size_t)NW * 2 * BM * BN;
-      hipLaunchKernelGGL(k_split_pack, dim3(2048), dim3(256), 0, 0, wp, a.ksteps, lda, (__bf16*)a.Ax6);
-    }
     if (MT == kMathX6PP) {
       a.Bx6 = ws + (size_t)NW * 2 * BM * BN + (size_t)a.ksteps * 6 * lda * 4;
       hipLaunchKernelGGL(k_split_act, dim3(2048), dim3(256), 0, 0, x, a.cimg, a.ncb, P, (__bf16*)a.Bx6);
     }
-    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, WM, WN, false, MT>), dim3(NW), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, BN, G, STAGES, WM, WN, PW, MT>), dim3(NW), dim3(256), 0, 0, a, sk);
     hipLaunchKernelGGL((k_sk_reduce<BM, BN>), dim3(BM * BN / 1024, tiles), dim3(256), 0, 0, a, sk);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
@@ -113,6 +114,36 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   std::vector<int> fl(tiles);
   CK(hipMemcpy(fl.data(), flags, tiles * 4, hipMemcpyDeviceToHost));
   for (int i = 0; i < tiles; ++i) if (fl[i]) { printf("COUNTER NOT RE-ARMED tile %d\n", i); break; }
+  return ms / iters;
+}
+
+template <bool PW>
+float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda) {
+  const int P = sh.h * sh.w;
+  const int taps = PW ? 1 : 9;
+  FwdArgs a;
+  a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
+  a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
+  a.ncb = (sh.cin + 15) / 16; a.dil0 = PW ? 0 : sh.dil; a.dil1 = 0;
+  a.ksteps = a.ncb * taps; a.kps = a.ksteps; a.slab = 0; a.taps = taps;
+  SkArgs sk;
+  sk.part = ws; sk.flags = nullptr;
+  sk.tiles_m = (sh.cout + 127) / 128; sk.tiles_n = (P + 127) / 128; sk.KS = a.ksteps;
+  sk.T = sk.tiles_m * sk.tiles_n * sk.KS;
+  sk.NW = std::min(NW, sk.T);
+  if (sk.T / sk.NW > 2 * sk.KS) { printf("NW too small\n"); return 1e9f; }
+  const int tiles = sk.tiles_m * sk.tiles_n;
+  a.Ax6 = ws + (size_t)NW * 2 * 128 * 128;
+  hipLaunchKernelGGL(k_split_pack, dim3(2048), dim3(256), 0, 0, wp, a.ksteps, lda, (__bf16*)a.Ax6);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) CK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k_x6_sk, dim3(sk.NW), dim3(256), 0, 0, a, sk);
+    hipLaunchKernelGGL((k_sk_reduce<128, 128>), dim3(128 * 128 / 1024, tiles), dim3(256), 0, 0, a, sk);
+  }
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
   return ms / iters;
 }
 
@@ -200,7 +231,7 @@ static unsigned lcg(unsigned& s) { s = s * 1664525u + 1013904223u; return s >> 8
 // row k = (tap * ncb + ci / 16) * 16 + ci % 16, column cout, stride lda.  Error relative to the
 // sum of |terms| of that output.
 static void err64_fwd(const Shape& sh, const std::vector<float>& hx, const std::vector<float>& hw, int lda,
-                      const float* dev, double* mx, double* rms) {
+                      const float* dev, double* mx, double* rms, int taps = 9) {
   const int P = sh.h * sh.w, ncb = (sh.cin + 15) / 16;
   std::vector<float> hy((size_t)sh.cout * P);
   CK(hipMemcpy(hy.data(), dev, hy.size() * 4, hipMemcpyDeviceToHost));
@@ -211,8 +242,8 @@ static void err64_fwd(const Shape& sh, const std::vector<float>& hx, const std::
     const int co = lcg(s) % sh.cout, p = lcg(s) % P;
     const int py = p / sh.w, px = p % sh.w;
     double acc = 0, mag = 0;
-    for (int t = 0; t < 9; ++t) {
-      const int yy = py + (t / 3 - 1) * sh.dil, xx = px + (t % 3 - 1) * sh.dil;
+    for (int t = 0; t < taps; ++t) {
+      const int yy = taps == 1 ? py : py + (t / 3 - 1) * sh.dil, xx = taps == 1 ? px : px + (t % 3 - 1) * sh.dil;
       if (yy < 0 || yy >= sh.h || xx < 0 || xx >= sh.w) continue;
       for (int ci = 0; ci < sh.cin; ++ci) {
         const double v = (double)hw[((size_t)(t * ncb + ci / 16) * 16 + ci % 16) * lda + co] *
@@ -269,14 +300,27 @@ int main(int argc, char** argv) {
   const bool x6_mode = argc > 1 && std::string(argv[1]) == "x6";
   // "rg": the row-grouped forward kernel (k_conv_rg) vs the stream-K one, every form, vs fp64
   const bool rg_mode = argc > 1 && std::string(argv[1]) == "rg";
+  // "big": 256-row x6 tiles (wave tile 128x64) vs the 128-row ones, vs fp64
+  const bool big_mode = argc > 1 && std::string(argv[1]) == "big";
+  // "pw": the pointwise (1x1) GEMMs of layer3 / layer4, x6 forms, vs fp64
+  const bool pw_mode = argc > 1 && std::string(argv[1]) == "pw";
+  // "reg": the register-staged x6 kernel (k_x6_sk) vs the LDS-DMA x6p one, 3x3 and pointwise
+  const bool reg3 = argc > 1 && std::string(argv[1]) == "reg3";  // profiling: layer3 shape only
+  const bool reg_mode = (argc > 1 && std::string(argv[1]) == "reg") || reg3;
   const int iters = sk_only ? 5 : 20;
   std::vector<Shape> shapes = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
   if (wsks) shapes = {{128, 128, 65, 129, 1}, {64, 64, 129, 257, 1}};
+  if (pw_mode) shapes = {{1024, 256, 65, 129, 0}, {256, 1024, 65, 129, 0}, {2048, 512, 65, 129, 0}, {512, 2048, 65, 129, 0}};
+  if (reg_mode) shapes = {{256, 256, 65, 129, 2}, {512, 512, 65, 129, 4}, {1024, 256, 65, 129, 0}, {256, 1024, 65, 129, 0},
+                          {2048, 512, 65, 129, 0}};
+  if (reg3) shapes = {{256, 256, 65, 129, 2}};
+  const bool pwx = pw_mode || reg_mode;
   for (const Shape& sh : shapes) {
-    if ((x6_mode || rg_mode) && (sh.cin != sh.cout || sh.h != 65)) continue;  // the model's layer3 / layer4 shapes
+    if ((x6_mode || rg_mode || big_mode) && (sh.cin != sh.cout || sh.h != 65)) continue;  // layer3 / layer4 shapes
     const int P = sh.h * sh.w;
-    const int lda = (sh.cout + 127) / 128 * 128;
-    const long long kp = (long long)((sh.cin + 15) / 16) * 9 * 16;
+    const int lda = (sh.cout + 255) / 256 * 256;
+    const bool shape_pw = pwx && sh.dil == 0;
+    const long long kp = (long long)((sh.cin + 15) / 16) * (shape_pw ? 1 : 9) * 16;
     std::vector<float> hx((size_t)sh.cin * P), hw((size_t)kp * lda), hdy((size_t)sh.cout * P);
     fill(hx, 1, 2.f); fill(hw, 2, 0.02f); fill(hdy, 3, 2.f);
     float *x, *wp, *dy, *y, *yref, *ws, *dw, *dwref;
@@ -288,8 +332,37 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(wp, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dy, hdy.data(), hdy.size() * 4, hipMemcpyHostToDevice));
-    const double gf = 2.0 * sh.cin * sh.cout * 9 * P / 1e9;
+    const double gf = 2.0 * sh.cin * sh.cout * (shape_pw ? 1 : 9) * P / 1e9;
     printf("=== shape cin %d cout %d %dx%d d=%d : %.2f GFLOP per conv\n", sh.cin, sh.cout, sh.h, sh.w, sh.dil, gf);
+    if (reg_mode) {
+      double mx, rms;
+#define REG(PW, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_x6reg<PW>(sh, x, wp, y, ws, NW, iters, lda); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
+      printf("reg  PW %d       NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, NW, ms * 1e3, gf / ms, mx, rms); }
+#define OLD(PW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_fwd_sk<128, 128, 1, 4, 2, 2, 3, PW>(sh, x, wp, y, ws, 512, iters, lda, flags); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
+      printf("x6p  PW %d ST 4  NW  512 : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, ms * 1e3, gf / ms, mx, rms); }
+      if (reg3) {
+        OLD(false) REG(false, 512)
+      } else if (shape_pw) {
+        OLD(true) REG(true, 512) REG(true, 384) REG(true, 256)
+      } else {
+        OLD(false) REG(false, 512) REG(false, 384) REG(false, 256)
+      }
+      continue;
+    }
+    if (pw_mode) {
+      double mx, rms;  // (no taps=9 reference launch in this mode: the weights are 1x1-sized)
+#define FSKP(BM, BN, G, ST, WM, WN, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_fwd_sk<BM, BN, G, ST, WM, WN, MT, true>(sh, x, wp, y, ws, NW, iters, lda, flags); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms, 1); \
+      printf("pw   MT %d BM %3d BN %3d G %d ST %d NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, BN, G, ST, NW, ms * 1e3, gf / ms, mx, rms); }
+      FSKP(128, 128, 1, 4, 2, 2, 512, 3)
+      if (sh.cout >= 256) { FSKP(256, 128, 1, 3, 2, 2, 256, 3) FSKP(256, 128, 1, 4, 2, 2, 256, 3) FSKP(256, 128, 2, 2, 2, 2, 256, 3) }
+      continue;
+    }
     double sc;
 #define FWD(BM, BN, BK, WM, WN, S) { float ms = run_fwd<BM, BN, BK, WM, WN>(sh, x, wp, y, ws, S, iters, lda); \
       double md = maxdiff(y, yref, (size_t)sh.cout * P, &sc); \
@@ -326,6 +399,17 @@ int main(int argc, char** argv) {
       RGE(128, 512, 0) RGE(128, 256, 0) RGE(128, 512, 2) RGE(128, 256, 2) RGE(128, 512, 1) RGE(64, 768, 0) RGE(64, 512, 2)
       continue;
     }
+    if (big_mode) {
+      double mx, rms;
+#define FSKB(BM, BN, G, ST, WM, WN, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_fwd_sk<BM, BN, G, ST, WM, WN, MT>(sh, x, wp, y, ws, NW, iters, lda, flags); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms); \
+      printf("fsk  MT %d BM %3d BN %3d G %d ST %d NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, BN, G, ST, NW, ms * 1e3, gf / ms, mx, rms); }
+      FSKB(128, 128, 1, 4, 2, 2, 512, 3)
+      FSKB(256, 128, 1, 3, 2, 2, 256, 3) FSKB(256, 128, 1, 4, 2, 2, 256, 3) FSKB(256, 128, 1, 2, 2, 2, 256, 3)
+      FSKB(256, 128, 1, 3, 2, 2, 512, 3) FSKB(256, 128, 2, 2, 2, 2, 256, 3)
+      continue;
+    }
     if (x6_mode) {
       double mx, rms;
 #define FSKE(BM, BN, G, ST, WM, WN, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
@@ -335,12 +419,19 @@ int main(int argc, char** argv) {
 #define WSKE(BM, BN, ST, NW, MT) { float ms = run_wgrad_sk<BM, BN, ST, MT>(sh, x, dy, dw, ws, NW, iters); \
       err64_wgrad(sh, hx, hdy, dw, &mx, &rms); \
       printf("wsk  MT %d BM %3d BN %3d ST %d NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, BN, ST, NW, ms * 1e3, gf / ms, mx, rms); }
-      FSKE(128, 128, 2, 2, 2, 2, 512, 0) FSKE(128, 128, 2, 2, 2, 2, 512, 1) FSKE(128, 128, 2, 2, 2, 2, 512, 2)
-      FSKE(128, 128, 2, 2, 2, 2, 256, 2) FSKE(128, 128, 1, 3, 2, 2, 512, 2) FSKE(128, 128, 2, 3, 2, 2, 256, 2)
-      FSKE(128, 128, 4, 2, 2, 2, 256, 2) FSKE(64, 128, 2, 2, 2, 2, 768, 2)
-      FSKE(128, 128, 1, 4, 2, 2, 512, 3) FSKE(128, 128, 1, 5, 2, 2, 256, 3) FSKE(128, 128, 1, 6, 2, 2, 256, 3)
-      FSKE(128, 128, 1, 7, 2, 2, 256, 3) FSKE(128, 128, 2, 4, 2, 2, 256, 3) FSKE(128, 128, 1, 3, 2, 2, 512, 4)
-      FSKE(128, 128, 1, 5, 2, 2, 256, 4)
+      {  // the per-call activation split of the x6pp rows, alone
+        __bf16* planes = (__bf16*)(ws + (size_t)32 * 1024 * 1024);  // 128 MB in: ws is >= 268 MB
+        hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+        for (int it = -2; it < iters; ++it) {
+          if (it == 0) CK(hipEventRecord(e0));
+          hipLaunchKernelGGL(k_split_act, dim3(2048), dim3(256), 0, 0, x, sh.cin, (sh.cin + 15) / 16, P, planes);
+        }
+        CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("k_split_act alone: %.1f us\n", ms * 1e3 / iters);
+      }
+      FSKE(128, 128, 1, 4, 2, 2, 512, 3) FSKE(128, 128, 1, 3, 2, 2, 512, 4) FSKE(128, 128, 1, 4, 2, 2, 512, 4)
+      FSKE(128, 128, 1, 5, 2, 2, 256, 4) FSKE(128, 128, 2, 2, 2, 2, 512, 4) FSKE(128, 128, 2, 3, 2, 2, 256, 4)
       WSKE(64, 64, 2, 512, 0) WSKE(64, 64, 2, 512, 1) WSKE(64, 64, 2, 512, 2)
       WSKE(128, 128, 2, 256, 0) WSKE(128, 128, 2, 256, 2) WSKE(64, 128, 2, 512, 2)
       continue;
