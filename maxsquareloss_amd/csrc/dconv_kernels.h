@@ -1508,204 +1508,3 @@ __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
 }
 
 }  // namespace msl
-
-namespace msl {
-
-// ---------------------------------------------------------------------------------------------
-// Register-staged bf16x6 stream-K forward form (fwd / dgrad of the dilated 3x3 convs and the
-// pointwise convs, 128x128 tiles, 4 waves of 64x64).  k_igemm_fwd_sk<.., kMathX6P> moves its B
-// operand (fp32 image rows, one shifted pixel per lane) by LDS-DMA - one dword per lane, 8 of those
-// ~60-cycle issues per wave and stage beside 3 for A - and every wave then splits the fp32 values
-// of its own B fragments into bf16 planes, so each B element is split by both waves that share its
-// pixel columns.  Here the operands go through registers instead:
-//   - each thread loads one pixel x 8 channels of the stage's B tile (eight coalesced dword buffer
-//     loads; out-of-image / padding channels come back 0 from the buffer unit), splits them once
-//     into the three bf16 planes and writes three 16-B vectors, and loads three 16-B vectors of the
-//     pre-split A planes (k_pack_split layout) and writes them;
-//   - LDS holds both operands as [plane][k half][128][8] bf16, so every fragment is one
-//     conflict-free ds_read_b128 per plane and the MFMA loop has no split work left;
-//   - stage s+1 is loaded into registers before the MFMAs of stage s and written after them
-//     (issue early / write late), double-buffered LDS, one barrier per stage.
-// Same iteration space, pieces, reduce (k_sk_reduce<128, 128>) and results as the DMA kernel.
-__global__ void __launch_bounds__(256, 2) k_x6_sk(FwdArgs a, SkArgs sk) {
-  constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
-  constexpr int VEC = 6 * 128;                   // 16-B vectors per operand per stage
-  constexpr int STAGE = 2 * VEC;                 // A then B
-  __shared__ __attribute__((aligned(16))) bf16x8 smem[2 * STAGE];  // 48 KB: the only LDS object
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
-  const int l32 = lane & 31, kh = lane >> 5;
-  const int nb = gridDim.x, b = blockIdx.x;
-  const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);  // XCD-aware worker id
-  const int T = sk.T;
-  const int it_begin = sk_start(w, T, sk.NW), it_end = sk_start(w + 1, T, sk.NW);
-
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * 6 * a.lda * 16), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
-  constexpr unsigned OOB = 0x80000000u;
-  const unsigned chan_bytes = (unsigned)a.P * 4u;
-  const int bn = tid & 127, bh = tid >> 7;  // this thread's B pixel column and channel half
-
-  f32x16 acc[TM][TN];
-  for (int it = it_begin; it < it_end;) {
-    const int t = (unsigned)it / (unsigned)sk.KS;
-    const int k_a = it - t * sk.KS;
-    const int k_b = min(sk.KS, k_a + (it_end - it));
-    const int nst = k_b - k_a;
-    it += nst;
-    const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int p = n0 + bn;
-    const bool pin = p < a.P;
-    const int py = p / a.W, px = p - py * a.W;
-    // K cursor: ks = (branch*taps + tap)*ncb + cb; the shifted pixel offset changes with the tap
-    int c_cb, c_tap, ks = k_a;
-    {
-      const int tq = k_a / a.ncb;
-      c_cb = k_a - tq * a.ncb;
-      c_tap = tq;
-    }
-    unsigned vrow = OOB;
-    auto set_tap = [&](int tq) {
-      const int br = tq / a.taps;
-      const int tp = tq - br * a.taps;
-      const int d = br ? a.dil1 : a.dil0;
-      const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
-      const bool v = pin && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
-      vrow = v ? (unsigned)((p + dh * a.W + dw) * 4) : OOB;
-    };
-    set_tap(c_tap);
-    u32x4 ra[3];
-    float rbv[8];
-    // per-thread parts of the load offsets (VGPRs, fixed for the segment); the K-step, plane and
-    // channel parts go in the scalar offset, so a stage's loads cost no vector ALU work
-    const unsigned a_voff = (unsigned)((((tid >> 7) * a.lda) + m0 + (tid & 127)) * 16);
-    const unsigned a_plane_bytes = (unsigned)a.lda * 16u;
-    const bool full_cb = (a.cimg & (kCB - 1)) == 0;  // no padding channel in any block
-    auto load = [&]() {  // the operands of K-step ks into registers; advances the cursor
-#pragma unroll
-      for (int i = 0; i < 3; ++i)  // vectors tid + 256 i: (plane*2 + half) = tid/128 + 2i, m = tid % 128
-        ra[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, a_voff, (int)((unsigned)(ks * 6 + 2 * i) * a_plane_bytes), 0);
-      const int c0 = c_cb * kCB + 8 * bh;
-      if (full_cb) {
-        const unsigned vb = vrow + (unsigned)c0 * chan_bytes;  // OOB stays out of range
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          rbv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vb, (int)(j * chan_bytes), 0));
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const unsigned cofs = c0 + j < a.cimg ? (unsigned)(c0 + j) * chan_bytes : OOB;
-          rbv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vrow + cofs, 0, 0));
-        }
-      }
-      ++ks;
-      if (++c_cb == a.ncb) {
-        c_cb = 0;
-        if (++c_tap * a.ncb < a.ksteps) set_tap(c_tap);
-      }
-    };
-    auto store = [&](int buf) {  // split B once, write both operands' planes
-      bf16x8* As = smem + buf * STAGE;
-      bf16x8* Bs = As + VEC;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        union { u32x4 u; bf16x8 h; } cv;
-        cv.u = ra[i];
-        As[tid + 256 * i] = cv.h;
-      }
-      Split3 sp;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) split3_set(sp, j, rbv[j]);
-      Bs[bh * 128 + bn] = sp.hi;
-      Bs[(2 + bh) * 128 + bn] = sp.mid;
-      Bs[(4 + bh) * 128 + bn] = sp.lo;
-    };
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    __syncthreads();  // the previous segment's LDS reads are complete in every wave
-    load();
-    store(0);
-    __syncthreads();
-    for (int i = 0; i < nst; ++i) {
-      const bool more = i + 1 < nst;
-      if (more) load();  // stage i+1: in flight during this stage's MFMAs
-      const bf16x8* As = smem + (i & 1) * STAGE;
-      const bf16x8* Bs = As + VEC;
-      Split3 av[TM], bv[TN];
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii) {
-        const int m = wm + ii * 32 + l32;
-        av[ii].hi = As[kh * 128 + m];
-        av[ii].mid = As[(2 + kh) * 128 + m];
-        av[ii].lo = As[(4 + kh) * 128 + m];
-      }
-#pragma unroll
-      for (int jj = 0; jj < TN; ++jj) {
-        const int n = wn + jj * 32 + l32;
-        bv[jj].hi = Bs[kh * 128 + n];
-        bv[jj].mid = Bs[(2 + kh) * 128 + n];
-        bv[jj].lo = Bs[(4 + kh) * 128 + n];
-      }
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < TN; ++jj) acc[ii][jj] = mfma_x6(av[ii], bv[jj], acc[ii][jj]);
-      if (more) store((i + 1) & 1);
-      __syncthreads();
-    }
-
-    constexpr int PSZ = BM * BN;
-    if (k_a > 0 || k_b < sk.KS) {  // a piece of a split tile (as k_igemm_fwd_sk)
-      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)sk.part, (short)0, (int)min(0x7fffffffLL, (long long)sk.NW * 2 * PSZ * 4), 0x00020000);
-      const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int nl = wn + j * 32 + l32;
-          const int ml = wm + i * 32 + 4 * kh;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ro = (r & 3) + 8 * (r >> 2);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rp,
-                                                  pbase + (unsigned)(((ml + ro) * BN + nl) * 4), 0, 0);
-          }
-        }
-      continue;
-    }
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn + j * 32 + l32;
-        const int mrow = m0 + wm + i * 32 + 4 * kh;
-        const unsigned voff = n < a.P ? (unsigned)((mrow * a.P + n) * 4) : OOB;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ro = (r & 3) + 8 * (r >> 2);
-          float v = acc[i][j][r];
-          if (a.bias && mrow + ro < a.M) {
-            float bsum = a.bias[mrow + ro];
-            for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + mrow + ro];
-            v += bsum;
-          }
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
-                                                mrow + ro < a.M ? voff + ro * a.P * 4 : OOB, 0, 0);
-        }
-      }
-  }
-}
-
-}  // namespace msl

@@ -44,11 +44,10 @@ class DilatedConv3x3(nn.Conv2d):
         return ops.dconv3x3(x, self.weight, self.dilation[0], self._pack)
 
 
-# The HIP pointwise GEMMs run at 45-90 TFLOP/s on these shapes; the library FP32 GEMMs reach
-# 85-145 on most of them (scripts/bench_pconv.py, scripts/bench_mm.py, profiles/).  By default
-# a stride-1 1x1 conv therefore runs each of its three GEMMs on the fastest library
-# (ops.conv1x1); USE_HIP_POINTWISE switches all three to the HIP kernels (parity-tested), and
-# so does the bf16 conv math (ops.set_conv_math), which has no library form here.
+# By default a stride-1 1x1 conv runs each of its three GEMMs on whichever of the HIP bf16x6
+# pointwise kernels, MIOpen and hipBLASLt is fastest for that shape on MI355X (ops.conv1x1_plan,
+# profiles/r02_conv1x1_dispatch.txt); USE_HIP_POINTWISE switches all three to the HIP kernels
+# (parity-tested), and so does the bf16 conv math (ops.set_conv_math), which has no library form.
 USE_HIP_POINTWISE = False
 
 

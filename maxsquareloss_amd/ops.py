@@ -282,27 +282,74 @@ def pconv(x, weight, cache):
     return _PConv.apply(x, weight, cache)
 
 
-# --------------------------------------------------------------------------- 1x1 conv, library GEMMs
+# --------------------------------------------------------------------------- 1x1 conv, per-GEMM dispatch
+def conv1x1_plan(cin, cout, p, form="bf16x6"):
+    """Implementation of each of the three GEMMs of a stride-1 1x1 conv: (fwd, dgrad, wgrad), each
+    "hip" (the bf16x6 pointwise kernels, fp32 form bf16x6 only), "miopen" or "hipblaslt".
+
+    Per-GEMM winners of every 1x1 shape the UDA step runs, timed on MI355X in isolation
+    (scripts/bench_conv1x1_dispatch.py, profiles/r02_conv1x1_dispatch.txt), as rules:
+      fwd    HIP on the 33k-px layer1 maps with 64 outputs, and at <= 16k px when cin >= 512 and
+             one side is >= 1024 channels (layer3/4 conv1/conv3/downsample); MIOpen elsewhere;
+      dgrad  HIP at <= 16k px when one side is >= 1024 and both >= 256, except the narrowing
+             1024 -> 256 (MIOpen wins there); else hipBLASLt when cout > cin or at 33k px, else MIOpen;
+      wgrad  HIP at 33k px, hipBLASLt addmm elsewhere.
+    """
+    x6 = form == "bf16x6"
+    big = p > 16384
+    fwd = "hip" if x6 and ((big and cout <= 64) or (not big and cin >= 512 and max(cin, cout) >= 1024)) \
+        else "miopen"
+    if x6 and not big and max(cin, cout) >= 1024 and min(cin, cout) >= 256 and not (cin > cout and cout < 512):
+        dgrad = "hip"
+    elif cout > cin or big:
+        dgrad = "hipblaslt"
+    else:
+        dgrad = "miopen"
+    wgrad = "hip" if big else "hipblaslt"
+    return fwd, dgrad, wgrad
+
+
+_PLANS = {}
+
+
 class _Conv1x1(Function):
-    """1x1, stride-1, bias-free conv as three plain GEMMs, each on the library that is fastest for
-    it on MI355X (scripts/bench_mm.py, profiles/r01_gemm_libraries.txt):
-      y  = W x        MIOpen (rocBLAS kernels)
-      dx = W^T dy     the HIP bf16x6 pointwise dgrad when cout > cin >= 128 at <= 16k pixels
-                      (that form only), else hipBLASLt (torch.mm) when cout > cin, else MIOpen
-      dW += dy x^T    hipBLASLt addmm straight into the flat gradient buffer (beta = 1), or the
-                      HIP pointwise wgrad at the 33k-pixel layer1 maps where it is the fastest.
+    """1x1, stride-1, bias-free conv as three GEMMs, each on the implementation conv1x1_plan picks:
+      y  = W x        HIP x6 pointwise fwd or MIOpen
+      dx = W^T dy     HIP x6 pointwise dgrad, hipBLASLt (torch.mm) or MIOpen
+      dW += dy x^T    HIP pointwise wgrad or hipBLASLt addmm, straight into the flat gradient
+                      buffer (beta = 1) when the parameter has a sink
     """
 
     @staticmethod
     def forward(ctx, x, weight, cache):
-        y = F.conv2d(x, weight)
+        cout, cin = weight.shape[0], weight.shape[1]
+        h, w = x.shape[2], x.shape[3]
+        p = h * w
+        form = f32_form()
+        key = (cin, cout, p, form)
+        plan = _PLANS.get(key)
+        if plan is None:
+            plan = _PLANS[key] = conv1x1_plan(cin, cout, p, form)
+        if plan[0] == "hip":
+            lib = hip.load()
+            packed = cache.get([weight], cin, cout, 0)
+            y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
+            wsb = lib.msl_pconv_fwd_workspace(cin, cout, p)
+            ws = hip.workspace(wsb, x.device)
+            hip.check(lib.msl_pconv_fwd(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
+                                        hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()),
+                      "msl_pconv_fwd")
+        else:
+            y = F.conv2d(x, weight)
         ctx.save_for_backward(x, weight)
         ctx.cache = cache
+        ctx.plan = plan
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
+        _, dplan, wplan = ctx.plan
         cout, cin = weight.shape[0], weight.shape[1]
         h, w = x.shape[2], x.shape[3]
         p = h * w
@@ -312,9 +359,7 @@ class _Conv1x1(Function):
         w2 = weight.view(cout, cin)
         dx = None
         if ctx.needs_input_grad[0]:
-            if cout > cin and cin >= 128 and p <= 16384 and f32_form() == "bf16x6":
-                # HIP x6 pointwise dgrad (layer3 conv3 256<-1024: 48.6 vs 65.2 us on hipBLASLt,
-                # profiles/r01_tune_pconv_x6.txt; layer4 conv3 512<-2048: 154.6 vs 166.7)
+            if dplan == "hip":
                 lib = hip.load()
                 packed_d = ctx.cache.get([weight], cin, cout, 1)
                 dx = torch.empty_like(x)
@@ -323,7 +368,7 @@ class _Conv1x1(Function):
                 hip.check(lib.msl_pconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
                                               hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
                                               hip.stream_ptr()), "msl_pconv_dgrad")
-            elif cout > cin:
+            elif dplan == "hipblaslt":
                 dx = torch.mm(w2.t(), g2).view(1, cin, h, w)
             else:
                 dx = torch.ops.aten.convolution_backward(gy, x, weight, None, (1, 1), (0, 0), (1, 1), False,
@@ -331,7 +376,7 @@ class _Conv1x1(Function):
         if not ctx.needs_input_grad[1]:
             return dx, None, None
         sink = grad_sink(weight)
-        if p > 16384:
+        if wplan == "hip":
             # HIP pointwise wgrad (accumulating into the flat buffer when it can)
             lib = hip.load()
             dst = sink[0] if sink is not None else torch.empty_like(weight)

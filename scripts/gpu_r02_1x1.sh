@@ -1,0 +1,10 @@
+#!/bin/bash
+# 1x1 dispatch: op tests, eager / graph bench lines, kernel-trace profile of the eager bench.
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd $R
+./scripts/gpu_steps.sh \
+  "300|t1x1.log|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ops.py -k 'conv1x1 or pconv'" \
+  "300|bench_eager.log|python bench.py --graph 0 --cpu-baseline-iters 0" \
+  "300|bench_graph.log|python bench.py --graph 1 --cpu-baseline-iters 0" || exit $?
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_e -o prof --output-format csv -- python3 $R/bench.py --graph 0 --steps 5 --warmup 2 --cpu-baseline-iters 0 > $R/gpurun_out/prof_e.log 2>&1

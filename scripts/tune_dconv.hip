@@ -1,5 +1,5 @@
 // Standalone tuning harness for the dilated-conv implicit-GEMM kernels (not part of the library).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I maxsquareloss_amd/csrc scripts/tune_dconv.hip -o /tmp/tune
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I maxsquareloss_amd/csrc -I scripts scripts/tune_dconv.hip -o scripts/tune_dconv
 // Times tile / depth / split variants at the layer3 (d=2) and layer4 (d=4) shapes in one process
 // and checks every variant against the first one.
 #include <cmath>
@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 #include "dconv_kernels.h"
+#include "tune_x6_variants.h"
 
 using namespace msl;
 
@@ -117,8 +118,9 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   return ms / iters;
 }
 
-template <bool PW>
-float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda) {
+template <bool PW, int EXP = 0, int V = 0>
+float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda,
+                bool reduce = true) {
   const int P = sh.h * sh.w;
   const int taps = PW ? 1 : 9;
   FwdArgs a;
@@ -139,8 +141,10 @@ float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, floa
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_x6_sk, dim3(sk.NW), dim3(256), 0, 0, a, sk);
-    hipLaunchKernelGGL((k_sk_reduce<128, 128>), dim3(128 * 128 / 1024, tiles), dim3(256), 0, 0, a, sk);
+    if (V == 1) hipLaunchKernelGGL(k_x6_sk2, dim3(sk.NW), dim3(256), 0, 0, a, sk);
+    else if (V == 2) hipLaunchKernelGGL(k_x6_sk3, dim3(sk.NW), dim3(256), 0, 0, a, sk);
+    else hipLaunchKernelGGL(k_x6_sk<EXP>, dim3(sk.NW), dim3(256), 0, 0, a, sk);
+    if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, 128>), dim3(128 * 128 / 1024, tiles), dim3(256), 0, 0, a, sk);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -306,7 +310,11 @@ int main(int argc, char** argv) {
   const bool pw_mode = argc > 1 && std::string(argv[1]) == "pw";
   // "reg": the register-staged x6 kernel (k_x6_sk) vs the LDS-DMA x6p one, 3x3 and pointwise
   const bool reg3 = argc > 1 && std::string(argv[1]) == "reg3";  // profiling: layer3 shape only
-  const bool reg_mode = (argc > 1 && std::string(argv[1]) == "reg") || reg3;
+  // "abl": k_x6_sk alone (no reduce) and its timing ablations, layer3 / layer4
+  const bool abl = argc > 1 && std::string(argv[1]) == "abl";
+  // "reg2": k_x6_sk2 (A fragments in registers) vs k_x6_sk vs the LDS-DMA kernel, vs fp64
+  const bool reg2 = argc > 1 && std::string(argv[1]) == "reg2";
+  const bool reg_mode = (argc > 1 && std::string(argv[1]) == "reg") || reg3 || abl || reg2;
   const int iters = sk_only ? 5 : 20;
   std::vector<Shape> shapes = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
   if (wsks) shapes = {{128, 128, 65, 129, 1}, {64, 64, 129, 257, 1}};
@@ -314,6 +322,7 @@ int main(int argc, char** argv) {
   if (reg_mode) shapes = {{256, 256, 65, 129, 2}, {512, 512, 65, 129, 4}, {1024, 256, 65, 129, 0}, {256, 1024, 65, 129, 0},
                           {2048, 512, 65, 129, 0}};
   if (reg3) shapes = {{256, 256, 65, 129, 2}};
+  if (abl) shapes = {{256, 256, 65, 129, 2}, {512, 512, 65, 129, 4}, {1024, 256, 65, 129, 0}};
   const bool pwx = pw_mode || reg_mode;
   for (const Shape& sh : shapes) {
     if ((x6_mode || rg_mode || big_mode) && (sh.cin != sh.cout || sh.h != 65)) continue;  // layer3 / layer4 shapes
@@ -323,6 +332,9 @@ int main(int argc, char** argv) {
     const long long kp = (long long)((sh.cin + 15) / 16) * (shape_pw ? 1 : 9) * 16;
     std::vector<float> hx((size_t)sh.cin * P), hw((size_t)kp * lda), hdy((size_t)sh.cout * P);
     fill(hx, 1, 2.f); fill(hw, 2, 0.02f); fill(hdy, 3, 2.f);
+    if (getenv("TUNE_ZERO")) {  // all-zero operands: the same instructions at a lower power draw (DVFS probe)
+      std::fill(hx.begin(), hx.end(), 0.f); std::fill(hw.begin(), hw.end(), 0.f); std::fill(hdy.begin(), hdy.end(), 0.f);
+    }
     float *x, *wp, *dy, *y, *yref, *ws, *dw, *dwref;
     int* flags; CK(hipMalloc(&flags, 1 << 20));
     CK(hipMalloc(&x, hx.size() * 4)); CK(hipMalloc(&wp, hw.size() * 4)); CK(hipMalloc(&dy, hdy.size() * 4));
@@ -344,7 +356,27 @@ int main(int argc, char** argv) {
       float ms = run_fwd_sk<128, 128, 1, 4, 2, 2, 3, PW>(sh, x, wp, y, ws, 512, iters, lda, flags); \
       err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
       printf("x6p  PW %d ST 4  NW  512 : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, ms * 1e3, gf / ms, mx, rms); }
-      if (reg3) {
+#define REG2(PW, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_x6reg<PW, 0, 1>(sh, x, wp, y, ws, NW, iters, lda); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
+      printf("reg2 PW %d       NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, NW, ms * 1e3, gf / ms, mx, rms); }
+#define REG3(PW, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_x6reg<PW, 0, 2>(sh, x, wp, y, ws, NW, iters, lda); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
+      printf("reg3 PW %d       NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, NW, ms * 1e3, gf / ms, mx, rms); }
+      if (reg2) {
+        if (shape_pw) { OLD(true) REG(true, 512) REG2(true, 512) REG3(true, 512) }
+        else { OLD(false) REG(false, 512) REG2(false, 512) REG3(false, 512) }
+      } else if (abl) {
+#define ABL(PW, EXP, what) { float ms = run_x6reg<PW, EXP>(sh, x, wp, y, ws, 512, iters, lda, false); \
+        printf("abl  %-34s : %8.1f us %7.1f TF\n", what, ms * 1e3, gf / ms); }
+#define ABLS(PW) ABL(PW, 0, "kernel only") ABL(PW, 1, "loads of K-step 0 only") ABL(PW, 2, "no MFMA") \
+        ABL(PW, 4, "no global loads") ABL(PW, 8, "no piece/output stores") ABL(PW, 16, "no split") \
+        ABL(PW, 6, "no loads, no MFMA") ABL(PW, 12, "no loads, no stores") ABL(PW, 14, "no loads/MFMA/stores") \
+        ABL(PW, 30, "no loads/MFMA/stores/split") ABL(PW, 96, "A bypasses LDS") ABL(PW, 104, "A bypasses LDS, no stores") \
+        ABL(PW, 110, "A bypasses LDS, no loads/MFMA/stores")
+        if (shape_pw) { ABLS(true) } else { ABLS(false) }
+      } else if (reg3) {
         OLD(false) REG(false, 512)
       } else if (shape_pw) {
         OLD(true) REG(true, 512) REG(true, 384) REG(true, 256)

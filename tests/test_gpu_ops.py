@@ -85,10 +85,12 @@ def test_pconv_fwd_bwd(cin, cout, h, w, f32_form):
     assert _rel(y2, -2.0 * yr.detach()) < 1e-5
 
 
-@pytest.mark.parametrize("cin,cout,h,w", [(64, 256, 129, 257), (256, 64, 129, 257), (1024, 256, 65, 129),
-                                           (256, 1024, 65, 129), (512, 2048, 17, 33)])
-def test_conv1x1_library_gemms(cin, cout, h, w):
-    """ops.conv1x1: MIOpen / hipBLASLt / HIP-wgrad mix, every gradient against fp64."""
+@pytest.mark.parametrize("cin,cout,h,w", [(64, 256, 129, 257), (256, 64, 129, 257), (64, 64, 129, 257),
+                                           (1024, 256, 65, 129), (256, 1024, 65, 129), (1024, 512, 65, 129),
+                                           (512, 128, 65, 129), (128, 512, 65, 129), (512, 2048, 17, 33)])
+def test_conv1x1_dispatch(cin, cout, h, w, f32_form):
+    """ops.conv1x1: every GEMM on the implementation conv1x1_plan picks (HIP x6 / MIOpen /
+    hipBLASLt), every gradient against fp64, in both fp32 forms."""
     g = torch.Generator().manual_seed(cin + 5 * cout)
     x = torch.randn(1, cin, h, w, generator=g)
     wt = torch.randn(cout, cin, 1, 1, generator=g) * 0.05

@@ -134,6 +134,30 @@ def test_bench_feature_geometry():
     assert bench.feat_hw(640) == 81 and bench.feat_hw(760) == 96 and bench.feat_hw(1280) == 161
 
 
+def test_conv1x1_plan_matches_measured_winners():
+    """ops.conv1x1_plan reproduces the per-GEMM winners measured on MI355X for every 1x1 shape of
+    the UDA step (profiles/r02_conv1x1_dispatch.txt), with near-ties (< 3 %) allowed either way."""
+    from maxsquareloss_amd import ops
+    table = {}
+    for line in open(os.path.join(ROOT, "profiles", "r02_conv1x1_dispatch.txt")):
+        m = re.match(r"\s*(\d+)->\s*(\d+) P\s+(\d+) x\s*\d+ \| (.*) \| packs", line)
+        if not m:
+            continue
+        times = {}
+        for part in m.group(4).split(" | "):
+            gemm, rest = part.split(": ")
+            vals = rest.split()
+            times[gemm] = {vals[i].replace("hip_x6", "hip"): float(vals[i + 1]) for i in range(0, len(vals), 2)}
+        table[(int(m.group(1)), int(m.group(2)), int(m.group(3)))] = times
+    assert len(table) == 13
+    for (cin, cout, p), times in table.items():
+        plan = dict(zip(("fwd", "dgrad", "wgrad"), ops.conv1x1_plan(cin, cout, p)))
+        for gemm, t in times.items():
+            assert t[plan[gemm]] <= 1.03 * min(t.values()), (cin, cout, p, gemm, plan[gemm], t)
+        # the mfma_f32 form: fwd and dgrad on the libraries (its HIP pointwise kernels are slower)
+        assert "hip" not in ops.conv1x1_plan(cin, cout, p, "mfma_f32")[:2]
+
+
 def test_poly_lr_matches_reference_formula():
     from maxsquareloss_amd.tools.train_source import Trainer
 
