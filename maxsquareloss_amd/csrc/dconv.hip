@@ -211,14 +211,25 @@ static FwdPlan plan_fwd(int nbranch, int taps, int cimg, int M, int P, bool has_
 // 512-channel layer4 convs, 64x64 at two per CU below, 32-row tiles for the 19-class ASPP.
 struct WgradPlan {
   int bm, bn, nw, tiles_m, tiles_n, ntap, KS, slots;
+  bool rx6;        // k_wgrad_x6 (register-staged bf16x6, dY pre-split) with 16-pixel K-steps
+  int lda;         // rx6: dY plane row length
   long long T;
 };
 
-static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, bool x6 = false) {
+static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, bool x6 = false, int w = 0) {
   WgradPlan pl;
-  if (x6 && cout >= 128 && cin >= 128) {
-    // x6: 128x128 tiles (2 x 2 fragments per wave amortise the operand splits); 110 vs 130 us
-    // on layer3, 390 vs 428 on layer4 (scripts/tune_dconv.hip x6)
+  pl.rx6 = false;
+  pl.lda = 0;
+  int bk = kWskBK;
+  if (x6 && cout >= 256 && cin >= 256 && w >= 16) {
+    // x6, >= 256 channels: k_wgrad_x6, 128x128 tiles at two workgroups per CU (layer3 96 vs 112 us,
+    // layer4 313 vs 388; 128 channels stay on k_wgrad_sk: 44 vs 50)
+    // (scripts/tune_dconv.hip wx6, profiles/r02_wgrad_x6.txt)
+    pl.bm = 128; pl.bn = 128; pl.nw = 512;
+    pl.rx6 = true;
+    pl.lda = pad_to(cout, kPackPad);
+    bk = kWx6BK;
+  } else if (x6 && cout >= 128 && cin >= 128) {
     pl.bm = 128; pl.bn = 128; pl.nw = 256;
   } else if (cout <= 32) {
     pl.bm = 32; pl.bn = 128; pl.nw = 256;
@@ -232,13 +243,16 @@ static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, boo
   pl.tiles_m = cdiv(cout, pl.bm);
   pl.tiles_n = cdiv(cin, pl.bn);
   pl.ntap = nbranch * taps;
-  pl.KS = cdiv(P, kWskBK);
+  pl.KS = cdiv(P, bk);
   pl.T = (long long)pl.tiles_m * pl.tiles_n * pl.ntap * pl.KS;
   pl.nw = (int)std::min<long long>(pl.nw, pl.T);
   // tiles a worker range can touch: its length (<= ceil(T/NW) stages) starting anywhere in a tile
   pl.slots = (int)((cdiv(pl.T, (long long)pl.nw) + pl.KS - 2) / pl.KS + 1);
   return pl;
 }
+
+static size_t wgrad_piece_bytes(const WgradPlan& pl) { return (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float); }
+static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)pl.KS * 6 * pl.lda * 16 : 0; }
 
 // stream-K workspace: the published pieces, NW x 2 x BM*BN floats.  The arrival counters live in
 // a caller-owned, persistent int[kMaxCounters] that is zero on entry and left zero on exit (the
@@ -410,12 +424,12 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
   return MSL_OK;
 }
 
-static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P) {
-  // large enough for either fp32 form
+static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P, int w) {
+  // large enough for either fp32 form: pieces, then (k_wgrad_x6) the split dY planes
   size_t b = 0;
   for (int x6 = 0; x6 < 2; ++x6) {
-    WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, x6 != 0);
-    b = std::max(b, (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float));
+    WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, x6 != 0, w);
+    b = std::max(b, wgrad_piece_bytes(pl) + wgrad_planes_bytes(pl));
   }
   return b;
 }
@@ -426,8 +440,8 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
                         int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
   const int P = h * w;
   constexpr int MS = MT == kMathX6 ? kMathF32 : MT;  // x6 only on 128x128 tiles (plan_wgrad)
-  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, MT == kMathX6);
-  if (ws_bytes < wgrad_ws_bytes(nbranch, taps, cin, cout, P)) return MSL_ERR_WORKSPACE;
+  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, MT == kMathX6, w);
+  if (ws_bytes < wgrad_ws_bytes(nbranch, taps, cin, cout, P, w)) return MSL_ERR_WORKSPACE;
   if (pl.T * pl.nw >= (1LL << 31) || (long long)pl.nw * pl.slots * pl.bm * pl.bn * 4 >= (1LL << 31) || (long long)std::max(cin, cout) * P >= (1LL << 29) ||
       (long long)P + kWskBK >= (1LL << 22))
     return MSL_ERR_SHAPE;  // 32-bit index arithmetic, float pixel-row division in the kernel
@@ -453,9 +467,20 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   a.NW = pl.nw;
   a.T = (int)pl.T;
   a.cbranch = (long long)cout * cin * taps;
+  a.dyx6 = nullptr;
+  a.lda = pl.lda;
   const dim3 grid(pl.nw), block(256);
-  const dim3 rgrid(cdiv((long long)pl.bm * pl.bn * taps, 256), pl.tiles_m * pl.tiles_n * nbranch), rblock(256);
-  if (pl.bm == 128) {
+  const dim3 rgrid(cdiv((long long)pl.bm * pl.bn / 4 * taps, 256), pl.tiles_m * pl.tiles_n * nbranch), rblock(256);
+  if (pl.rx6) {
+    bf16x8* planes = reinterpret_cast<bf16x8*>((char*)ws + wgrad_piece_bytes(pl));
+    a.dyx6 = planes;
+    hipLaunchKernelGGL(k_split_rows, dim3(pl.lda / 32, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P, pl.KS,
+                       pl.lda, planes);
+    MSL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_wgrad_x6, grid, block, 0, st, a);
+    MSL_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
+  } else if (pl.bm == 128) {
     hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2, MT>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
@@ -572,7 +597,7 @@ int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int n
 
 size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
   if (bad_dims(nbranch, cin, cout, h, w)) return 0;
-  return wgrad_ws_bytes(nbranch, 9, cin, cout, h * w);
+  return wgrad_ws_bytes(nbranch, 9, cin, cout, h * w, w);
 }
 
 int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
@@ -623,7 +648,7 @@ int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int c
 
 size_t msl_pconv_wgrad_workspace(int cin, int cout, int p) {
   if (bad_dims(1, cin, cout, 1, p)) return 0;
-  return wgrad_ws_bytes(1, 1, cin, cout, p);
+  return wgrad_ws_bytes(1, 1, cin, cout, p, p);
 }
 
 int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,

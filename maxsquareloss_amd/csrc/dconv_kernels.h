@@ -1306,6 +1306,8 @@ struct WskArgs {
   float invW;
   int tiles_m, tiles_n, KS, NW, T;
   long long cbranch;  // M * N * taps
+  const void* dyx6;   // k_wgrad_x6: dY split into bf16 planes by k_split_rows
+  int lda;            // k_wgrad_x6: plane row length (M rounded up to kPackPad)
 };
 
 constexpr int kWskBK = 64;
@@ -1472,39 +1474,285 @@ __global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
   }
 }
 
-// dW (=|+=) the sum of every tile's pieces, in worker order.  One thread per (m, n, tap) of an
-// (m-block, n-block, branch) group, tap fastest: the dW stores are contiguous, and there are
-// enough waves in flight to hide the (serial, per-thread) piece loads.
-// grid = (ceil(BM*BN*taps / 256), tiles_m * tiles_n * nbranch).
+// dW (=|+=) the sum of every tile's pieces, in worker order.  One thread per (4 consecutive
+// (m, n), tap) of an (m-block, n-block, branch) group, (m, n) fastest: the piece reads are float4
+// and coalesced (consecutive threads, consecutive elements of one piece); the dW stores ([m][n]
+// [tap]) are taps apart.  grid = (ceil(BM*BN / 4 * taps / 256), tiles_m * tiles_n * nbranch).
 template <int BM, int BN>
 __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
-  constexpr int PSZ = BM * BN;
+  constexpr int PSZ = BM * BN, P4 = PSZ / 4;
+  static_assert(BN % 4 == 0, "float4 rows");
   const int gsz = a.tiles_m * a.tiles_n;
   const int br = blockIdx.y / gsz;
   const int rem = blockIdx.y - br * gsz;
   const int tn = rem / a.tiles_m, tm = rem - tn * a.tiles_m;
   const int e = blockIdx.x * 256 + threadIdx.x;
-  const int g = e / a.taps, tap = e - g * a.taps;
-  const int m = tm * BM + g / BN, n = tn * BN + g % BN;
-  if (g >= PSZ || m >= a.M || n >= a.N) return;
+  const int tap = e / P4, g4 = e - tap * P4;
+  if (tap >= a.taps) return;
+  const int m = tm * BM + (g4 * 4) / BN, n = tn * BN + (g4 * 4) % BN;
+  if (m >= a.M || n >= a.N) return;
   const int t = ((br * a.taps + tap) * a.tiles_n + tn) * a.tiles_m + tm;
   const int w_lo = sk_worker_of(t * a.KS, a.T, a.NW);
   const int w_hi = sk_worker_of((t + 1) * a.KS - 1, a.T, a.NW);
-  const float* __restrict__ part = a.part;
+  const float4* __restrict__ part = reinterpret_cast<const float4*>(a.part);
   auto piece = [&](int wc) {
     const int slot = t - sk_start(wc, a.T, a.NW) / a.KS;
-    return part[(long long)(wc * a.slots + slot) * PSZ + g];
+    return part[(long long)(wc * a.slots + slot) * P4 + g4];
   };
+  auto add = [](float4& s, const float4& x) { s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w; };
   // four loads in flight per step (the sum stays in worker order)
-  float v = 0.f;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
   int wc = w_lo;
   for (; wc + 3 <= w_hi; wc += 4) {
-    const float p0 = piece(wc), p1 = piece(wc + 1), p2 = piece(wc + 2), p3 = piece(wc + 3);
-    v += p0; v += p1; v += p2; v += p3;
+    const float4 p0 = piece(wc), p1 = piece(wc + 1), p2 = piece(wc + 2), p3 = piece(wc + 3);
+    add(v, p0); add(v, p1); add(v, p2); add(v, p3);
   }
-  for (; wc <= w_hi; ++wc) v += piece(wc);
-  float* dst = a.dw + br * a.cbranch + (long long)m * a.N * a.taps + (long long)n * a.taps + tap;
-  *dst = a.accumulate ? *dst + v : v;
+  for (; wc <= w_hi; ++wc) add(v, piece(wc));
+  float* dst = a.dw + br * a.cbranch + ((long long)m * a.N + n) * a.taps + tap;
+  const float vals[4] = {v.x, v.y, v.z, v.w};
+  const int nn = min(4, a.N - n);
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (c < nn) dst[c * a.taps] = a.accumulate ? dst[c * a.taps] + vals[c] : vals[c];
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16x6 weight gradient, register-staged (the layer2-4 and ASPP-free x6 path).
+//
+// k_wgrad_sk moves both fp32 operands by LDS-DMA, one 64-pixel row per wave-instruction (64 DMA
+// issues per wave and stage at 128x128), and every wave splits the fp32 values of its own
+// fragments into bf16 terms - each element twice, once per wave sharing its rows.  Here:
+//   - dY is split once per call into bf16 planes (k_split_rows: [K-step = 16 pixels][plane]
+//     [k half][row][8], zeros past P and M), read by each wave straight into registers (one 16-B
+//     vector per lane and plane, one K-step ahead, like the forward's packed weights);
+//   - X rows are loaded by threads in 4-pixel chunks (16-B loads; 8 lanes cover a row's 32
+//     pixels of the stage, one 128-B line), masked, split once and written to LDS as 8-B quarters
+//     of [plane][k half][n][8] rows - the forward kernels' B layout (ds_read_b128 fragments), with
+//     32 B of padding per (plane, half) row block so both the 8-B stores and the fragment reads
+//     are conflict-free;
+//   - the image-border mask of a tap depends only on the pixel, so it is computed per K-step in
+//     scalar registers (16 bits: row and column range tests of the K-step's pixel run) and each
+//     lane tests its chunk's 4 bits;
+//   - two K-steps per LDS stage, one barrier per 48 MFMAs per wave; pieces and k_wsk_reduce as
+//     k_wgrad_sk (every tile leaves its pieces; the reduce writes dW taps-innermost).
+// K-step = 16 pixels: KS = ceil(P / 16) per tile.  Needs W >= 16 (the mask handles one row wrap).
+constexpr int kWx6BK = 16;
+
+// planes[((ks*3 + q)*2 + h)*lda + m][j] = term q of src[m][ks*16 + 8h + j] (0 past P or M).
+// Block = 32 rows x 4 K-steps: reads of 8 consecutive pixels per thread (8 lanes per 256-B row
+// run), split, transposed through LDS so each plane row is written as 32 contiguous vectors.
+// grid = (lda / 32, ceil(KS / 4)).
+__global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ src, int M, int P, int KS, int lda,
+                                                     bf16x8* __restrict__ planes) {
+  __shared__ bf16x8 tile[3][8][33];
+  const int tid = threadIdx.x;
+  const int m0 = blockIdx.x * 32, ks0 = blockIdx.y * 4;
+  {
+    const int r = tid >> 3, c = tid & 7;  // row, 8-pixel chunk (= K-step ks0 + c/2, half c%2)
+    const int m = m0 + r, p0 = ks0 * kWx6BK + c * 8;
+    const float* row = src + (long long)m * P;
+    Split3 sp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_set(sp, j, (m < M && p0 + j < P) ? row[p0 + j] : 0.f);
+    tile[0][c][r] = sp.hi;
+    tile[1][c][r] = sp.mid;
+    tile[2][c][r] = sp.lo;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int v = tid + 256 * i;  // (q, c, r): r fastest
+    const int r = v & 31, c = (v >> 5) & 7, q = v >> 8;
+    const int ks = ks0 + (c >> 1);
+    if (ks < KS) planes[(long long)((ks * 3 + q) * 2 + (c & 1)) * lda + m0 + r] = tile[q][c][r];
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
+  constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
+  constexpr int RB = 128 * 16 + 32;   // bytes per (plane, k half) block of 128 rows, padded
+  constexpr int KVB = 6 * RB;         // one K-step's B planes
+  constexpr int STAGEB = 2 * KVB;     // two K-steps
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGEB];  // 48.75 KB: the only LDS object
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);  // XCD-aware worker id
+  const int it_begin = sk_start(w, a.T, a.NW), it_end = sk_start(w + 1, a.T, a.NW);
+
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.dyx6, (short)0, (int)min(0x7fffffffLL, (long long)a.KS * 6 * a.lda * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)min(0x7fffffffLL, (long long)a.N * a.P * 4), 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  const unsigned a_plane_bytes = (unsigned)a.lda * 16u;
+  // this thread's B chunks: c = tid + 256 i -> row c / 8, chunk c % 8 (4 pixels) of the stage's 32
+  const int cc = tid & 7;
+  const int ck = cc >> 2, chh = (cc >> 1) & 1, cq = cc & 1;  // K-step, k half, quarter
+  const int wofs = ck * KVB + chh * RB + (tid >> 3) * 16 + cq * 8;  // + q*2*RB + i*32*16
+
+  f32x16 acc[TM][TN];
+  for (int it = it_begin; it < it_end;) {
+    const int t = (unsigned)it / (unsigned)a.KS;
+    const int k_a = it - t * a.KS;
+    const int k_b = min(a.KS, k_a + (it_end - it));
+    const int nst = k_b - k_a;
+    it += nst;
+    const int tm = t % a.tiles_m;
+    const int t2 = t / a.tiles_m;
+    const int tn = t2 % a.tiles_n;
+    const int z = t2 / a.tiles_n;  // branch * taps + tap
+    const int br = z / a.taps, tap = z - br * a.taps;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int d = br ? a.dil1 : a.dil0;
+    const int dh = (tap / 3 - 1) * d, dw = (tap % 3 - 1) * d;
+    const int shift = dh * a.W + dw;
+    // pixel cursor of the next K-step to load (scalar): ks*16 = cy*W + cx
+    int ld_ks = k_a;
+    int cy = (k_a * kWx6BK) / a.W, cx = k_a * kWx6BK - cy * a.W;
+    const int clo = max(0, -dw), chi = a.W - max(0, dw);  // valid source columns px + dw
+    auto seg = [](int lo, int hi) -> unsigned {      // bits lo .. hi-1 of a 16-bit mask
+      lo = max(lo, 0);
+      hi = min(hi, 16);
+      return hi > lo ? ((1u << hi) - (1u << lo)) : 0u;
+    };
+    auto kmask = [&]() -> unsigned {  // valid pixels of K-step ld_ks; advances the cursor
+      unsigned m16 = 0;
+      if (ld_ks < k_b) {
+        const int L1 = a.W - cx;  // pixels of the K-step left in row cy
+        if ((unsigned)(cy + dh) < (unsigned)a.H) m16 |= seg(clo - cx, min(L1, chi - cx));
+        if ((unsigned)(cy + 1 + dh) < (unsigned)a.H) m16 |= seg(L1 + clo, L1 + chi);
+      }
+      ++ld_ks;
+      cx += kWx6BK;
+      if (cx >= a.W) { cx -= a.W; ++cy; }
+      return m16;
+    };
+    float rbv[16];
+    auto loadB = [&]() {  // the stage's two K-steps (a missing second one is all-masked)
+      const int ks0 = ld_ks;
+      const unsigned m32 = kmask() | (kmask() << 16);
+      const unsigned mb = (m32 >> (4 * cc)) & 0xfu;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int nr = (tid >> 3) + 32 * i;
+        const long long e = (long long)(n0 + nr) * a.P + ks0 * kWx6BK + 4 * cc + shift;
+        union { u32x4 u; float f[4]; } c;
+        if (n0 + nr < a.N && e >= 0) {
+          c.u = __builtin_amdgcn_raw_buffer_load_b128(rB, (unsigned)e * 4u, 0, 0);
+        } else {  // row past N, or a run starting before X (row 0, negative shift): per element
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const unsigned off = (n0 + nr < a.N && e + j >= 0) ? (unsigned)(e + j) * 4u : OOB;
+            c.f[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rB, off, 0, 0));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rbv[4 * i + j] = (mb >> j) & 1u ? c.f[j] : 0.f;
+      }
+    };
+    auto storeB = [&](int buf) {  // split once, three 8-B plane quarters per chunk
+      char* base = smem + buf * STAGEB + wofs;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bf16x4 hi, mid, lo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = rbv[4 * i + j];
+          const __bf16 h = (__bf16)v;
+          const float r = v - (float)h;
+          const __bf16 m = (__bf16)r;
+          hi[j] = h;
+          mid[j] = m;
+          lo[j] = (__bf16)(r - (float)m);
+        }
+        char* dst = base + i * 32 * 16;
+        *reinterpret_cast<bf16x4*>(dst) = hi;
+        *reinterpret_cast<bf16x4*>(dst + 2 * RB) = mid;
+        *reinterpret_cast<bf16x4*>(dst + 4 * RB) = lo;
+      }
+    };
+    const unsigned a_voff = (unsigned)((kh * a.lda + m0 + wm + l32) * 16);
+    u32x4 A0[TM][3], A1[TM][3];
+    auto loadA = [&](u32x4 (&A)[TM][3], int ks) {
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          A[ii][q] = __builtin_amdgcn_raw_buffer_load_b128(rA, a_voff + ii * 512,
+                                                           (int)((unsigned)(ks * 6 + 2 * q) * a_plane_bytes), 0);
+    };
+    auto compute = [&](const char* Bs, const u32x4 (&A)[TM][3]) {
+      Split3 bv[TN];
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) {
+        const char* src = Bs + kh * RB + (wn + jj * 32 + l32) * 16;
+        bv[jj].hi = *reinterpret_cast<const bf16x8*>(src);
+        bv[jj].mid = *reinterpret_cast<const bf16x8*>(src + 2 * RB);
+        bv[jj].lo = *reinterpret_cast<const bf16x8*>(src + 4 * RB);
+      }
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) {
+        union { u32x4 u; bf16x8 h; } c0, c1, c2;
+        c0.u = A[ii][0]; c1.u = A[ii][1]; c2.u = A[ii][2];
+        Split3 av;
+        av.hi = c0.h; av.mid = c1.h; av.lo = c2.h;
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) acc[ii][jj] = mfma_x6(av, bv[jj], acc[ii][jj]);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    __syncthreads();  // the previous segment's LDS reads are complete in every wave
+    loadB();
+    loadA(A0, k_a);
+    storeB(0);
+    __syncthreads();
+    int ks = k_a;  // the K-step computed next
+    for (int s = 0; 2 * s < nst; ++s) {
+      const int left = nst - 2 * s;
+      const bool more = left > 2;  // a next stage
+      if (more) loadB();           // in flight during this stage's MFMAs
+      const char* Bs = smem + (s & 1) * STAGEB;
+      if (ks + 1 < k_b) loadA(A1, ks + 1);
+      compute(Bs, A0);
+      ++ks;
+      if (left > 1) {
+        if (ks + 1 < k_b) loadA(A0, ks + 1);
+        compute(Bs + KVB, A1);
+        ++ks;
+      }
+      if (more) storeB((s + 1) & 1);
+      __syncthreads();
+    }
+    // every tile leaves its piece(s) in `part` (k_wsk_reduce<128, 128>, as k_wgrad_sk)
+    constexpr int PSZ = BM * BN;
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.part, (short)0, (int)min(0x7fffffffLL, (long long)a.NW * a.slots * PSZ * 4), 0x00020000);
+    const int slot = t - it_begin / a.KS;
+    const unsigned pbase = (unsigned)((w * a.slots + slot) * PSZ * 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn + j * 32 + l32;
+        const int ml = wm + i * 32 + 4 * kh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rp,
+                                                pbase + (unsigned)(((ml + ro) * BN + nl) * 4), 0, 0);
+        }
+      }
+  }
 }
 
 }  // namespace msl

@@ -212,7 +212,36 @@ float run_wgrad_sk(const Shape& sh, const float* x, const float* dy, float* dw, 
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
     hipLaunchKernelGGL((k_wgrad_sk<BM, BN, ST, (BM >= 64 ? 2 : 1), (BM >= 64 ? 2 : 4), MT>), dim3(a.NW), dim3(256), 0, 0, a);
-    hipLaunchKernelGGL((k_wsk_reduce<BM, BN>), dim3(BM * BN * 9 / 256, a.tiles_m * a.tiles_n), dim3(256), 0, 0, a);
+    hipLaunchKernelGGL((k_wsk_reduce<BM, BN>), dim3((BM * BN / 4 * 9 + 255) / 256, a.tiles_m * a.tiles_n), dim3(256), 0, 0, a);
+  }
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / iters;
+}
+
+// k_split_rows + k_wgrad_x6 + k_wsk_reduce<128, 128> (the library's x6 weight gradient at >= 128 ch)
+float run_wgrad_x6(const Shape& sh, const float* x, const float* dy, float* dw, float* ws, int NWmax, int iters,
+                   bool split_only = false) {
+  const int P = sh.h * sh.w;
+  WskArgs a;
+  a.dy = dy; a.x = x; a.dw = dw; a.part = ws; a.M = sh.cout; a.N = sh.cin; a.H = sh.h; a.W = sh.w; a.P = P;
+  a.dil0 = sh.dil; a.dil1 = 0; a.taps = 9; a.accumulate = 0; a.invW = 1.0f / sh.w;
+  a.tiles_m = (sh.cout + 127) / 128; a.tiles_n = (sh.cin + 127) / 128; a.KS = (P + kWx6BK - 1) / kWx6BK;
+  const int tiles = a.tiles_m * a.tiles_n * 9;
+  a.T = tiles * a.KS; a.NW = std::min(NWmax, a.T); a.cbranch = (long long)sh.cout * sh.cin * 9;
+  a.slots = ((a.T + a.NW - 1) / a.NW + a.KS - 2) / a.KS + 1;
+  a.lda = (sh.cout + 127) / 128 * 128;
+  const size_t piece_bytes = (size_t)a.NW * a.slots * 128 * 128 * 4;
+  bf16x8* planes = (bf16x8*)((char*)ws + piece_bytes);
+  a.dyx6 = planes;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) CK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k_split_rows, dim3(a.lda / 32, (a.KS + 3) / 4), dim3(256), 0, 0, dy, a.M, P, a.KS, a.lda, planes);
+    if (split_only) continue;
+    hipLaunchKernelGGL(k_wgrad_x6, dim3(a.NW), dim3(256), 0, 0, a);
+    hipLaunchKernelGGL((k_wsk_reduce<128, 128>), dim3(128 * 128 / 4 * 9 / 256, a.tiles_m * a.tiles_n), dim3(256), 0, 0, a);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -315,6 +344,8 @@ int main(int argc, char** argv) {
   // "reg2": k_x6_sk2 (A fragments in registers) vs k_x6_sk vs the LDS-DMA kernel, vs fp64
   const bool reg2 = argc > 1 && std::string(argv[1]) == "reg2";
   const bool reg_mode = (argc > 1 && std::string(argv[1]) == "reg") || reg3 || abl || reg2;
+  // "wx6": the register-staged x6 weight gradient (k_wgrad_x6) vs k_wgrad_sk's x6 form, vs fp64
+  const bool wx6 = argc > 1 && std::string(argv[1]) == "wx6";
   const int iters = sk_only ? 5 : 20;
   std::vector<Shape> shapes = {{256, 256, 65, 129, 2}, {256, 128, 64, 256, 2}, {256, 256, 64, 128, 2}, {512, 512, 65, 129, 4}};
   if (wsks) shapes = {{128, 128, 65, 129, 1}, {64, 64, 129, 257, 1}};
@@ -322,6 +353,7 @@ int main(int argc, char** argv) {
   if (reg_mode) shapes = {{256, 256, 65, 129, 2}, {512, 512, 65, 129, 4}, {1024, 256, 65, 129, 0}, {256, 1024, 65, 129, 0},
                           {2048, 512, 65, 129, 0}};
   if (reg3) shapes = {{256, 256, 65, 129, 2}};
+  if (wx6) shapes = {{256, 256, 65, 129, 2}, {512, 512, 65, 129, 4}, {128, 128, 65, 129, 1}, {256, 256, 17, 33, 2}};
   if (abl) shapes = {{256, 256, 65, 129, 2}, {512, 512, 65, 129, 4}, {1024, 256, 65, 129, 0}};
   const bool pwx = pw_mode || reg_mode;
   for (const Shape& sh : shapes) {
@@ -421,6 +453,17 @@ int main(int argc, char** argv) {
 #define WSKE(BM, BN, ST, NW, MT) { float ms = run_wgrad_sk<BM, BN, ST, MT>(sh, x, dy, dw, ws, NW, iters); \
       err64_wgrad(sh, hx, hdy, dw, &mx, &rms); \
       printf("wsk  MT %d BM %3d BN %3d ST %d NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", MT, BM, BN, ST, NW, ms * 1e3, gf / ms, mx, rms); }
+    if (wx6) {
+      double mx, rms;
+      WSKE(128, 128, 2, 256, 2)
+#define WX6(NW) { CK(hipMemset(dw, 0, (size_t)sh.cout * sh.cin * 9 * 4)); \
+      float ms = run_wgrad_x6(sh, x, dy, dw, ws, NW, iters); \
+      err64_wgrad(sh, hx, hdy, dw, &mx, &rms); \
+      printf("wx6  (split+kernel+reduce) NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", NW, ms * 1e3, gf / ms, mx, rms); }
+      WX6(512) WX6(384) WX6(256)
+      printf("k_split_rows alone: %.1f us\n", run_wgrad_x6(sh, x, dy, dw, ws, 512, iters, true) * 1e3);
+      continue;
+    }
     if (rg_mode) {
       double mx, rms;
 #define RGE(BM, NW, MT) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
