@@ -293,7 +293,8 @@ def conv1x1_plan(cin, cout, p, form="bf16x6"):
              one side is >= 1024 channels (layer3/4 conv1/conv3/downsample); MIOpen elsewhere;
       dgrad  HIP at <= 16k px when one side is >= 1024 and both >= 256, except the narrowing
              1024 -> 256 (MIOpen wins there); else hipBLASLt when cout > cin or at 33k px, else MIOpen;
-      wgrad  HIP at 33k px, hipBLASLt addmm elsewhere.
+      wgrad  HIP at 33k px and on the 2048-channel layer4 GEMMs (k_wgrad_x6 with one tap),
+             hipBLASLt addmm elsewhere.
     """
     x6 = form == "bf16x6"
     big = p > 16384
@@ -305,7 +306,7 @@ def conv1x1_plan(cin, cout, p, form="bf16x6"):
         dgrad = "hipblaslt"
     else:
         dgrad = "miopen"
-    wgrad = "hip" if big else "hipblaslt"
+    wgrad = "hip" if big or (x6 and max(cin, cout) >= 2048) else "hipblaslt"
     return fwd, dgrad, wgrad
 
 
