@@ -155,6 +155,10 @@ def main():
         traffic = None  # the committed PMC figure belongs to another form of the kernel
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
+                "traffic_source": (os.path.relpath(a.pmc, ROOT) + ": committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                   "passes of this kernel (scripts/gpu_bench_prof.sh), not measured in this run; "
+                                   "memory-side bytes incl. Infinity-Cache hits") if traffic is not None else None,
+                "frac_of_fp32_spec": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "kernel": "dconv3x3 fwd layer3 d=2 (one op call: stream-K k_igemm_fwd_sk + k_sk_reduce; the bf16x6 weight planes are split at pack time, once per SGD step)",
                 "form": form, "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
