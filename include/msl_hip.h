@@ -11,9 +11,15 @@
  *   - Tensors are fp32 NCHW with N = 1 (bs = 1 per GPU), i.e.
  *     a [C][H][W] block; labels are int64 with -1 = ignore.
  *   - All pointers are caller-owned device pointers (the PyTorch caching
- *     allocator on the Python side).  The library allocates nothing and keeps
- *     no per-call global state; scratch comes from the caller's workspace,
- *     sized by the matching *_workspace() query.
+ *     allocator on the Python side).  The library allocates nothing; scratch
+ *     comes from the caller's workspace, sized by the matching *_workspace()
+ *     query, and no call leaves state that a later call reads.
+ *   - Process-wide configuration: three switches select kernel FORMS, not
+ *     results' meaning - msl_conv_set_f32_form, msl_conv_set_pack_form and
+ *     msl_bn_set_fused.  They are plain globals read on the host at launch
+ *     time: set them once at start-up, before work is enqueued; changing one
+ *     while another host thread enqueues calls is a data race, and a captured
+ *     hipGraph keeps the forms that were current at capture.
  *   - Work is enqueued on the given hipStream_t (passed as msl_stream_t) and
  *     is stream-ordered; no entry point synchronises the host, so every call
  *     is safe to capture in a hipGraph.
@@ -41,9 +47,10 @@ int msl_abi_version(void);
 const char* msl_status_string(int status);
 
 /* Length (ints) of the arrival-counter array the conv forward / data-gradient calls take.
- * The caller allocates it once per stream, zero-fills it once, and passes it to every call:
- * each call finds it zero and leaves it zero (the stream-K kernel re-arms what it uses).
- * Calls that may run concurrently need separate arrays. */
+ * Reserved: the current stream-K kernels never read or write it (split tiles are summed by a
+ * separate reduce launch, with no inter-workgroup signalling), so no call depends on its
+ * contents; it stays in the signatures for ABI stability.  Pass a zero-filled array of this
+ * length (non-NULL is checked). */
 int msl_counter_elems(void);
 
 /* Matrix-core form of the fp32 conv entry points (msl_dconv_* / msl_pconv_* without _bf16),

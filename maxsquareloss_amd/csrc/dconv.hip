@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(256) k_pack_split(const float* __restrict__ w,
 // persistent workgroups (2 per CU), so every CU gets the same number of MFMA stages whatever
 // the tile count.  The split-K tile kernel remains for an odd K-step count with M <= 32.
 constexpr int kSkBN = 128, kSkNW = 512;
-constexpr int kMaxCounters = 65536;  // stream-K arrival counters (one per output tile)
+constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
 
 struct FwdPlan {
   bool sk;
@@ -254,9 +254,8 @@ static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, boo
 static size_t wgrad_piece_bytes(const WgradPlan& pl) { return (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float); }
 static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)pl.KS * 6 * pl.lda * 16 : 0; }
 
-// stream-K workspace: the published pieces, NW x 2 x BM*BN floats.  The arrival counters live in
-// a caller-owned, persistent int[kMaxCounters] that is zero on entry and left zero on exit (the
-// finishing workgroup of each tile re-arms its counter), so no per-call memset is needed.
+// stream-K workspace: the published pieces, NW x 2 x BM*BN floats (summed by k_sk_reduce; no
+// counters, flags or other state survive a call).
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
   if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float);
   return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;

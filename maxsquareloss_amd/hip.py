@@ -131,8 +131,9 @@ _COUNTERS = {}
 
 
 def counters(device):
-    """The persistent, zero-initialised stream-K arrival counters for `device` and torch's current
-    stream (msl_counter_elems() ints; every conv call leaves them zero again)."""
+    """The zero-filled counter array the conv forward / data-gradient entry points take
+    (msl_counter_elems() ints, one per device and stream).  Reserved by the C-ABI: the current
+    kernels never touch it, so no call depends on what an earlier (or aborted) call left."""
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch._C._cuda_getDevice()
     key = (idx, torch._C._cuda_getCurrentRawStream(idx))

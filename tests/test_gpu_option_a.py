@@ -1,0 +1,86 @@
+"""INTEGRATION.md Option A end to end (GPU only): the reference's own train_target body
+(tools/solve_gta5.py:178-217, restated line by line below) driven through the drop-in modules -
+explicit F.softmax, target_loss(pred, prob) on the msl_*_prob_* kernels, the multi-level label
+built with torch ops and the drop-in CrossEntropyLoss - must give the losses and the parameter
+gradients of the package's fused train_target (softmax + upsample + loss in one kernel pair) on
+the same model, weights and target image.
+
+Tolerances: one forward/backward of the same network from the same state, so the two paths
+differ only by fp32 rounding of the loss arithmetic (torch softmax vs the fused kernel): losses
+1e-5 relative, the whole gradient 1e-4 normwise; the IW class histogram (argmax of the two
+paths' probabilities - torch's softmax vs the kernel's) within 0.05 % of the pixels.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from maxsquareloss_amd.tools.solve_gta5 import UDATrainer, build_parser  # noqa: E402
+from maxsquareloss_amd.tools.train_source import init_args  # noqa: E402
+from maxsquareloss_amd.utils.loss import CrossEntropyLoss  # noqa: E402
+from maxsquareloss_amd.utils.synthetic import synthetic_image  # noqa: E402
+
+H, W = 128, 256
+
+
+def _trainer(mode):
+    argv = ["--crop_size", f"{W},{H}", "--target_crop_size", f"{W},{H}", "--imagenet_pretrained", "False",
+            "--save_dir", "", "--target_mode", mode, "--multi", "True", "--lambda_target", "0.09",
+            "--threshold", "0.2", "--iter_max", "1000"]
+    args, _, _ = init_args(build_parser().parse_args(argv))
+    tr = UDATrainer(args, cuda=True)
+    tr.model.train()
+    return tr
+
+
+def _reference_train_target(tr, pred, hard_loss):
+    """solve_gta5.py:178-217 for the soft target modes (maxsquare / IW_maxsquare), verbatim in
+    structure: the drop-in target_loss receives the probabilities."""
+    pred_2 = pred[1]
+    pred = pred[0]
+    pred_P_2 = F.softmax(pred_2, dim=1)
+    pred_P = F.softmax(pred, dim=1)
+    label = pred_P
+    maxpred, argpred = torch.max(pred_P.detach(), dim=1)
+    maxpred_2, argpred_2 = torch.max(pred_P_2.detach(), dim=1)
+    loss_target = tr.args.lambda_target * tr.target_loss(pred, label)
+    loss_target_ = loss_target
+    pred_c = (pred_P + pred_P_2) / 2
+    maxpred_c, argpred_c = torch.max(pred_c, dim=1)
+    mask = (maxpred > tr.threshold) | (maxpred_2 > tr.threshold)
+    label_2 = torch.where(mask, argpred_c, torch.ones(1).to(tr.device, dtype=torch.long) * -1)
+    loss_target_2 = tr.args.lambda_seg * tr.args.lambda_target * hard_loss(pred_2, label_2)
+    loss_target_ = loss_target_ + loss_target_2
+    loss_target_.backward()
+    return loss_target.detach(), loss_target_2.detach(), int(mask.sum())
+
+
+def _grads(model):
+    return torch.cat([p.grad.detach().flatten().double() for p in model.parameters() if p.grad is not None])
+
+
+@pytest.mark.parametrize("mode", ["maxsquare", "IW_maxsquare"])
+def test_reference_train_target_through_drop_in_modules(mode):
+    tr = _trainer(mode)
+    xt = synthetic_image(H, W, 321).cuda()
+    # the package's fused path
+    tr.optimizer.zero_grad()
+    tr.train_target(tr.model(xt))
+    fused = (tr.loss_target.detach().clone(), tr.loss_target_2.detach().clone())
+    g_fused = _grads(tr.model).clone()
+    hist_fused = tr.target_loss.last_hist.clone() if mode == "IW_maxsquare" else None
+    # the reference's train_target, imports swapped
+    tr.optimizer.zero_grad()
+    ref = _reference_train_target(tr, tr.model(xt), CrossEntropyLoss(ignore_index=-1))
+    g_ref = _grads(tr.model)
+    torch.cuda.synchronize()
+    assert ref[2] > 0  # the guidance label has pixels (threshold 0.2)
+    for a, b in zip(fused, ref[:2]):
+        assert a.item() == pytest.approx(b.item(), rel=1e-5), (mode, fused, ref)
+    assert g_fused.shape == g_ref.shape and g_ref.abs().max() > 0
+    rel = ((g_fused - g_ref).norm() / g_ref.norm()).item()
+    assert rel < 1e-4, (mode, rel)
+    if hist_fused is not None:
+        d = (hist_fused.long() - tr.target_loss.last_hist.long()).abs().sum().item()
+        assert d <= 2 * 0.0005 * H * W, (hist_fused, tr.target_loss.last_hist)
