@@ -694,6 +694,20 @@ struct SkArgs {
 };
 
 __device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
+// Tile t of the forward-form stream-K space -> (m-block, n-block), n fastest: consecutive tiles
+// share an m-block, so the 64 workers of one XCD (consecutive ranges) read one or two m-blocks'
+// weights and a contiguous pixel range - their L2 holds the operands.  Layer3 fwd: 66 vs 154 MB
+// fetched per launch with m fastest (FETCH_SIZE x 2), same time; 2048->512 pointwise 121 vs 133
+// us (profiles/r02_sk_tile_order.txt).  MSL_SK_MMAJOR restores m fastest for A/B builds.
+__device__ __forceinline__ void sk_tile(int t, int tiles_m, int tiles_n, int& tm, int& tn) {
+#ifdef MSL_SK_MMAJOR
+  tm = t % tiles_m;
+  tn = t / tiles_m;
+#else
+  tm = t / tiles_n;
+  tn = t - tm * tiles_n;
+#endif
+}
 __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
   return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
 }
@@ -758,7 +772,8 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
     const int k_b = min(sk.KS, k_a + (it_end - it));
     const int nst = k_b - k_a;
     it += nst;
-    const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
+    int tm, tn;
+    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     // per-lane constants of this tile: A byte offsets (stage 0), pixel coordinates
     unsigned a_off[A_INST_W];
@@ -995,7 +1010,8 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   const int w_lo = sk_worker_of(t * sk.KS, sk.T, sk.NW);
   const int w_hi = sk_worker_of((t + 1) * sk.KS - 1, sk.T, sk.NW);
   if (w_lo == w_hi) return;
-  const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
+  int tm, tn;
+    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const float4* __restrict__ part = reinterpret_cast<const float4*>(sk.part);
   for (int g = blockIdx.x * 256 + threadIdx.x; g < PSZ / 4; g += gridDim.x * 256) {
@@ -1159,7 +1175,8 @@ __global__ void __launch_bounds__(256) k_conv_rg(FwdArgs a, SkArgs sk) {
     const int k_b = min(sk.KS, k_a + (it_end - it));
     const int nst = k_b - k_a;
     it += nst;
-    const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
+    int tm, tn;
+    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     // A: instruction wid*A_INST_W + i loads rows of tap block a_tx[i] (wave-uniform)
     unsigned a_off[A_INST_W];

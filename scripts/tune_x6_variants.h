@@ -57,7 +57,8 @@ __global__ void __launch_bounds__(256, 2) k_x6_sk(FwdArgs a, SkArgs sk) {
     const int k_b = min(sk.KS, k_a + (it_end - it));
     const int nst = k_b - k_a;
     it += nst;
-    const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
+    int tm, tn;
+    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     const int p = n0 + bn;
     const bool pin = p < a.P;
@@ -282,7 +283,8 @@ __global__ void __launch_bounds__(256, 2) k_x6_sk2(FwdArgs a, SkArgs sk) {
     const int k_b = min(sk.KS, k_a + (it_end - it));
     const int nst = k_b - k_a;
     it += nst;
-    const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
+    int tm, tn;
+    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     const int p = n0 + bn;
     const bool pin = p < a.P;
@@ -496,7 +498,8 @@ __global__ void __launch_bounds__(256, 2) k_x6_sk3(FwdArgs a, SkArgs sk) {
     const int k_b = min(sk.KS, k_a + (it_end - it));
     const int nst = k_b - k_a;
     it += nst;
-    const int tm = t % sk.tiles_m, tn = t / sk.tiles_m;
+    int tm, tn;
+    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     const int p = n0 + bn;
     const bool pin = p < a.P;
