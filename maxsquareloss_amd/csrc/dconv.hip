@@ -213,22 +213,55 @@ struct WgradPlan {
   int bm, bn, nw, tiles_m, tiles_n, ntap, KS, slots;
   bool rx6;        // k_wgrad_x6 (register-staged bf16x6, dY pre-split) with 16-pixel K-steps
   int lda;         // rx6: dY plane row length
+  int nchunk, kchunk;  // rx6: chunked split-K (items = tiles x nchunk, kchunk K-steps each)
   long long T;
 };
+
+// k_wgrad_x6 with chunked split-K: the chunk count whose (tile, chunk) items fill whole rounds of
+// 512 resident workgroups best, at least 8 K-steps per item.  Returns the fill (0 if none).
+static double plan_chunks(long long ntiles, int KS, int& nchunk, int& kchunk) {
+  double best = 0.0;
+  nchunk = kchunk = 0;
+  for (int C = 1; C <= KS && ntiles * C <= 4096; ++C) {
+    const int L = cdiv(KS, C);
+    if (L < 8) break;
+    const int Ce = cdiv(KS, L);
+    const long long items = ntiles * Ce;
+    const double eff = (double)items / (double)(cdiv(items, 512LL) * 512);
+    if (eff > best + 0.01) {
+      best = eff;
+      nchunk = Ce;
+      kchunk = L;
+    }
+  }
+  return best;
+}
 
 static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, bool x6 = false, int w = 0) {
   WgradPlan pl;
   pl.rx6 = false;
   pl.lda = 0;
+  pl.nchunk = 0;
+  pl.kchunk = 0;
   int bk = kWskBK;
-  if (x6 && cout >= 256 && cin >= 256 && w >= 16) {
-    // x6, >= 256 channels: k_wgrad_x6, 128x128 tiles at two workgroups per CU (layer3 96 vs 112 us,
-    // layer4 313 vs 388; 128 channels stay on k_wgrad_sk: 44 vs 50)
-    // (scripts/tune_dconv.hip wx6, profiles/r02_wgrad_x6.txt)
+  const int ntap = nbranch * taps;
+  int nchunk = 0, kchunk = 0;
+  const bool rx6_ok = x6 && cout >= 128 && cin >= 128 && w >= 16;
+  const double fill = rx6_ok ? plan_chunks((long long)cdiv(cout, 128) * cdiv(cin, 128) * ntap, cdiv(P, kWx6BK),
+                                           nchunk, kchunk) : 0.0;
+  if (rx6_ok && (fill >= 0.75 || (cout >= 256 && cin >= 256))) {
+    // x6, >= 128 channels: k_wgrad_x6 (dY split once, 16-pixel K-steps, two workgroups per CU),
+    // chunked split-K when its items fill the resident slots (layer3 77.6 us, layer4 274,
+    // layer2 38.8; stream-K 86.5 / 306 / 44.1; k_wgrad_sk 110 / 395 / 41.0 -
+    // scripts/tune_dconv.hip wx6, profiles/r02_wgrad_x6.txt), else stream-K over 512 workers
     pl.bm = 128; pl.bn = 128; pl.nw = 512;
     pl.rx6 = true;
     pl.lda = pad_to(cout, kPackPad);
     bk = kWx6BK;
+    if (fill >= 0.75) {
+      pl.nchunk = nchunk;
+      pl.kchunk = kchunk;
+    }
   } else if (x6 && cout >= 128 && cin >= 128) {
     pl.bm = 128; pl.bn = 128; pl.nw = 256;
   } else if (cout <= 32) {
@@ -242,12 +275,16 @@ static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, boo
   }
   pl.tiles_m = cdiv(cout, pl.bm);
   pl.tiles_n = cdiv(cin, pl.bn);
-  pl.ntap = nbranch * taps;
+  pl.ntap = ntap;
   pl.KS = cdiv(P, bk);
   pl.T = (long long)pl.tiles_m * pl.tiles_n * pl.ntap * pl.KS;
   pl.nw = (int)std::min<long long>(pl.nw, pl.T);
   // tiles a worker range can touch: its length (<= ceil(T/NW) stages) starting anywhere in a tile
   pl.slots = (int)((cdiv(pl.T, (long long)pl.nw) + pl.KS - 2) / pl.KS + 1);
+  if (pl.nchunk > 0) {  // one piece per (tile, chunk) item
+    pl.nw = (int)((long long)pl.tiles_m * pl.tiles_n * pl.ntap * pl.nchunk);
+    pl.slots = 1;
+  }
   return pl;
 }
 
@@ -468,6 +505,9 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   a.cbranch = (long long)cout * cin * taps;
   a.dyx6 = nullptr;
   a.lda = pl.lda;
+  a.nchunk = pl.nchunk;
+  a.kchunk = pl.kchunk;
+  a.ntiles = pl.tiles_m * pl.tiles_n * pl.ntap;
   const dim3 grid(pl.nw), block(256);
   const dim3 rgrid(cdiv((long long)pl.bm * pl.bn / 4 * taps, 256), pl.tiles_m * pl.tiles_n * nbranch), rblock(256);
   if (pl.rx6) {

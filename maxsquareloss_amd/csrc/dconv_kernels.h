@@ -1325,6 +1325,12 @@ struct WskArgs {
   long long cbranch;  // M * N * taps
   const void* dyx6;   // k_wgrad_x6: dY split into bf16 planes by k_split_rows
   int lda;            // k_wgrad_x6: plane row length (M rounded up to kPackPad)
+  // k_wgrad_x6 chunked split-K (nchunk > 0): work item i = (chunk c = i / ntiles, tile
+  // t = i % ntiles) covers K-steps [c*kchunk, (c+1)*kchunk) of tile t and leaves one piece (slot
+  // 0 of worker i); NW = ntiles * nchunk items.  Chunk-major items give the workgroups of one XCD
+  // (consecutive items) the same pixel window of every tile: the window's dY and X rows stay in
+  // that XCD's L2 across all tiles and taps.
+  int nchunk, kchunk, ntiles;
 };
 
 constexpr int kWskBK = 64;
@@ -1509,10 +1515,12 @@ __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
   const int m = tm * BM + (g4 * 4) / BN, n = tn * BN + (g4 * 4) % BN;
   if (m >= a.M || n >= a.N) return;
   const int t = ((br * a.taps + tap) * a.tiles_n + tn) * a.tiles_m + tm;
-  const int w_lo = sk_worker_of(t * a.KS, a.T, a.NW);
-  const int w_hi = sk_worker_of((t + 1) * a.KS - 1, a.T, a.NW);
   const float4* __restrict__ part = reinterpret_cast<const float4*>(a.part);
+  // stream-K: the workers whose ranges touch tile t, in order; chunked: the items (c, t), c = 0..
+  const int w_lo = a.nchunk > 0 ? 0 : sk_worker_of(t * a.KS, a.T, a.NW);
+  const int w_hi = a.nchunk > 0 ? a.nchunk - 1 : sk_worker_of((t + 1) * a.KS - 1, a.T, a.NW);
   auto piece = [&](int wc) {
+    if (a.nchunk > 0) return part[(long long)(wc * a.ntiles + t) * a.slots * P4 + g4];
     const int slot = t - sk_start(wc, a.T, a.NW) / a.KS;
     return part[(long long)(wc * a.slots + slot) * P4 + g4];
   };
@@ -1599,7 +1607,16 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
   const int l32 = lane & 31, kh = lane >> 5;
   const int nb = gridDim.x, b = blockIdx.x;
   const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);  // XCD-aware worker id
-  const int it_begin = sk_start(w, a.T, a.NW), it_end = sk_start(w + 1, a.T, a.NW);
+  int it_begin, it_end;
+  if (a.nchunk > 0) {  // chunked split-K: one (chunk, tile) item per workgroup
+    if (w >= a.NW) return;
+    const int c = w / a.ntiles, t = w - c * a.ntiles;
+    it_begin = t * a.KS + c * a.kchunk;
+    it_end = t * a.KS + min(a.KS, (c + 1) * a.kchunk);
+  } else {
+    it_begin = sk_start(w, a.T, a.NW);
+    it_end = sk_start(w + 1, a.T, a.NW);
+  }
 
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.dyx6, (short)0, (int)min(0x7fffffffLL, (long long)a.KS * 6 * a.lda * 16), 0x00020000);

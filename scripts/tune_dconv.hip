@@ -142,6 +142,7 @@ float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, floa
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
     if (V == 1) hipLaunchKernelGGL(k_x6_sk2, dim3(sk.NW), dim3(256), 0, 0, a, sk);
+    else if (V == 3) hipLaunchKernelGGL(k_x6_sk4, dim3(sk.NW), dim3(512), 0, 0, a, sk);
     else if (V == 2) hipLaunchKernelGGL(k_x6_sk3, dim3(sk.NW), dim3(256), 0, 0, a, sk);
     else hipLaunchKernelGGL(k_x6_sk<EXP>, dim3(sk.NW), dim3(256), 0, 0, a, sk);
     if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, 128>), dim3(128 * 128 / 1024, tiles), dim3(256), 0, 0, a, sk);
@@ -207,6 +208,7 @@ float run_wgrad_sk(const Shape& sh, const float* x, const float* dy, float* dw, 
   const int tiles = a.tiles_m * a.tiles_n * 9;
   a.T = tiles * a.KS; a.NW = std::min(NWmax, a.T); a.cbranch = (long long)sh.cout * sh.cin * 9;
   a.slots = ((a.T + a.NW - 1) / a.NW + a.KS - 2) / a.KS + 1;
+  a.nchunk = 0; a.kchunk = 0; a.ntiles = tiles; a.dyx6 = nullptr; a.lda = 0;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int it = -2; it < iters; ++it) {
@@ -221,7 +223,7 @@ float run_wgrad_sk(const Shape& sh, const float* x, const float* dy, float* dw, 
 
 // k_split_rows + k_wgrad_x6 + k_wsk_reduce<128, 128> (the library's x6 weight gradient at >= 128 ch)
 float run_wgrad_x6(const Shape& sh, const float* x, const float* dy, float* dw, float* ws, int NWmax, int iters,
-                   bool split_only = false) {
+                   bool split_only = false, int chunks = 0) {
   const int P = sh.h * sh.w;
   WskArgs a;
   a.dy = dy; a.x = x; a.dw = dw; a.part = ws; a.M = sh.cout; a.N = sh.cin; a.H = sh.h; a.W = sh.w; a.P = P;
@@ -231,6 +233,13 @@ float run_wgrad_x6(const Shape& sh, const float* x, const float* dy, float* dw, 
   a.T = tiles * a.KS; a.NW = std::min(NWmax, a.T); a.cbranch = (long long)sh.cout * sh.cin * 9;
   a.slots = ((a.T + a.NW - 1) / a.NW + a.KS - 2) / a.KS + 1;
   a.lda = (sh.cout + 127) / 128 * 128;
+  a.nchunk = 0; a.kchunk = 0; a.ntiles = tiles;
+  if (chunks > 0) {  // chunked split-K: tiles x chunks items, one piece each
+    a.kchunk = (a.KS + chunks - 1) / chunks;
+    a.nchunk = (a.KS + a.kchunk - 1) / a.kchunk;
+    a.NW = tiles * a.nchunk;
+    a.slots = 1;
+  }
   const size_t piece_bytes = (size_t)a.NW * a.slots * 128 * 128 * 4;
   bf16x8* planes = (bf16x8*)((char*)ws + piece_bytes);
   a.dyx6 = planes;
@@ -342,7 +351,8 @@ int main(int argc, char** argv) {
   // "abl": k_x6_sk alone (no reduce) and its timing ablations, layer3 / layer4
   const bool abl = argc > 1 && std::string(argv[1]) == "abl";
   // "reg2": k_x6_sk2 (A fragments in registers) vs k_x6_sk vs the LDS-DMA kernel, vs fp64
-  const bool reg2 = argc > 1 && std::string(argv[1]) == "reg2";
+  const bool reg4 = argc > 1 && std::string(argv[1]) == "reg4";  // k_x6_sk4 (two K-groups, NW 256)
+  const bool reg2 = (argc > 1 && std::string(argv[1]) == "reg2") || reg4;
   const bool reg_mode = (argc > 1 && std::string(argv[1]) == "reg") || reg3 || abl || reg2;
   // "wx6": the register-staged x6 weight gradient (k_wgrad_x6) vs k_wgrad_sk's x6 form, vs fp64
   const bool wx6 = argc > 1 && std::string(argv[1]) == "wx6";
@@ -396,7 +406,14 @@ int main(int argc, char** argv) {
       float ms = run_x6reg<PW, 0, 2>(sh, x, wp, y, ws, NW, iters, lda); \
       err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
       printf("reg3 PW %d       NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, NW, ms * 1e3, gf / ms, mx, rms); }
-      if (reg2) {
+#define REG4(PW, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_x6reg<PW, 0, 3>(sh, x, wp, y, ws, NW, iters, lda); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
+      printf("reg4 PW %d       NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, NW, ms * 1e3, gf / ms, mx, rms); }
+      if (reg4) {
+        if (shape_pw) { OLD(true) REG2(true, 512) REG4(true, 256) }
+        else { OLD(false) REG2(false, 512) REG4(false, 256) }
+      } else if (reg2) {
         if (shape_pw) { OLD(true) REG(true, 512) REG2(true, 512) REG3(true, 512) }
         else { OLD(false) REG(false, 512) REG2(false, 512) REG3(false, 512) }
       } else if (abl) {
@@ -460,7 +477,16 @@ int main(int argc, char** argv) {
       float ms = run_wgrad_x6(sh, x, dy, dw, ws, NW, iters); \
       err64_wgrad(sh, hx, hdy, dw, &mx, &rms); \
       printf("wx6  (split+kernel+reduce) NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", NW, ms * 1e3, gf / ms, mx, rms); }
-      WX6(512) WX6(384) WX6(256)
+      WX6(512)
+#define WX6C(C) { CK(hipMemset(dw, 0, (size_t)sh.cout * sh.cin * 9 * 4)); \
+      float ms = run_wgrad_x6(sh, x, dy, dw, ws, 512, iters, false, C); \
+      err64_wgrad(sh, hx, hdy, dw, &mx, &rms); \
+      printf("wx6  chunked split-K  chunks %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", C, ms * 1e3, gf / ms, mx, rms); }
+      {
+        const int tiles = ((sh.cout + 127) / 128) * ((sh.cin + 127) / 128) * 9;
+        const int c1 = std::max(1, 512 / tiles), c2 = std::max(1, 1024 / tiles);
+        WX6C(c1) WX6C(c2)
+      }
       printf("k_split_rows alone: %.1f us\n", run_wgrad_x6(sh, x, dy, dw, ws, 512, iters, true) * 1e3);
       continue;
     }

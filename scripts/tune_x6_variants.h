@@ -660,4 +660,235 @@ __global__ void __launch_bounds__(256, 2) k_x6_sk3(FwdArgs a, SkArgs sk) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_x6_sk2 with two K-groups per workgroup: 512 threads, one workgroup per CU (NW = 256), waves
+// 0-3 and 4-7 each run the k_x6_sk2 loop on one half of the worker's K range of a tile, with
+// LDS rings of their own (2 x 48 KB), and the two partial tiles are summed through LDS before the
+// piece / output store.  Stream-K leaves ~NW + tiles pieces: half the workers, half the piece
+// bytes (and reduce reads) of the 512-worker kernels at the same occupancy.
+__global__ void __launch_bounds__(512, 1) k_x6_sk4(FwdArgs a, SkArgs sk) {
+  constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
+  constexpr int KV = 6 * 128;
+  constexpr int STAGE = 2 * KV;
+  __shared__ __attribute__((aligned(16))) bf16x8 smem[2 * 2 * STAGE];  // 96 KB: the only LDS object
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int grp = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int gt = tid & 255;
+  const int gw = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int wm = (gw >> 1) * 64, wn = (gw & 1) * 64;
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
+  const int T = sk.T;
+  const int it_begin = sk_start(w, T, sk.NW), it_end = sk_start(w + 1, T, sk.NW);
+
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * 6 * a.lda * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  const unsigned chan_bytes = (unsigned)a.P * 4u;
+  const unsigned a_plane_bytes = (unsigned)a.lda * 16u;
+  const bool full_cb = (a.cimg & (kCB - 1)) == 0;
+  const int bn = gt & 127, bh = gt >> 7;
+  bf16x8* gsm = smem + grp * 2 * STAGE;  // this group's ring
+
+  f32x16 acc[TM][TN];
+  for (int it = it_begin; it < it_end;) {
+    const int t = (unsigned)it / (unsigned)sk.KS;
+    const int k_a = it - t * sk.KS;
+    const int k_b = min(sk.KS, k_a + (it_end - it));
+    const int nst = k_b - k_a;
+    it += nst;
+    int tm, tn;
+    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    // this group's K-steps: group 0 the first ceil(nst/2), group 1 the rest
+    const int h0 = (nst + 1) >> 1;
+    const int g_a = grp ? k_a + h0 : k_a;
+    const int g_n = grp ? nst - h0 : h0;
+    const int g_b = g_a + g_n;
+    const int nstages = (h0 + 1) >> 1;  // both groups run as many barriers as group 0
+    const int p = n0 + bn;
+    const bool pin = p < a.P;
+    const int py = p / a.W, px = p - py * a.W;
+    int c_cb, c_tap;
+    {
+      const int tq = g_a / a.ncb;
+      c_cb = g_a - tq * a.ncb;
+      c_tap = tq;
+    }
+    unsigned vrow = OOB;
+    auto set_tap = [&](int tq) {
+      const int br = tq / a.taps;
+      const int tp = tq - br * a.taps;
+      const int d = br ? a.dil1 : a.dil0;
+      const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
+      const bool v = pin && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
+      vrow = v ? (unsigned)((p + dh * a.W + dw) * 4) : OOB;
+    };
+    if (g_n > 0) set_tap(c_tap);
+    float rbv[16];
+    auto loadB = [&](int j0) {
+      const int c0 = c_cb * kCB + 8 * bh;
+      if (full_cb) {
+        const unsigned vb = vrow + (unsigned)c0 * chan_bytes;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          rbv[j0 + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vb, (int)(j * chan_bytes), 0));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const unsigned cofs = c0 + j < a.cimg ? (unsigned)(c0 + j) * chan_bytes : OOB;
+          rbv[j0 + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vrow + cofs, 0, 0));
+        }
+      }
+      if (++c_cb == a.ncb) {
+        c_cb = 0;
+        if (++c_tap * a.ncb < a.ksteps) set_tap(c_tap);
+      }
+    };
+    auto storeB = [&](int buf, int j0, int kk) {
+      Split3 sp;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) split3_set(sp, j, rbv[j0 + j]);
+      bf16x8* Bs = gsm + buf * STAGE + kk * KV;
+      Bs[bh * 128 + bn] = sp.hi;
+      Bs[(2 + bh) * 128 + bn] = sp.mid;
+      Bs[(4 + bh) * 128 + bn] = sp.lo;
+    };
+    const unsigned a_voff = (unsigned)((kh * a.lda + m0 + wm + l32) * 16);
+    u32x4 A0[TM][3], A1[TM][3];
+    auto loadA = [&](u32x4 (&A)[TM][3], int ks) {
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          A[ii][q] = __builtin_amdgcn_raw_buffer_load_b128(rx, a_voff + ii * 512,
+                                                           (int)((unsigned)(ks * 6 + 2 * q) * a_plane_bytes), 0);
+    };
+    auto compute = [&](const bf16x8* Bs, const u32x4 (&A)[TM][3]) {
+      Split3 bv[TN];
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) {
+        const int n = wn + jj * 32 + l32;
+        bv[jj].hi = Bs[kh * 128 + n];
+        bv[jj].mid = Bs[(2 + kh) * 128 + n];
+        bv[jj].lo = Bs[(4 + kh) * 128 + n];
+      }
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) {
+        union { u32x4 u; bf16x8 h; } c0, c1, c2;
+        c0.u = A[ii][0]; c1.u = A[ii][1]; c2.u = A[ii][2];
+        Split3 av;
+        av.hi = c0.h; av.mid = c1.h; av.lo = c2.h;
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) acc[ii][jj] = mfma_x6(av, bv[jj], acc[ii][jj]);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    __syncthreads();  // the previous segment's LDS reads (and the partial-sum exchange) are done
+    if (g_n > 0) {
+      loadB(0);
+      if (g_n > 1) loadB(8);
+      loadA(A0, g_a);
+      storeB(0, 0, 0);
+      if (g_n > 1) storeB(0, 8, 1);
+    }
+    __syncthreads();
+    int ks = g_a;
+    for (int s = 0; s < nstages; ++s) {
+      const int left = g_n - 2 * s;  // this group's K-steps from this stage on (<= 0: idle)
+      const int nxt = left - 2;
+      if (nxt > 0) {
+        loadB(0);
+        if (nxt > 1) loadB(8);
+      }
+      const bf16x8* Bs = gsm + (s & 1) * STAGE;
+      if (left > 0) {
+        if (ks + 1 < g_b) loadA(A1, ks + 1);
+        compute(Bs, A0);
+        ++ks;
+        if (left > 1) {
+          if (ks + 1 < g_b) loadA(A0, ks + 1);
+          compute(Bs + KV, A1);
+          ++ks;
+        }
+      }
+      if (nxt > 0) {
+        storeB((s + 1) & 1, 0, 0);
+        if (nxt > 1) storeB((s + 1) & 1, 8, 1);
+      }
+      __syncthreads();
+    }
+    // group 1's partial tile -> LDS (each wave its 64x64 quadrant, lane-linear), group 0 adds it
+    float* xs = reinterpret_cast<float*>(smem);
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xs[((gw * 4 + i * 2 + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (grp == 1) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] += xs[((gw * 4 + i * 2 + j) * 16 + r) * 64 + lane];
+
+    constexpr int PSZ = BM * BN;
+    if (k_a > 0 || k_b < sk.KS) {
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)sk.part, (short)0, (int)min(0x7fffffffLL, (long long)sk.NW * 2 * PSZ * 4), 0x00020000);
+      const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int nl = wn + j * 32 + l32;
+          const int ml = wm + i * 32 + 4 * kh;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ro = (r & 3) + 8 * (r >> 2);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rp,
+                                                  pbase + (unsigned)(((ml + ro) * BN + nl) * 4), 0, 0);
+          }
+        }
+      continue;
+    }
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn + j * 32 + l32;
+        const int mrow = m0 + wm + i * 32 + 4 * kh;
+        const unsigned voff = n < a.P ? (unsigned)((mrow * a.P + n) * 4) : OOB;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          float v = acc[i][j][r];
+          if (a.bias && mrow + ro < a.M) {
+            float bsum = a.bias[mrow + ro];
+            for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + mrow + ro];
+            v += bsum;
+          }
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
+                                                mrow + ro < a.M ? voff + ro * a.P * 4 : OOB, 0, 0);
+        }
+      }
+  }
+}
+
 }  // namespace msl
