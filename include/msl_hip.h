@@ -78,6 +78,22 @@ int msl_conv_set_pack_form(int form);
  * pack followed by its bf16x6 planes (split once here, read by the bf16x6 fp32 form).  All
  * nbranch branches are packed by one call (branch b's weights at w + b*branch_stride floats). */
 long long msl_dconv_packed_elems(int nbranch, int cin, int cout, int for_dgrad);
+/* One weight pack of a batch: exactly what msl_dconv_pack (taps 9) / msl_pconv_pack (taps 1,
+ * nbranch 1, branch_stride 0) would write into `packed`. */
+typedef struct msl_pack_job {
+  const float* w;
+  long long branch_stride;
+  float* packed;
+  int nbranch, cin, cout, for_dgrad;
+} msl_pack_job;
+/* Blocks of one job in msl_conv_pack_many (-1 on bad arguments). */
+long long msl_conv_pack_blocks(int nbranch, int taps, int cin, int cout, int for_dgrad);
+/* Every job of `jobs` (device array, all with the same tap count) in one launch: job j runs blocks
+ * block_start[j] .. block_start[j+1]-1 (device array of njobs+1 ascending offsets built with
+ * msl_conv_pack_blocks; block_start[njobs] = total_blocks).  Byte-identical to the per-job calls;
+ * replaces the ~120 per-conv pack launches of a training step by two. */
+int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, int njobs, int taps,
+                       long long total_blocks, msl_stream_t stream);
 int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin, int cout,
                    int for_dgrad, float* packed, msl_stream_t stream);
 

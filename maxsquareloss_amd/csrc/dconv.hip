@@ -102,13 +102,13 @@ __global__ void __launch_bounds__(256) k_pack(const float* __restrict__ w, long 
 // (64-row chunks: 64 blocks for that weight, 24 us - too few workgroups.)
 constexpr int kPackTileM = 16;
 
+// One (16-row m chunk, 16-channel block, branch) block of the pack + split; s = the block's LDS tile.
 template <int TAPS>
-__global__ void __launch_bounds__(256) k_pack_split(const float* __restrict__ w, long long branch_stride,
-                                                    int cin, int cout, int for_dgrad, int ncb, int lda,
-                                                    int split, float* __restrict__ out,
-                                                    __bf16* __restrict__ planes) {
-  __shared__ float s[kCB * TAPS][kPackTileM + 1];  // [cl*TAPS + t][ml], t = packed tap index
-  const int m0 = blockIdx.x * kPackTileM, cb = blockIdx.y, b = blockIdx.z;
+__device__ __forceinline__ void pack_split_block(const float* __restrict__ w, long long branch_stride, int cin,
+                                                 int cout, int for_dgrad, int ncb, int lda, int split,
+                                                 float* __restrict__ out, __bf16* __restrict__ planes, int mx,
+                                                 int cb, int b, float (*s)[kPackTileM + 1]) {
+  const int m0 = mx * kPackTileM;
   const int cimg = for_dgrad ? cout : cin;
   const int mreal = for_dgrad ? cin : cout;
   const float* wb = w + (long long)b * branch_stride;
@@ -150,6 +150,44 @@ __global__ void __launch_bounds__(256) k_pack_split(const float* __restrict__ w,
     pl[row + 2LL * lda] = sp.mid;
     pl[row + 4LL * lda] = sp.lo;
   }
+}
+
+template <int TAPS>
+__global__ void __launch_bounds__(256) k_pack_split(const float* __restrict__ w, long long branch_stride,
+                                                    int cin, int cout, int for_dgrad, int ncb, int lda,
+                                                    int split, float* __restrict__ out,
+                                                    __bf16* __restrict__ planes) {
+  __shared__ float s[kCB * TAPS][kPackTileM + 1];  // [cl*TAPS + t][ml], t = packed tap index
+  pack_split_block<TAPS>(w, branch_stride, cin, cout, for_dgrad, ncb, lda, split, out, planes, blockIdx.x,
+                         blockIdx.y, blockIdx.z, s);
+}
+
+// Every weight pack of a step in one launch (per tap count): block b runs block b - start[j] of
+// job j (start[] ascending, start[njobs] = the total), each job exactly as msl_*_pack would.
+template <int TAPS>
+__global__ void __launch_bounds__(256) k_pack_split_many(const msl_pack_job* __restrict__ jobs,
+                                                         const long long* __restrict__ start, int njobs) {
+  __shared__ float s[kCB * TAPS][kPackTileM + 1];
+  const long long b = blockIdx.x;
+  int lo = 0, hi = njobs - 1;  // the last job with start <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (start[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const msl_pack_job jb = jobs[lo];
+  const int cimg = jb.for_dgrad ? jb.cout : jb.cin;
+  const int m = jb.for_dgrad ? jb.cin : jb.cout;
+  const int lda = (m + kPackPad - 1) / kPackPad * kPackPad;
+  const int ncb = (cimg + kCB - 1) / kCB;
+  const int nmx = lda / kPackTileM;
+  const long long local = b - start[lo];
+  const int mx = (int)(local % nmx);
+  const long long rest = local / nmx;
+  const int cb = (int)(rest % ncb), br = (int)(rest / ncb);
+  const long long f32 = (long long)jb.nbranch * ncb * TAPS * kCB * lda;
+  pack_split_block<TAPS>(jb.w, jb.branch_stride, jb.cin, jb.cout, jb.for_dgrad, ncb, lda, m > 64, jb.packed,
+                         reinterpret_cast<__bf16*>(jb.packed + f32), mx, cb, br, s);
 }
 
 // ---------------------------------------------------------------- planning
@@ -600,6 +638,27 @@ int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin
                    int for_dgrad, float* packed, msl_stream_t stream) {
   if (bad_dims(nbranch, cin, cout, 1, 1) || !w || !packed) return MSL_ERR_ARG;
   return pack(w, branch_stride, nbranch, 9, cin, cout, for_dgrad, packed, as_stream(stream));
+}
+
+long long msl_conv_pack_blocks(int nbranch, int taps, int cin, int cout, int for_dgrad) {
+  if (bad_dims(nbranch, cin, cout, 1, 1) || (taps != 1 && taps != 9)) return -1;
+  const int cimg = for_dgrad ? cout : cin;
+  const int m = for_dgrad ? cin : cout;
+  return (long long)(pad_to(m, kPackPad) / kPackTileM) * cdiv(cimg, kCB) * nbranch;
+}
+
+int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, int njobs, int taps,
+                       long long total_blocks, msl_stream_t stream) {
+  if (!jobs || !block_start || njobs < 1 || total_blocks < 1 || total_blocks >= (1LL << 31) ||
+      (taps != 1 && taps != 9))
+    return MSL_ERR_ARG;
+  hipStream_t st = as_stream(stream);
+  if (taps == 9)
+    hipLaunchKernelGGL(k_pack_split_many<9>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs);
+  else
+    hipLaunchKernelGGL(k_pack_split_many<1>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
 }
 
 size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w) {

@@ -21,6 +21,8 @@ SIGNATURES = {
     "msl_status_string": (ctypes.c_char_p, [c_int]),
     "msl_dconv_packed_elems": (c_ll, [c_int, c_int, c_int, c_int]),
     "msl_dconv_pack": (c_int, [c_p, c_ll, c_int, c_int, c_int, c_int, c_p, c_p]),
+    "msl_conv_pack_blocks": (c_ll, [c_int] * 5),
+    "msl_conv_pack_many": (c_int, [c_p, c_p, c_int, c_int, c_ll, c_p]),
     "msl_dconv_fwd_workspace": (c_sz, [c_int] * 5),
     "msl_counter_elems": (c_int, []),
     "msl_conv_set_f32_form": (c_int, [c_int]),

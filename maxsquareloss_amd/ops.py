@@ -102,9 +102,17 @@ class PackCache:
         self.pointwise = pointwise
         self.key = {0: None, 1: None}
         self.buf = {0: None, 1: None}
+        self.used = {0: False, 1: False}  # read by PackBatch: the directions a step consumes
+        self.meta = {0: None, 1: None}    # (weights, cin, cout) of the last get()
+
+    @staticmethod
+    def key_of(weights):
+        return tuple((w.data_ptr(), w._version) for w in weights)
 
     def get(self, weights, cin, cout, for_dgrad):
-        key = tuple((w.data_ptr(), w._version) for w in weights)
+        key = self.key_of(weights)
+        self.used[for_dgrad] = True
+        self.meta[for_dgrad] = (list(weights), cin, cout)
         if self.key[for_dgrad] != key:
             lib = hip.load()
             nb = len(weights)
@@ -130,6 +138,97 @@ class PackCache:
             self.buf[for_dgrad] = buf
             self.key[for_dgrad] = key
         return self.buf[for_dgrad]
+
+
+class PackBatch:
+    """Every weight pack of a model in two launches (one per tap count) instead of one per conv
+    and direction (~120 per training step): `run()` after the optimizer step packs each
+    (PackCache, direction) that the previous step consumed, when all of them are stale, through
+    msl_conv_pack_many (byte-identical to the per-conv calls), and marks them fresh; anything else
+    (a partial update, a new input size, the first step) is left to PackCache.get's lazy path.
+    The job tables are built outside graph capture (utils/graph.py captures iteration 1, after
+    iteration 0 built them eagerly)."""
+
+    _JOB = None
+
+    def __init__(self, module):
+        self.caches = [m._pack for m in module.modules() if isinstance(getattr(m, "_pack", None), PackCache)]
+        self.sig = None
+        self.tables = {}
+        self.launches = 0
+
+    @classmethod
+    def _dtype(cls):
+        import numpy as np
+        if cls._JOB is None:
+            cls._JOB = np.dtype([("w", "<u8"), ("bs", "<i8"), ("packed", "<u8"), ("nb", "<i4"), ("cin", "<i4"),
+                                 ("cout", "<i4"), ("fd", "<i4")])
+            assert cls._JOB.itemsize == 40  # sizeof(msl_pack_job)
+        return cls._JOB
+
+    def _jobs(self):
+        out = []
+        for c in self.caches:
+            for d in (0, 1):
+                if c.used[d] and c.buf[d] is not None and c.meta[d] is not None:
+                    out.append((c, d))
+        return out
+
+    def _build(self, jobs, device):
+        import numpy as np
+        lib = hip.load()
+        tables = {}
+        for taps in (9, 1):
+            sel = [(c, d) for c, d in jobs if (1 if c.pointwise else 9) == taps]
+            if not sel:
+                continue
+            rec = np.zeros(len(sel), dtype=self._dtype())
+            starts = np.zeros(len(sel) + 1, dtype=np.int64)
+            for i, (c, d) in enumerate(sel):
+                ws, cin, cout = c.meta[d]
+                nb = len(ws)
+                stride = 0
+                if nb == 2:
+                    diff = ws[1].data_ptr() - ws[0].data_ptr()
+                    if diff % 4:
+                        return None
+                    stride = diff // 4
+                if any(not w.is_contiguous() for w in ws):
+                    return None
+                rec[i] = (ws[0].data_ptr(), stride, c.buf[d].data_ptr(), nb, cin, cout, d)
+                nblk = lib.msl_conv_pack_blocks(nb, taps, cin, cout, d)
+                if nblk < 1:
+                    return None
+                starts[i + 1] = starts[i] + nblk
+            jt = torch.from_numpy(rec.view(np.uint8).copy()).to(device)
+            st = torch.from_numpy(starts).to(device)
+            tables[taps] = (jt, st, len(sel), int(starts[-1]))
+        return tables
+
+    def run(self):
+        jobs = self._jobs()
+        if not jobs:
+            return False
+        keys = [c.key_of(c.meta[d][0]) for c, d in jobs]
+        if any(c.key[d] == k for (c, d), k in zip(jobs, keys)):
+            return False  # not everything changed: the lazy path packs what did
+        sig = tuple((id(c), d, c.buf[d].data_ptr(), c.buf[d].numel(), tuple(w.data_ptr() for w in c.meta[d][0]),
+                     c.meta[d][1], c.meta[d][2]) for c, d in jobs)
+        if sig != self.sig:
+            if torch.cuda.is_current_stream_capturing():
+                return False
+            tables = self._build(jobs, jobs[0][0].buf[jobs[0][1]].device)
+            if tables is None:
+                return False
+            self.tables, self.sig = tables, sig
+        lib = hip.load()
+        s = hip.stream_ptr()
+        for taps, (jt, st, n, total) in self.tables.items():
+            hip.check(lib.msl_conv_pack_many(jt.data_ptr(), st.data_ptr(), n, taps, total, s), "msl_conv_pack_many")
+        for (c, d), k in zip(jobs, keys):
+            c.key[d] = k
+        self.launches += 1
+        return True
 
 
 # --------------------------------------------------------------------------- dilated conv

@@ -117,6 +117,7 @@ class UDATrainer(Trainer):
             self.reducer.finish()
         self.optimizer.step()
         self.optimizer.zero_grad()
+        self.packer.run()  # the next iteration's weight packs, batched (ops.PackBatch)
 
     # ---------------------------------------------------------------- loop
     def main(self):

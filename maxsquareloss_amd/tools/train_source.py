@@ -86,6 +86,7 @@ class Trainer:
         self.optimizer = SGD(lr=self.args.lr, params=self.params, momentum=self.args.momentum,
                              weight_decay=self.args.weight_decay)
         self.reducer = GradReducer(self.optimizer) if self.world > 1 else None
+        self.packer = ops.PackBatch(self.model)  # every weight pack of a step in two launches
 
         h, w = self.args.crop_size[1], self.args.crop_size[0]
         self.dataloader = SyntheticDomain(h, w, self.args.num_classes, self.args.synthetic_images,
@@ -151,6 +152,7 @@ class Trainer:
         if self.reducer:
             self.reducer.finish()
         self.optimizer.step()
+        self.packer.run()
         return cur_loss
 
     # ------------------------------------------------------------------ checkpoints

@@ -143,6 +143,7 @@ float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, floa
     if (it == 0) CK(hipEventRecord(e0));
     if (V == 1) hipLaunchKernelGGL(k_x6_sk2, dim3(sk.NW), dim3(256), 0, 0, a, sk);
     else if (V == 3) hipLaunchKernelGGL(k_x6_sk4, dim3(sk.NW), dim3(512), 0, 0, a, sk);
+    else if (V == 4) hipLaunchKernelGGL(k_x6_sk5, dim3(sk.NW), dim3(512), 0, 0, a, sk);
     else if (V == 2) hipLaunchKernelGGL(k_x6_sk3, dim3(sk.NW), dim3(256), 0, 0, a, sk);
     else hipLaunchKernelGGL(k_x6_sk<EXP>, dim3(sk.NW), dim3(256), 0, 0, a, sk);
     if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, 128>), dim3(128 * 128 / 1024, tiles), dim3(256), 0, 0, a, sk);
@@ -352,7 +353,8 @@ int main(int argc, char** argv) {
   const bool abl = argc > 1 && std::string(argv[1]) == "abl";
   // "reg2": k_x6_sk2 (A fragments in registers) vs k_x6_sk vs the LDS-DMA kernel, vs fp64
   const bool reg4 = argc > 1 && std::string(argv[1]) == "reg4";  // k_x6_sk4 (two K-groups, NW 256)
-  const bool reg2 = (argc > 1 && std::string(argv[1]) == "reg2") || reg4;
+  const bool reg5 = argc > 1 && std::string(argv[1]) == "reg5";  // k_x6_sk5 (16x16x32, 8 waves, NW 256)
+  const bool reg2 = (argc > 1 && std::string(argv[1]) == "reg2") || reg4 || reg5;
   const bool reg_mode = (argc > 1 && std::string(argv[1]) == "reg") || reg3 || abl || reg2;
   // "wx6": the register-staged x6 weight gradient (k_wgrad_x6) vs k_wgrad_sk's x6 form, vs fp64
   const bool wx6 = argc > 1 && std::string(argv[1]) == "wx6";
@@ -410,7 +412,14 @@ int main(int argc, char** argv) {
       float ms = run_x6reg<PW, 0, 3>(sh, x, wp, y, ws, NW, iters, lda); \
       err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
       printf("reg4 PW %d       NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, NW, ms * 1e3, gf / ms, mx, rms); }
-      if (reg4) {
+#define REG5(PW, NW) { CK(hipMemset(y, 0, (size_t)sh.cout * P * 4)); \
+      float ms = run_x6reg<PW, 0, 4>(sh, x, wp, y, ws, NW, iters, lda); \
+      err64_fwd(sh, hx, hw, lda, y, &mx, &rms, PW ? 1 : 9); \
+      printf("reg5 PW %d       NW %4d : %8.1f us %7.1f TF  err64 max %.2e rms %.2e\n", PW, NW, ms * 1e3, gf / ms, mx, rms); }
+      if (reg5) {
+        if (shape_pw) { OLD(true) REG5(true, 256) }
+        else { OLD(false) REG5(false, 256) }
+      } else if (reg4) {
         if (shape_pw) { OLD(true) REG2(true, 512) REG4(true, 256) }
         else { OLD(false) REG2(false, 512) REG4(false, 256) }
       } else if (reg2) {

@@ -891,4 +891,188 @@ __global__ void __launch_bounds__(512, 1) k_x6_sk4(FwdArgs a, SkArgs sk) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 16x16x32 form for the clock: 512 threads (8 waves of 32x64, one workgroup per CU, NW = 256),
+// A fragments straight from the planes into registers (a stage = two K-steps = one K = 32 MFMA
+// slab), B split once into LDS by all 512 threads.  Per wave and stage: 2 row blocks x 4 column
+// blocks x 6 products of v_mfma_f32_16x16x32_bf16 (the same FLOPs per SIMD as two 32x32x16
+// waves of 64x64), 24 A + 48 B fragment registers, 32 accumulators.
+__global__ void __launch_bounds__(512, 1) k_x6_sk5(FwdArgs a, SkArgs sk) {
+  constexpr int BM = 128, BN = 128, TI = 2, TJ = 4;
+  constexpr int KV = 6 * 128;
+  constexpr int STAGE = 2 * KV;
+  __shared__ __attribute__((aligned(16))) bf16x8 smem[2 * STAGE];  // 48 KB: the only LDS object
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
+  const int T = sk.T;
+  const int it_begin = sk_start(w, T, sk.NW), it_end = sk_start(w + 1, T, sk.NW);
+
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * 6 * a.lda * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  const unsigned chan_bytes = (unsigned)a.P * 4u;
+  const unsigned a_plane_bytes = (unsigned)a.lda * 16u;
+  const bool full_cb = (a.cimg & (kCB - 1)) == 0;
+  // B staging: thread -> pixel column bn, K-step kk of the stage, channel half bh
+  const int bn = tid & 127, bkk = (tid >> 7) & 1, bh = tid >> 8;
+
+  f32x4 acc[TI][TJ];
+  for (int it = it_begin; it < it_end;) {
+    const int t = (unsigned)it / (unsigned)sk.KS;
+    const int k_a = it - t * sk.KS;
+    const int k_b = min(sk.KS, k_a + (it_end - it));
+    const int nst = k_b - k_a;
+    it += nst;
+    int tm, tn;
+    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int p = n0 + bn;
+    const bool pin = p < a.P;
+    const int py = p / a.W, px = p - py * a.W;
+    // this thread's B cursor runs over the K-steps k_a + bkk, k_a + bkk + 2, ...
+    auto vrow_of = [&](int ks) -> unsigned {
+      const int tq = ks / a.ncb;
+      const int br = tq / a.taps;
+      const int tp = tq - br * a.taps;
+      const int d = br ? a.dil1 : a.dil0;
+      const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
+      const bool v = pin && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
+      return v ? (unsigned)((p + dh * a.W + dw) * 4) : OOB;
+    };
+    float rbv[8];
+    auto loadB = [&](int ks) {  // K-step ks (this thread's half of it), zeros past k_b
+      if (ks >= k_b) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rbv[j] = 0.f;
+        return;
+      }
+      const unsigned vrow = vrow_of(ks);
+      const int c0 = (ks - (ks / a.ncb) * a.ncb) * kCB + 8 * bh;
+      if (full_cb) {
+        const unsigned vb = vrow + (unsigned)c0 * chan_bytes;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          rbv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vb, (int)(j * chan_bytes), 0));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const unsigned cofs = c0 + j < a.cimg ? (unsigned)(c0 + j) * chan_bytes : OOB;
+          rbv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vrow + cofs, 0, 0));
+        }
+      }
+    };
+    auto storeB = [&](int buf) {
+      Split3 sp;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) split3_set(sp, j, rbv[j]);
+      bf16x8* Bs = smem + buf * STAGE + bkk * KV;
+      Bs[bh * 128 + bn] = sp.hi;
+      Bs[(2 + bh) * 128 + bn] = sp.mid;
+      Bs[(4 + bh) * 128 + bn] = sp.lo;
+    };
+    const unsigned a_voff = (unsigned)((((g >> 1) * 6 + (g & 1)) * a.lda + m0 + wr * 32 + l16) * 16);
+    u32x4 A0[TI][3], A1[TI][3];
+    auto loadA = [&](u32x4 (&A)[TI][3], int ks) {  // the stage starting at K-step ks
+      const bool two = ks + 1 < k_b;
+#pragma unroll
+      for (int ii = 0; ii < TI; ++ii)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          A[ii][q] = __builtin_amdgcn_raw_buffer_load_b128(
+              rx, (two || g < 2) ? a_voff + ii * 256 : OOB, (int)((unsigned)(ks * 6 + 2 * q) * a_plane_bytes), 0);
+    };
+    auto compute = [&](const bf16x8* Bs, const u32x4 (&A)[TI][3]) {
+      Split3 bv[TJ];
+#pragma unroll
+      for (int jj = 0; jj < TJ; ++jj) {
+        const bf16x8* src = Bs + (g >> 1) * KV + (g & 1) * 128 + wc * 64 + jj * 16 + l16;
+        bv[jj].hi = src[0];
+        bv[jj].mid = src[256];
+        bv[jj].lo = src[512];
+      }
+#pragma unroll
+      for (int ii = 0; ii < TI; ++ii) {
+        union { u32x4 u; bf16x8 h; } c0, c1, c2;
+        c0.u = A[ii][0]; c1.u = A[ii][1]; c2.u = A[ii][2];
+        Split3 av;
+        av.hi = c0.h; av.mid = c1.h; av.lo = c2.h;
+#pragma unroll
+        for (int jj = 0; jj < TJ; ++jj) acc[ii][jj] = mfma16_x6(av, bv[jj], acc[ii][jj]);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    loadB(k_a + bkk);
+    loadA(A0, k_a);
+    storeB(0);
+    __syncthreads();
+    const int nstg = (nst + 1) >> 1;
+    for (int s = 0; s < nstg; ++s) {
+      const int ks = k_a + 2 * s;
+      const bool more = s + 1 < nstg;
+      if (more) loadB(ks + 2 + bkk);
+      const bf16x8* Bs = smem + (s & 1) * STAGE;
+      if (s & 1) {
+        if (more) loadA(A0, ks + 2);
+        compute(Bs, A1);
+      } else {
+        if (more) loadA(A1, ks + 2);
+        compute(Bs, A0);
+      }
+      if (more) storeB((s + 1) & 1);
+      __syncthreads();
+    }
+
+    constexpr int PSZ = BM * BN;
+    if (k_a > 0 || k_b < sk.KS) {
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)sk.part, (short)0, (int)min(0x7fffffffLL, (long long)sk.NW * 2 * PSZ * 4), 0x00020000);
+      const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int nl = wc * 64 + j * 16 + l16;
+          const int ml = wr * 32 + i * 16 + 4 * g;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rp,
+                                                  pbase + (unsigned)(((ml + r) * BN + nl) * 4), 0, 0);
+        }
+      continue;
+    }
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int n = n0 + wc * 64 + j * 16 + l16;
+        const int mrow = m0 + wr * 32 + i * 16 + 4 * g;
+        const unsigned voff = n < a.P ? (unsigned)((mrow * a.P + n) * 4) : OOB;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r];
+          if (a.bias && mrow + r < a.M) {
+            float bsum = a.bias[mrow + r];
+            for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + mrow + r];
+            v += bsum;
+          }
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
+                                                mrow + r < a.M ? voff + r * a.P * 4 : OOB, 0, 0);
+        }
+      }
+  }
+}
+
 }  // namespace msl

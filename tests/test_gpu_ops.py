@@ -423,3 +423,79 @@ def test_pack_forms_identical(kind, nb, cin, cout, for_dgrad):
     finally:
         lib.msl_conv_set_pack_form(1)
     assert torch.equal(bufs[0].view(torch.int32), bufs[1].view(torch.int32))
+
+
+def test_pack_batch_matches_per_conv_packs():
+    """ops.PackBatch (msl_conv_pack_many: every pack of a step in one launch per tap count) writes
+    exactly the bytes of the per-conv msl_*_pack calls, for 9- and 1-tap packs, both directions,
+    a 2-branch ASPP pack and M <= 64 (no planes) - and only once every consumed pack is stale."""
+    import torch.nn as nn
+    g = torch.Generator().manual_seed(5)
+
+    class Holder(nn.Module):
+        def __init__(self, weights, cin, cout, pointwise):
+            super().__init__()
+            self.ws = nn.ParameterList([nn.Parameter(w) for w in weights])
+            self._pack = ops.PackCache(pointwise=pointwise)
+            self.dims = (cin, cout)
+
+        def use(self):
+            cin, cout = self.dims
+            for d in (0, 1):
+                self._pack.get(list(self.ws), cin, cout, d)
+
+    specs = [([torch.randn(256, 256, 3, 3, generator=g)], 256, 256, False),
+             ([torch.randn(64, 40, 3, 3, generator=g)], 40, 64, False),
+             (list(torch.randn(2, 19, 1024, 3, 3, generator=g).unbind(0)), 1024, 19, False),
+             ([torch.randn(1024, 256, 1, 1, generator=g)], 256, 1024, True),
+             ([torch.randn(70, 130, 1, 1, generator=g)], 130, 70, True)]
+    hs = nn.ModuleList([Holder(*s) for s in specs]).to(DEV)
+    for h in hs:  # the 2-branch pack reads branch 1 at a fixed stride from branch 0: one storage
+        if len(h.ws) == 2:
+            both = torch.stack([h.ws[0].data, h.ws[1].data])
+            h.ws[0].data, h.ws[1].data = both[0], both[1]
+    for h in hs:
+        h.use()  # lazy packs; marks both directions used
+    batch = ops.PackBatch(hs)
+    assert len(batch.caches) == len(specs)
+    with torch.no_grad():
+        for h in hs:
+            for w in h.ws:
+                w.mul_(-1.5)
+    for h in hs:
+        h.use()  # lazy repack of the new weights
+    torch.cuda.synchronize()
+    ref = [{d: h._pack.buf[d].clone() for d in (0, 1)} for h in hs]
+    assert not batch.run()  # nothing stale: no launch
+    with torch.no_grad():
+        hs[0].ws[0].mul_(1.0)  # one stale pack only: left to the lazy path
+    assert not batch.run()
+    with torch.no_grad():
+        for h in hs:
+            for w in h.ws:
+                w.mul_(-2.0)
+            for d in (0, 1):
+                h._pack.buf[d].fill_(float("nan"))
+    assert batch.run() and batch.launches == 1
+    with torch.no_grad():
+        for h in hs:
+            for w in h.ws:
+                w.mul_(-0.5)  # back to the values of the reference packs (x(-2)x(-0.5) = 1)
+            for d in (0, 1):
+                h._pack.buf[d].fill_(float("nan"))
+    assert batch.run() and batch.launches == 2
+    torch.cuda.synchronize()
+    for h, r in zip(hs, ref):
+        for d in (0, 1):
+            total = ops.hip.load().msl_dconv_packed_elems(len(h.ws), h.dims[0], h.dims[1], d) if not h._pack.pointwise \
+                else ops.hip.load().msl_pconv_packed_elems(h.dims[0], h.dims[1], d)
+            m = h.dims[1] if d == 0 else h.dims[0]
+            n = total if m > 64 else total * 2 // 5  # M <= 64: no planes behind the fp32 pack
+            assert torch.equal(h._pack.buf[d][:n].view(torch.int32), r[d][:n].view(torch.int32)), (h.dims, d)
+            # the per-conv calls never touch the planes region of an M <= 64 pack; neither does the batch
+            if m <= 64:
+                assert torch.isnan(h._pack.buf[d][n:]).all()
+            # lazy get() finds them fresh: no repack
+            key = h._pack.key[d]
+            h._pack.get(list(h.ws), h.dims[0], h.dims[1], d)
+            assert h._pack.key[d] == key
