@@ -142,12 +142,13 @@ class PackCache:
 
 class PackBatch:
     """Every weight pack of a model in two launches (one per tap count) instead of one per conv
-    and direction (~120 per training step): `run()` after the optimizer step packs each
-    (PackCache, direction) that the previous step consumed, when all of them are stale, through
-    msl_conv_pack_many (byte-identical to the per-conv calls), and marks them fresh; anything else
-    (a partial update, a new input size, the first step) is left to PackCache.get's lazy path.
-    The job tables are built outside graph capture (utils/graph.py captures iteration 1, after
-    iteration 0 built them eagerly)."""
+    and direction (~130 per training step): `run()` after the optimizer step packs each stale
+    (PackCache, direction) that an earlier step consumed through msl_conv_pack_many
+    (byte-identical to the per-conv calls) and marks it fresh.  The set of stale packs is the
+    same every step (the parameters the loss reaches: with --multi False the layer3 ASPP head
+    gets no gradient and keeps its packs), so the job tables are built once, outside graph
+    capture (utils/graph.py captures iteration 1, after iteration 0 built them eagerly); a new
+    set while capturing is left to PackCache.get's lazy path."""
 
     _JOB = None
 
@@ -206,12 +207,14 @@ class PackBatch:
         return tables
 
     def run(self):
-        jobs = self._jobs()
+        jobs, keys = [], []
+        for c, d in self._jobs():
+            k = c.key_of(c.meta[d][0])
+            if c.key[d] != k:
+                jobs.append((c, d))
+                keys.append(k)
         if not jobs:
             return False
-        keys = [c.key_of(c.meta[d][0]) for c, d in jobs]
-        if any(c.key[d] == k for (c, d), k in zip(jobs, keys)):
-            return False  # not everything changed: the lazy path packs what did
         sig = tuple((id(c), d, c.buf[d].data_ptr(), c.buf[d].numel(), tuple(w.data_ptr() for w in c.meta[d][0]),
                      c.meta[d][1], c.meta[d][2]) for c, d in jobs)
         if sig != self.sig:

@@ -22,7 +22,7 @@ def counting_get(self, weights, cin, cout, for_dgrad):
 
 
 ops.PackCache.get = counting_get
-argv = ["--crop_size", "1024,512", "--target_crop_size", "1024,512", "--imagenet_pretrained", "False", "--save_dir", "",
+argv = ["--crop_size", "1024,512", "--target_crop_size", "1024,512", "--imagenet_pretrained", "False", "--save_dir", "", "--multi", "False",
         "--iter_max", "1000"]
 args, _, _ = init_args(build_parser().parse_args(argv))
 tr = UDATrainer(args, cuda=True)

@@ -428,7 +428,7 @@ def test_pack_forms_identical(kind, nb, cin, cout, for_dgrad):
 def test_pack_batch_matches_per_conv_packs():
     """ops.PackBatch (msl_conv_pack_many: every pack of a step in one launch per tap count) writes
     exactly the bytes of the per-conv msl_*_pack calls, for 9- and 1-tap packs, both directions,
-    a 2-branch ASPP pack and M <= 64 (no planes) - and only once every consumed pack is stale."""
+    a 2-branch ASPP pack and M <= 64 (no planes) - exactly the stale ones."""
     import torch.nn as nn
     g = torch.Generator().manual_seed(5)
 
@@ -468,22 +468,27 @@ def test_pack_batch_matches_per_conv_packs():
     ref = [{d: h._pack.buf[d].clone() for d in (0, 1)} for h in hs]
     assert not batch.run()  # nothing stale: no launch
     with torch.no_grad():
-        hs[0].ws[0].mul_(1.0)  # one stale pack only: left to the lazy path
-    assert not batch.run()
+        hs[0].ws[0].mul_(1.0)  # one stale conv (same values): only its two packs are redone
+        for d in (0, 1):
+            hs[0]._pack.buf[d].fill_(float("nan"))
+    assert batch.run() and batch.launches == 1
+    torch.cuda.synchronize()
+    for d in (0, 1):
+        assert torch.equal(hs[0]._pack.buf[d].view(torch.int32), ref[0][d].view(torch.int32))
     with torch.no_grad():
         for h in hs:
             for w in h.ws:
                 w.mul_(-2.0)
             for d in (0, 1):
                 h._pack.buf[d].fill_(float("nan"))
-    assert batch.run() and batch.launches == 1
+    assert batch.run() and batch.launches == 2
     with torch.no_grad():
         for h in hs:
             for w in h.ws:
                 w.mul_(-0.5)  # back to the values of the reference packs (x(-2)x(-0.5) = 1)
             for d in (0, 1):
                 h._pack.buf[d].fill_(float("nan"))
-    assert batch.run() and batch.launches == 2
+    assert batch.run() and batch.launches == 3
     torch.cuda.synchronize()
     for h, r in zip(hs, ref):
         for d in (0, 1):
