@@ -138,6 +138,12 @@ int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int co
 size_t msl_pconv_dgrad_workspace(int cin, int cout, int p);
 int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+/* msl_pconv_dgrad with accumulate = 1: dx += W^T dy (dx read and written by the GEMM's own
+ * epilogue / piece reduce; the bottleneck's residual gradient summed without a separate add).
+ * accumulate = 0 is msl_pconv_dgrad.  Replaces autograd's grad accumulation at the block input
+ * (Bottleneck.forward, deeplab_multi.py:31-48: conv1(x) and the identity residual both read x). */
+int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                        int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* dw[cout][cin] (= or += when accumulate) = sum_p dy[cout][p] x[cin][p] */
 size_t msl_pconv_wgrad_workspace(int cin, int cout, int p);

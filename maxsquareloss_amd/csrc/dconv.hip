@@ -339,7 +339,8 @@ static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
 template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int dil0,
-                           int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st) {
+                           int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st,
+                           int accum = 0) {
   const int P = h * w;
   FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
   // The x6 form runs one K-step per stage, three stages deep (scripts/tune_dconv.hip x6, layer3:
@@ -352,8 +353,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     pl.kps = pl.ksteps;
   }
   if (ws_bytes < fwd_ws_bytes(pl, M, P)) return MSL_ERR_WORKSPACE;
-  FwdArgs a;
+  FwdArgs a{};
   a.Ax6 = nullptr;
+  a.accum = accum;
   a.A = packed;
   a.B = img;
   a.C = pl.S > 1 ? (float*)ws : out;
@@ -423,7 +425,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     return MSL_OK;
   }
   // the split-K tile kernel (odd K-step count, M <= 32) has no bf16 form; x6 runs it in exact f32
-  if (MT == kMathBf16) return MSL_ERR_SHAPE;
+  if (MT == kMathBf16 || accum) return MSL_ERR_SHAPE;
   dim3 grid(pl.tiles_n, pl.tiles_m, pl.S);
   hipLaunchKernelGGL((k_igemm_fwd<64, 128, 16, 2, 2>), grid, dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
@@ -519,7 +521,7 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   if (pl.T * pl.nw >= (1LL << 31) || (long long)pl.nw * pl.slots * pl.bm * pl.bn * 4 >= (1LL << 31) || (long long)std::max(cin, cout) * P >= (1LL << 29) ||
       (long long)P + kWskBK >= (1LL << 22))
     return MSL_ERR_SHAPE;  // 32-bit index arithmetic, float pixel-row division in the kernel
-  WskArgs a;
+  WskArgs a{};
   a.dy = dy;
   a.x = x;
   a.dw = dw;
@@ -742,6 +744,16 @@ int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int c
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
   return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
                          ws, ws_bytes, as_stream(stream));
+}
+
+int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                        int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
+  if (!accumulate)
+    return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+                   as_stream(stream));
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+                 as_stream(stream), 1);
 }
 
 size_t msl_pconv_wgrad_workspace(int cin, int cout, int p) {

@@ -23,6 +23,7 @@ struct FwdArgs {
   long long slab;
   const void* Ax6;    // kMathX6P/PP: A split into bf16 planes [ks][plane][k half][lda][8] (k_split_pack)
   const void* Bx6;    // kMathX6PP: B split into bf16 planes [cb][plane][k half][P][8] (k_split_act)
+  int accum;          // stream-K forms: C = C_old + result (the fused residual-gradient sum)
 };
 
 struct WgradArgs {
@@ -990,11 +991,9 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
             for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + mrow + ro];
             v += bsum;
           }
-          if (full_m)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, voff, ro * a.P * 4, 0);
-          else
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
-                                                  mrow + ro < a.M ? voff + ro * a.P * 4 : OOB, 0, 0);
+          const unsigned off = full_m ? voff + ro * a.P * 4 : (mrow + ro < a.M ? voff + ro * a.P * 4 : OOB);
+          if (a.accum) v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, off, 0, 0)) + v;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, off, 0, 0);
         }
       }
   }
@@ -1042,7 +1041,10 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
     const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      if (n + c < a.P) dst[c] = a.bias ? vals[c] + bsum : vals[c];
+      if (n + c < a.P) {
+        const float v = a.bias ? vals[c] + bsum : vals[c];
+        dst[c] = a.accum ? dst[c] + v : v;
+      }
   }
 }
 

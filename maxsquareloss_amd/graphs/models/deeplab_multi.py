@@ -18,9 +18,10 @@ What runs where:
   - every BatchNorm (train mode, batch statistics of the one image, Q9) fused with the
     following ReLU and, for bn3, the residual add -> HIP kernels with fp64-accumulated
     statistics (MIOpen's single-pass variance is not accurate enough at bs=1);
-  - stride-1 1x1 convs -> `PointwiseConv`: three plain GEMMs on the fastest library per GEMM
-    (MIOpen/rocBLAS, hipBLASLt; the HIP pointwise kernels behind USE_HIP_POINTWISE), weight
-    gradients accumulated in place into the flat gradient buffer;
+  - stride-1 1x1 convs -> `PointwiseConv`: three GEMMs, each on the fastest of the HIP bf16x6
+    pointwise kernels, MIOpen and hipBLASLt for its shape (ops.conv1x1_plan), weight gradients
+    accumulated in place into the flat gradient buffer, and conv1's data gradient summing in
+    the identity residual's gradient (ops.ResidualGrad);
   - stem 7x7 conv, the two stride-2 1x1 convs of layer2 block 0, maxpool -> PyTorch-ROCm
     (MIOpen), SURVEY.md §8f row 1.
 """
@@ -58,10 +59,13 @@ class PointwiseConv(nn.Conv2d):
         super().__init__(in_channels, out_channels, kernel_size=1, stride=1, bias=False)
         self._pack = ops.PackCache(pointwise=True)
 
-    def forward(self, x):
+    def fuses_residual_grad(self):
+        return not (USE_HIP_POINTWISE or ops.CONV_MATH != "fp32")
+
+    def forward(self, x, residual_grad=None):
         if USE_HIP_POINTWISE or ops.CONV_MATH != "fp32":
             return ops.pconv(x, self.weight, self._pack)
-        return ops.conv1x1(x, self.weight, self._pack)
+        return ops.conv1x1(x, self.weight, self._pack, residual_grad)
 
 
 def conv1x1(inplanes, planes, stride):
@@ -88,13 +92,18 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        out = ops.bn_act(self.bn1, self.conv1(x), relu=True)
+        # identity residual: its gradient is summed into x's gradient by conv1's data-gradient
+        # GEMM (ops.ResidualGrad) rather than by autograd's accumulation kernel
+        fuse = (self.downsample is None and torch.is_grad_enabled() and isinstance(self.conv1, PointwiseConv)
+                and self.conv1.fuses_residual_grad())
+        hold = ops.ResidualGrad() if fuse else None
+        out = ops.bn_act(self.bn1, self.conv1(x, hold) if fuse else self.conv1(x), relu=True)
         out = ops.bn_act(self.bn2, self.conv2(out), relu=True)
-        residual = x
+        residual = x.detach() if fuse else x
         if self.downsample is not None:
             residual = ops.bn_act(self.downsample[1], self.downsample[0](x))
         # bn3 + residual add + ReLU in one kernel (deeplab_multi.py:38-46)
-        return ops.bn_act(self.bn3, self.conv3(out), residual=residual, relu=True)
+        return ops.bn_act(self.bn3, self.conv3(out), residual=residual, relu=True, residual_grad=hold)
 
 
 class Classifier_Module(nn.Module):

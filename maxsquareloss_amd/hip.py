@@ -39,6 +39,7 @@ SIGNATURES = {
     "msl_pconv_fwd": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_dgrad_workspace": (c_sz, [c_int] * 3),
     "msl_pconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
+    "msl_pconv_dgrad_acc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_wgrad_workspace": (c_sz, [c_int] * 3),
     "msl_pconv_wgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
     "msl_dconv_fwd_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),

@@ -384,6 +384,19 @@ def pconv(x, weight, cache):
     return _PConv.apply(x, weight, cache)
 
 
+# --------------------------------------------------------------------------- fused residual gradient
+class ResidualGrad:
+    """Carries the gradient of a bottleneck's identity residual from bn3's backward (which runs
+    first) to conv1's backward, which adds it into the block input's gradient inside its data-
+    gradient GEMM (msl_pconv_dgrad_acc / hipBLASLt addmm with beta = 1) instead of autograd's
+    separate accumulation kernel (deeplab_multi.py:31-48: x feeds conv1 and the residual)."""
+
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
 # --------------------------------------------------------------------------- 1x1 conv, per-GEMM dispatch
 def conv1x1_plan(cin, cout, p, form="bf16x6"):
     """Implementation of each of the three GEMMs of a stride-1 1x1 conv: (fwd, dgrad, wgrad), each
@@ -424,11 +437,13 @@ class _Conv1x1(Function):
     """
 
     @staticmethod
-    def forward(ctx, x, weight, cache):
+    def forward(ctx, x, weight, cache, hold=None):
         cout, cin = weight.shape[0], weight.shape[1]
         h, w = x.shape[2], x.shape[3]
         p = h * w
         form = f32_form()
+        ctx.hold = hold
+        ctx.form = form
         key = (cin, cout, p, form)
         plan = _PLANS.get(key)
         if plan is None:
@@ -461,7 +476,21 @@ class _Conv1x1(Function):
         x2 = x.view(cin, p)
         w2 = weight.view(cout, cin)
         dx = None
-        if ctx.needs_input_grad[0]:
+        hold = ctx.hold
+        if ctx.needs_input_grad[0] and hold is not None and hold.g is not None:
+            # dx = (the residual's gradient) + W^T dy, accumulated by the GEMM itself
+            dx, hold.g = hold.g, None
+            if ctx.form == "bf16x6" and dplan in ("hip", "miopen"):
+                lib = hip.load()
+                packed_d = ctx.cache.get([weight], cin, cout, 1)
+                wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
+                ws = hip.workspace(wsb, x.device)
+                hip.check(lib.msl_pconv_dgrad_acc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, 1,
+                                                  hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                                                  hip.stream_ptr()), "msl_pconv_dgrad_acc")
+            else:
+                dx.view(cin, p).addmm_(w2.t(), g2)
+        elif ctx.needs_input_grad[0]:
             if dplan == "hip":
                 lib = hip.load()
                 packed_d = ctx.cache.get([weight], cin, cout, 1)
@@ -477,7 +506,7 @@ class _Conv1x1(Function):
                 dx = torch.ops.aten.convolution_backward(gy, x, weight, None, (1, 1), (0, 0), (1, 1), False,
                                                          (0, 0), 1, (True, False, False))[0]
         if not ctx.needs_input_grad[1]:
-            return dx, None, None
+            return dx, None, None, None
         sink = grad_sink(weight)
         if wplan == "hip":
             # HIP pointwise wgrad (accumulating into the flat buffer when it can)
@@ -489,21 +518,23 @@ class _Conv1x1(Function):
                                           int(sink is not None), ws.data_ptr(), wsb, hip.stream_ptr()),
                       "msl_pconv_wgrad")
             if sink is None:
-                return dx, dst, None
+                return dx, dst, None, None
         elif sink is not None:
             sink[0].view(cout, cin).addmm_(g2, x2.t())
         else:
-            return dx, torch.mm(g2, x2.t()).view_as(weight), None
+            return dx, torch.mm(g2, x2.t()).view_as(weight), None, None
         sink[1].notify(sink[2])
-        return dx, None, None
+        return dx, None, None, None
 
 
-def conv1x1(x, weight, cache):
-    """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99)."""
+def conv1x1(x, weight, cache, residual_grad=None):
+    """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99).
+    `residual_grad` (a ResidualGrad also given to the block's bn_act): its gradient is added into
+    this conv's input gradient by the data-gradient GEMM."""
     x = _check_act(x, "conv1x1")
     if weight.shape[2:] != (1, 1) or x.size(1) != weight.shape[1]:
         raise hip.MSLError(f"conv1x1: weight {tuple(weight.shape)} does not match input {tuple(x.shape)}")
-    return _Conv1x1.apply(x, weight, cache)
+    return _Conv1x1.apply(x, weight, cache, residual_grad)
 
 
 # --------------------------------------------------------------------------- upsample
@@ -802,7 +833,7 @@ def iw_maxsquare_prob(prob, label, ratio):
 class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, training, momentum,
-                eps, relu):
+                eps, relu, hold=None):
         x = _check_act(x, "bn_act")
         c, p = x.size(1), x.size(2) * x.size(3)
         if residual is not None:
@@ -824,6 +855,7 @@ class _BNAct(Function):
         ctx.save_for_backward(x, weight, y if relu else None, save_mean, save_invstd)
         ctx.bias = bias
         ctx.meta = (c, p, bool(training), bool(relu))
+        ctx.hold = hold
         return y
 
     @staticmethod
@@ -834,7 +866,8 @@ class _BNAct(Function):
         lib = hip.load()
         nig = ctx.needs_input_grad
         dx = torch.empty_like(x) if nig[0] else None
-        dres = torch.empty_like(x) if nig[3] else None
+        hold = ctx.hold
+        dres = torch.empty_like(x) if (nig[3] or hold is not None) else None
         sw = grad_sink(weight) if nig[1] else None
         sb = grad_sink(ctx.bias) if nig[2] else None
         direct = sw is not None and sb is not None
@@ -853,12 +886,18 @@ class _BNAct(Function):
             sw[1].notify(sw[2])
             sb[1].notify(sb[2])
             dgamma = dbeta = None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+        if hold is not None:  # handed to the block's conv1 backward (ResidualGrad)
+            hold.g = dres
+            dres = None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
-def bn_act(bn, x, residual=None, relu=False):
-    """act(bn(x) [+ residual]) for an nn.BatchNorm2d `bn` (train mode: batch statistics, bs = 1)."""
+def bn_act(bn, x, residual=None, relu=False, residual_grad=None):
+    """act(bn(x) [+ residual]) for an nn.BatchNorm2d `bn` (train mode: batch statistics, bs = 1).
+    With `residual_grad` (ResidualGrad) the residual's gradient goes to that holder instead of
+    autograd (pass the residual detached; the conv that shares its input adds it)."""
     training = bn.training or not bn.track_running_stats
     momentum = 0.1 if bn.momentum is None else bn.momentum
     return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
-                        bn.num_batches_tracked if training else None, training, momentum, bn.eps, relu)
+                        bn.num_batches_tracked if training else None, training, momentum, bn.eps, relu,
+                        residual_grad)

@@ -35,7 +35,7 @@ struct Shape { int cin, cout, h, w, dil; };
 template <int BM, int BN, int BK, int WM, int WN>
 float run_fwd(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int S, int iters, int lda) {
   const int P = sh.h * sh.w;
-  FwdArgs a;
+  FwdArgs a{};
   a.A = wp; a.B = x; a.C = S > 1 ? ws : y; a.bias = nullptr; a.nbias = 0;
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
@@ -59,7 +59,7 @@ float run_fwd(const Shape& sh, const float* x, const float* wp, float* y, float*
 template <int BM, int BN, int STAGES, int WM, int WN>
 float run_fwd_dma(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int S, int iters, int lda) {
   const int P = sh.h * sh.w;
-  FwdArgs a;
+  FwdArgs a{};
   a.A = wp; a.B = x; a.C = S > 1 ? ws : y; a.bias = nullptr; a.nbias = 0;
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
@@ -83,7 +83,7 @@ template <int BM, int BN, int G, int STAGES, int WM, int WN, int MT = 0, bool PW
 float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda, int* flags) {
   const int P = sh.h * sh.w;
   const int taps = PW ? 1 : 9;
-  FwdArgs a;
+  FwdArgs a{};
   a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = PW ? 0 : sh.dil; a.dil1 = 0;
@@ -123,7 +123,7 @@ float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, floa
                 bool reduce = true) {
   const int P = sh.h * sh.w;
   const int taps = PW ? 1 : 9;
-  FwdArgs a;
+  FwdArgs a{};
   a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = PW ? 0 : sh.dil; a.dil1 = 0;
@@ -156,7 +156,7 @@ float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, floa
 template <int BM, int MT>
 float run_rg(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int NW, int iters, int lda) {
   const int P = sh.h * sh.w;
-  FwdArgs a;
+  FwdArgs a{};
   a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
@@ -202,7 +202,7 @@ float run_wgrad(const Shape& sh, const float* x, const float* dy, float* dw, flo
 template <int BM, int BN, int ST, int MT = 0>
 float run_wgrad_sk(const Shape& sh, const float* x, const float* dy, float* dw, float* ws, int NWmax, int iters) {
   const int P = sh.h * sh.w;
-  WskArgs a;
+  WskArgs a{};
   a.dy = dy; a.x = x; a.dw = dw; a.part = ws; a.M = sh.cout; a.N = sh.cin; a.H = sh.h; a.W = sh.w; a.P = P;
   a.dil0 = sh.dil; a.dil1 = 0; a.taps = 9; a.accumulate = 0; a.invW = 1.0f / sh.w;
   a.tiles_m = (sh.cout + BM - 1) / BM; a.tiles_n = (sh.cin + BN - 1) / BN; a.KS = (P + kWskBK - 1) / kWskBK;
@@ -226,7 +226,7 @@ float run_wgrad_sk(const Shape& sh, const float* x, const float* dy, float* dw, 
 float run_wgrad_x6(const Shape& sh, const float* x, const float* dy, float* dw, float* ws, int NWmax, int iters,
                    bool split_only = false, int chunks = 0) {
   const int P = sh.h * sh.w;
-  WskArgs a;
+  WskArgs a{};
   a.dy = dy; a.x = x; a.dw = dw; a.part = ws; a.M = sh.cout; a.N = sh.cin; a.H = sh.h; a.W = sh.w; a.P = P;
   a.dil0 = sh.dil; a.dil1 = 0; a.taps = 9; a.accumulate = 0; a.invW = 1.0f / sh.w;
   a.tiles_m = (sh.cout + 127) / 128; a.tiles_n = (sh.cin + 127) / 128; a.KS = (P + kWx6BK - 1) / kWx6BK;

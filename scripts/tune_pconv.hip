@@ -44,7 +44,7 @@ struct Shape { int cimg, M, P; };
 
 template <int BM, int BN, int G, int STAGES, bool PW, int MT = 0>
 float run_sk(const Shape& sh, const float* x, const float* wp, float* y, float* ws, int* flags, int NW, int iters, int lda) {
-  FwdArgs a;
+  FwdArgs a{};
   a.A = wp; a.B = x; a.C = y; a.bias = nullptr; a.nbias = 0;
   a.M = sh.M; a.lda = lda; a.H = 1; a.W = sh.P; a.P = sh.P; a.cimg = sh.cimg;
   a.ncb = (sh.cimg + 15) / 16; a.dil0 = 0; a.dil1 = 0;

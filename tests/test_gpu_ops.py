@@ -504,3 +504,50 @@ def test_pack_batch_matches_per_conv_packs():
             key = h._pack.key[d]
             h._pack.get(list(h.ws), h.dims[0], h.dims[1], d)
             assert h._pack.key[d] == key
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(1024, 256, 17, 33), (2048, 512, 9, 17), (256, 1024, 17, 33)])
+def test_pconv_dgrad_accumulate(cin, cout, h, w, f32_form):
+    """msl_pconv_dgrad_acc: dx += W^T dy in the GEMM's own epilogue / piece reduce."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    g = torch.Generator().manual_seed(cin + cout)
+    p = h * w
+    wt = torch.randn(cout, cin, 1, 1, generator=g) * 0.05
+    gy = torch.randn(1, cout, h, w, generator=g)
+    dx0 = torch.randn(1, cin, h, w, generator=g)
+    ref = dx0.double() + torch.mm(wt.view(cout, cin).double().t(), gy.view(cout, p).double()).view(1, cin, h, w)
+    cache = ops.PackCache(pointwise=True)
+    wd = wt.to(DEV)
+    packed_d = cache.get([wd], cin, cout, 1)
+    dx = dx0.to(DEV)
+    wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
+    ws = hip.workspace(wsb, dx.device)
+    assert lib.msl_pconv_dgrad_acc(gy.to(DEV).data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, 1,
+                                   hip.counters(dx.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()) == 0
+    torch.cuda.synchronize()
+    assert _rel(dx, ref) < 1e-5
+
+
+def test_bottleneck_fused_residual_grad(f32_form, monkeypatch):
+    """Bottleneck with an identity residual: the residual's gradient summed into x's gradient by
+    conv1's data-gradient GEMM (ops.ResidualGrad) equals autograd's separate accumulation."""
+    from maxsquareloss_amd.graphs.models import deeplab_multi as dm
+    torch.manual_seed(3)
+    blk = dm.Bottleneck(1024, 256, dilation=2).to(DEV).train()
+    x = (torch.randn(1, 1024, 17, 33) * 2).to(DEV)
+    gy = torch.randn(1, 1024, 17, 33).to(DEV)
+    out = {}
+    for fused in (True, False):
+        monkeypatch.setattr(dm.PointwiseConv, "fuses_residual_grad", lambda self, f=fused: f)
+        xg = x.clone().requires_grad_()
+        for prm in blk.parameters():
+            prm.grad = None
+        y = blk(xg)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        out[fused] = (y.detach().clone(), xg.grad.clone(), [prm.grad.clone() for prm in blk.parameters()])
+    assert torch.equal(out[True][0], out[False][0])
+    assert _rel(out[True][1], out[False][1].double()) < 1e-6
+    for a, b in zip(out[True][2], out[False][2]):
+        assert _rel(a, b.double()) < 1e-6
