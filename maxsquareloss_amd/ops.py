@@ -480,7 +480,7 @@ class _Conv1x1(Function):
         if ctx.needs_input_grad[0] and hold is not None and hold.g is not None:
             # dx = (the residual's gradient) + W^T dy, accumulated by the GEMM itself
             dx, hold.g = hold.g, None
-            if ctx.form == "bf16x6" and dplan in ("hip", "miopen"):
+            if dplan == "hip":
                 lib = hip.load()
                 packed_d = ctx.cache.get([weight], cin, cout, 1)
                 wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
@@ -488,8 +488,11 @@ class _Conv1x1(Function):
                 hip.check(lib.msl_pconv_dgrad_acc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, 1,
                                                   hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
                                                   hip.stream_ptr()), "msl_pconv_dgrad_acc")
-            else:
+            elif dplan == "hipblaslt":
                 dx.view(cin, p).addmm_(w2.t(), g2)
+            else:  # MIOpen's data gradient has no accumulate form: the add stays a kernel of its own
+                dx.add_(torch.ops.aten.convolution_backward(gy, x, weight, None, (1, 1), (0, 0), (1, 1), False,
+                                                            (0, 0), 1, (True, False, False))[0])
         elif ctx.needs_input_grad[0]:
             if dplan == "hip":
                 lib = hip.load()

@@ -506,7 +506,8 @@ def test_pack_batch_matches_per_conv_packs():
             assert h._pack.key[d] == key
 
 
-@pytest.mark.parametrize("cin,cout,h,w", [(1024, 256, 17, 33), (2048, 512, 9, 17), (256, 1024, 17, 33)])
+@pytest.mark.parametrize("cin,cout,h,w", [(1024, 256, 17, 33), (2048, 512, 9, 17), (256, 1024, 17, 33),
+                                           (256, 64, 33, 65), (512, 128, 17, 33), (1024, 256, 65, 129)])
 def test_pconv_dgrad_accumulate(cin, cout, h, w, f32_form):
     """msl_pconv_dgrad_acc: dx += W^T dy in the GEMM's own epilogue / piece reduce."""
     from maxsquareloss_amd import hip

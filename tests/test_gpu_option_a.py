@@ -7,8 +7,12 @@ the same model, weights and target image.
 
 Tolerances: one forward/backward of the same network from the same state, so the two paths
 differ only by fp32 rounding of the loss arithmetic (torch softmax vs the fused kernel): losses
-1e-5 relative, the whole gradient 1e-4 normwise; the IW class histogram (argmax of the two
-paths' probabilities - torch's softmax vs the kernel's) within 0.05 % of the pixels.
+1e-5 relative; the IW class histogram (argmax of the two paths' probabilities - torch's softmax
+vs the kernel's) within 0.05 % of the pixels; the parameter gradients per tensor within 4x the
+distance between two runs of the fused path itself, or 1e-4 of the tensor's norm.  (MIOpen's
+stride-2 1x1 data gradients in layer2 block 0 are not bit-reproducible (~2e-7), and the bs=1 BN
+backward amplifies that into up to a few % of the early layers' BN-parameter gradients from one
+run to the next: scripts/diag_nondet.py; the first two passes warm MIOpen's solver choice up.)
 """
 import pytest
 import torch
@@ -57,19 +61,25 @@ def _reference_train_target(tr, pred, hard_loss):
 
 
 def _grads(model):
-    return torch.cat([p.grad.detach().flatten().double() for p in model.parameters() if p.grad is not None])
+    return [p.grad.detach().double().clone() for p in model.parameters() if p.grad is not None]
 
 
 @pytest.mark.parametrize("mode", ["maxsquare", "IW_maxsquare"])
 def test_reference_train_target_through_drop_in_modules(mode):
     tr = _trainer(mode)
     xt = synthetic_image(H, W, 321).cuda()
-    # the package's fused path
+    for _ in range(2):  # warm MIOpen's solver choice up
+        tr.optimizer.zero_grad()
+        tr.train_target(tr.model(xt))
+    # the package's fused path, twice (its own run-to-run spread)
     tr.optimizer.zero_grad()
     tr.train_target(tr.model(xt))
     fused = (tr.loss_target.detach().clone(), tr.loss_target_2.detach().clone())
-    g_fused = _grads(tr.model).clone()
+    g_fused = _grads(tr.model)
     hist_fused = tr.target_loss.last_hist.clone() if mode == "IW_maxsquare" else None
+    tr.optimizer.zero_grad()
+    tr.train_target(tr.model(xt))
+    g_fused2 = _grads(tr.model)
     # the reference's train_target, imports swapped
     tr.optimizer.zero_grad()
     ref = _reference_train_target(tr, tr.model(xt), CrossEntropyLoss(ignore_index=-1))
@@ -78,9 +88,10 @@ def test_reference_train_target_through_drop_in_modules(mode):
     assert ref[2] > 0  # the guidance label has pixels (threshold 0.2)
     for a, b in zip(fused, ref[:2]):
         assert a.item() == pytest.approx(b.item(), rel=1e-5), (mode, fused, ref)
-    assert g_fused.shape == g_ref.shape and g_ref.abs().max() > 0
-    rel = ((g_fused - g_ref).norm() / g_ref.norm()).item()
-    assert rel < 1e-4, (mode, rel)
+    assert len(g_fused) == len(g_ref) == len(g_fused2)
+    for i, (a, a2, b) in enumerate(zip(g_fused, g_fused2, g_ref)):
+        err, spread = (a - b).norm().item(), (a - a2).norm().item()
+        assert err <= max(4 * spread, 1e-4 * b.norm().item()), (mode, i, err, spread, b.norm().item())
     if hist_fused is not None:
         d = (hist_fused.long() - tr.target_loss.last_hist.long()).abs().sum().item()
         assert d <= 2 * 0.0005 * H * W, (hist_fused, tr.target_loss.last_hist)
