@@ -14,9 +14,9 @@
  *     allocator on the Python side).  The library allocates nothing; scratch
  *     comes from the caller's workspace, sized by the matching *_workspace()
  *     query, and no call leaves state that a later call reads.
- *   - Process-wide configuration: three switches select kernel FORMS, not
- *     results' meaning - msl_conv_set_f32_form, msl_conv_set_pack_form and
- *     msl_bn_set_fused.  They are plain globals read on the host at launch
+ *   - Process-wide configuration: four switches select kernel FORMS, not
+ *     results' meaning - msl_conv_set_f32_form, msl_conv_set_pack_form,
+ *     msl_conv_set_sk_hybrid and msl_bn_set_fused.  They are plain globals read on the host at launch
  *     time: set them once at start-up, before work is enqueued; changing one
  *     while another host thread enqueues calls is a data race, and a captured
  *     hipGraph keeps the forms that were current at capture.
@@ -63,6 +63,11 @@ int msl_conv_f32_form(void);
 /* Weight-pack kernel (process-wide; identical packed bytes either way): 1 = one LDS-transposing
  * pack+split launch per msl_*_pack call (default), 0 = element-wise gather + separate split. */
 int msl_conv_set_pack_form(int form);
+/* Schedule of the forward-form conv kernels (fwd and data gradient; process-wide; same results
+ * up to the fp32 summation order of split tiles): 1 = when the output tiles outnumber the 512
+ * workgroups, whole rounds of tiles run data-parallel and only the remainder is split stream-K
+ * (default); 0 = pure stream-K (every tile range-split over 512 workgroups). */
+int msl_conv_set_sk_hybrid(int on);
 
 /* ------------------------------------------------------------------------
  * Dilated 3x3 convolution, stride 1, padding = dilation, as an FP32-MFMA

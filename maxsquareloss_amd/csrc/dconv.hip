@@ -196,6 +196,9 @@ __global__ void __launch_bounds__(256) k_pack_split_many(const msl_pack_job* __r
 // persistent workgroups (2 per CU), so every CU gets the same number of MFMA stages whatever
 // the tile count.  The split-K tile kernel remains for an odd K-step count with M <= 32.
 constexpr int kSkBN = 128, kSkNW = 512;
+// Forward-form schedule (msl_conv_set_sk_hybrid): 1 = data-parallel rounds + stream-K remainder
+// when the tiles outnumber the workers (SkArgs), 0 = pure stream-K.  Process-wide.
+static int g_sk_hybrid = 1;
 constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
 
 struct FwdPlan {
@@ -377,49 +380,53 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   if (pl.sk) {
     if (!counters) return MSL_ERR_ARG;
     if ((long long)pl.tiles_m * pl.tiles_n > kMaxCounters) return MSL_ERR_SHAPE;
-    SkArgs sk;
+    SkArgs sk{};
     sk.flags = counters;
     sk.part = (float*)ws;
     sk.tiles_m = pl.tiles_m;
     sk.tiles_n = pl.tiles_n;
     sk.KS = pl.kps;
-    const long long T = (long long)pl.tiles_m * pl.tiles_n * sk.KS;
-    // every workgroup must own at least one iteration: the piece count of a tile is the number
-    // of workgroups its iteration range touches
-    sk.NW = (int)std::min<long long>(kSkNW, T);
-    if (T * kSkNW >= (1LL << 31) || (long long)cimg * P >= (1LL << 29) ||
+    const long long tiles = (long long)pl.tiles_m * pl.tiles_n;
+    if (tiles * sk.KS * kSkNW >= (1LL << 31) || (long long)cimg * P >= (1LL << 29) ||
         (long long)pl.ksteps * kCB * a.lda >= (1LL << 29))
       return MSL_ERR_SHAPE;  // 32-bit index arithmetic in the kernel
+    // at least as many tiles as workers: whole rounds of tiles data-parallel, stream-K over the
+    // rest (SkArgs); fewer: pure stream-K.  Every stream-K worker must own at least one iteration:
+    // the piece count of a tile is the number of workgroups its iteration range touches.
+    sk.tdp = (g_sk_hybrid && tiles >= kSkNW) ? (int)(tiles / kSkNW * kSkNW) : 0;
+    const long long T = (tiles - sk.tdp) * sk.KS;
+    sk.NW = (int)std::min<long long>(kSkNW, T);
     sk.T = (int)T;
     a.C = out;
     a.bias = bias;
-    const dim3 grid(sk.NW), block(256);
-    const dim3 rgrid(pl.bm * kSkBN / 1024, pl.tiles_m * pl.tiles_n);
+    const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
+    const dim3 rgrid(pl.bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp));
+    const bool reduce = T > 0;
     if (MT == kMathX6 && pl.bm == 128) {
       // the x6 kernel stages its weights from the bf16 planes that pack() split once, behind
       // the fp32 part of the same buffer (M > 64 <=> 128-row tiles)
       a.Ax6 = reinterpret_cast<const __bf16*>(packed + (long long)pl.ksteps * kCB * a.lda);
       hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 4, 2, 2, false, kMathX6P>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
+      if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 128) {
       if (pl.G == 2)
         hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2, false, MT>), grid, block, 0, st, a, sk);
       else
         hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2, false, MT>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
+      if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
       if (pl.G == 2)
         hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2, false, MS>), grid, block, 0, st, a, sk);
       else
         hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2, false, MS>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
+      if (reduce) hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
     } else {
       hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4, false, MS>), grid, block, 0, st, a, sk);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
+      if (reduce) hipLaunchKernelGGL((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
     }
     MSL_CHECK_LAUNCH();
     return MSL_OK;
@@ -553,7 +560,7 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   if (pl.rx6) {
     bf16x8* planes = reinterpret_cast<bf16x8*>((char*)ws + wgrad_piece_bytes(pl));
     a.dyx6 = planes;
-    hipLaunchKernelGGL(k_split_rows, dim3(pl.lda / 32, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P, pl.KS,
+    hipLaunchKernelGGL(k_split_rows, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P, pl.KS,
                        pl.lda, planes);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_wgrad_x6, grid, block, 0, st, a);
@@ -614,6 +621,12 @@ int msl_conv_set_f32_form(int form) {
 }
 
 int msl_conv_f32_form(void) { return g_f32_form; }
+
+int msl_conv_set_sk_hybrid(int on) {
+  if (on != 0 && on != 1) return MSL_ERR_ARG;
+  g_sk_hybrid = on;
+  return MSL_OK;
+}
 
 int msl_conv_set_pack_form(int form) {
   if (form != 0 && form != 1) return MSL_ERR_ARG;

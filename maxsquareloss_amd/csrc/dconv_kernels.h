@@ -687,11 +687,17 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
 // piece per workgroup that touched it; k_sk_reduce (the next launch on the stream) sums them in
 // worker order.  Nothing ever waits on another workgroup, so the kernel needs no co-residency
 // and no dispatch-order assumption, and the sum order - hence the result - is fixed.
+// Hybrid form (r02): when there are at least as many tiles as workers, the first tdp = R x grid
+// tiles run data-parallel (worker w owns whole tiles w, w + grid, ...: no pieces, direct stores)
+// and only the remaining tiles' iterations are cut into stream-K ranges over NW workers.  A
+// 256->1024 pointwise forward (528 tiles) left ~1040 pieces (67 MB written and re-read) as pure
+// stream-K and leaves 272 this way.  tdp = 0 is pure stream-K.
 struct SkArgs {
   float* part;     // [NW][2][BM][BN] pieces of split tiles (row-major)
   int* flags;      // unused (kept for the C-ABI's caller-owned counter array)
   int tiles_m, tiles_n, KS, NW;
-  int T;           // tiles * KS  (T * NW < 2^31, checked by the planner)
+  int T;           // stream-K iterations: (tiles - tdp) * KS  (T * NW < 2^31, checked by the planner)
+  int tdp;         // leading tiles that run data-parallel (a multiple of the grid size)
 };
 
 __device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
@@ -752,8 +758,13 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   // XCD-aware worker id: workgroups b, b+8, ... share an XCD and get consecutive ranges
   const int nb = gridDim.x, b = blockIdx.x;
   const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);  // a bijection for any nb
-  const int T = sk.T;
-  const int it_begin = sk_start(w, T, sk.NW), it_end = sk_start(w + 1, T, sk.NW);
+  // whole data-parallel tiles w, w + nb, ... below sk.tdp first, then this worker's stream-K
+  // range of the remaining tiles' iterations (none for w >= sk.NW)
+  int dp_t = w, it = 0, it_end = 0;
+  if (w < sk.NW) {
+    it = sk.tdp * sk.KS + sk_start(w, sk.T, sk.NW);
+    it_end = sk.tdp * sk.KS + sk_start(w + 1, sk.T, sk.NW);
+  }
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.A, (short)0, (int)min(0x7fffffffLL, (long long)sk.KS * BK * a.lda * 4), 0x00020000);
@@ -767,12 +778,22 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   const unsigned chan_bytes = (unsigned)a.P * 4u;
 
   f32x16 acc[TM][TN];
-  for (int it = it_begin; it < it_end;) {
-    const int t = (unsigned)it / (unsigned)sk.KS;
-    const int k_a = it - t * sk.KS;
-    const int k_b = min(sk.KS, k_a + (it_end - it));
+  while (true) {
+    int t, k_a, k_b;
+    if (dp_t < sk.tdp) {
+      t = dp_t;
+      k_a = 0;
+      k_b = sk.KS;
+      dp_t += nb;
+    } else if (it < it_end) {
+      t = (unsigned)it / (unsigned)sk.KS;
+      k_a = it - t * sk.KS;
+      k_b = min(sk.KS, k_a + (it_end - it));
+      it += k_b - k_a;
+    } else {
+      break;
+    }
     const int nst = k_b - k_a;
-    it += nst;
     int tm, tn;
     sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
@@ -975,13 +996,28 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
     const bool full_m = m0 + BM <= a.M;
+    auto out_off = [&](int i, int j, int r) {
+      const int n = n0 + wn + j * 32 + (lane & 31);
+      const int mr = m0 + wm + i * 32 + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2);
+      return (n < a.P && (full_m || mr < a.M)) ? (unsigned)((mr * a.P + n) * 4) : OOB;
+    };
+    if (a.accum) {
+      // accumulate epilogue (msl_pconv_dgrad_acc): every old value is loaded before the first
+      // store, so the loads are in flight together (load-add-store per element serialised each
+      // load behind the previous element's store: +30 us on a 2048 x 8385 output)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            acc[i][j][r] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, out_off(i, j, r), 0, 0));
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn + j * 32 + (lane & 31);
         const int mrow = m0 + wm + i * 32 + 4 * (lane >> 5);
-        const unsigned voff = n < a.P ? (unsigned)((mrow * a.P + n) * 4) : OOB;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ro = (r & 3) + 8 * (r >> 2);
@@ -991,23 +1027,22 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
             for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + mrow + ro];
             v += bsum;
           }
-          const unsigned off = full_m ? voff + ro * a.P * 4 : (mrow + ro < a.M ? voff + ro * a.P * 4 : OOB);
-          if (a.accum) v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, off, 0, 0)) + v;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, out_off(i, j, r), 0, 0);
         }
       }
   }
 }
 
 // Sum of the pieces of every split stream-K tile (worker order: deterministic), + the branch
-// biases, into the output.  grid = (BM*BN / 1024 chunks, tiles); blocks of unsplit tiles exit.
-// Pieces are row-major [BM][BN]: one float4 of 4 consecutive pixels per thread.
+// biases, into the output.  grid = (BM*BN / 1024 chunks, tiles - tdp: the stream-K tiles); blocks
+// of unsplit tiles exit.  Pieces are row-major [BM][BN]: one float4 of 4 consecutive pixels per
+// thread.
 template <int BM, int BN>
 __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   constexpr int PSZ = BM * BN;
-  const int t = blockIdx.y;
-  const int w_lo = sk_worker_of(t * sk.KS, sk.T, sk.NW);
-  const int w_hi = sk_worker_of((t + 1) * sk.KS - 1, sk.T, sk.NW);
+  const int tl = blockIdx.y, t = sk.tdp + tl;  // tile, and its index in the stream-K space
+  const int w_lo = sk_worker_of(tl * sk.KS, sk.T, sk.NW);
+  const int w_hi = sk_worker_of((tl + 1) * sk.KS - 1, sk.T, sk.NW);
   if (w_lo == w_hi) return;
   int tm, tn;
     sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
@@ -1015,7 +1050,7 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   const float4* __restrict__ part = reinterpret_cast<const float4*>(sk.part);
   for (int g = blockIdx.x * 256 + threadIdx.x; g < PSZ / 4; g += gridDim.x * 256) {
     auto piece = [&](int wc) {
-      const int slot = sk_start(wc, sk.T, sk.NW) > t * sk.KS ? 0 : 1;
+      const int slot = sk_start(wc, sk.T, sk.NW) > tl * sk.KS ? 0 : 1;
       return part[(long long)(wc * 2 + slot) * (PSZ / 4) + g];
     };
     auto add = [](float4& acc, const float4& v) { acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w; };
@@ -1038,13 +1073,21 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
       for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + m];
     }
     float* dst = a.C + (long long)m * a.P + n;
-    const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+    float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+    if (a.bias) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) vals[c] += bsum;
+    }
+    if (a.accum) {  // all four old values loaded before the first store
+      float old[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) old[c] = n + c < a.P ? dst[c] : 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) vals[c] = old[c] + vals[c];
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      if (n + c < a.P) {
-        const float v = a.bias ? vals[c] + bsum : vals[c];
-        dst[c] = a.accum ? dst[c] + v : v;
-      }
+      if (n + c < a.P) dst[c] = vals[c];
   }
 }
 
@@ -1566,32 +1609,46 @@ __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
 constexpr int kWx6BK = 16;
 
 // planes[((ks*3 + q)*2 + h)*lda + m][j] = term q of src[m][ks*16 + 8h + j] (0 past P or M).
-// Block = 32 rows x 4 K-steps: reads of 8 consecutive pixels per thread (8 lanes per 256-B row
-// run), split, transposed through LDS so each plane row is written as 32 contiguous vectors.
-// grid = (lda / 32, ceil(KS / 4)).
+// Block = 64 rows x 4 K-steps (64 pixels).  Each wave loads 16 rows, one dword per lane and row
+// (lane = pixel: one coalesced 256-B run per load, 16 loads in flight per lane), splits them and
+// stores the bf16 terms to LDS as [plane][row][pixel] rows padded to 144 B; the block then writes
+// every (K-step, plane, half) as 64 consecutive rows of 16-B vectors (ds_read_b128 at a 144-B
+// stride: conflict-free).  The r01 form (32 rows, 8 scalar loads per thread at a 32-B stride
+// across lanes) ran 8.3 us on a 256 x 8385 dY.  grid = (lda / 64, ceil(KS / 4)).
 __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ src, int M, int P, int KS, int lda,
                                                      bf16x8* __restrict__ planes) {
-  __shared__ bf16x8 tile[3][8][33];
-  const int tid = threadIdx.x;
-  const int m0 = blockIdx.x * 32, ks0 = blockIdx.y * 4;
-  {
-    const int r = tid >> 3, c = tid & 7;  // row, 8-pixel chunk (= K-step ks0 + c/2, half c%2)
-    const int m = m0 + r, p0 = ks0 * kWx6BK + c * 8;
-    const float* row = src + (long long)m * P;
-    Split3 sp;
+  constexpr int R = 64, LDP = 72;  // rows per block, LDS row stride in bf16 (64 pixels + 8)
+  __shared__ __attribute__((aligned(16))) __bf16 tile[3 * R * LDP];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int m0 = blockIdx.x * R, ks0 = blockIdx.y * 4;
+  const int p = ks0 * kWx6BK + lane;
+  const bool pin = p < P;
+  float v[R / 4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) split3_set(sp, j, (m < M && p0 + j < P) ? row[p0 + j] : 0.f);
-    tile[0][c][r] = sp.hi;
-    tile[1][c][r] = sp.mid;
-    tile[2][c][r] = sp.lo;
+  for (int i = 0; i < R / 4; ++i) {
+    const int m = m0 + wv + 4 * i;
+    v[i] = (pin && m < M) ? src[(long long)m * P + p] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < R / 4; ++i) {
+    const int r = wv + 4 * i;
+    const __bf16 h = (__bf16)v[i];
+    const float rem = v[i] - (float)h;
+    const __bf16 md = (__bf16)rem;
+    tile[(0 * R + r) * LDP + lane] = h;
+    tile[(1 * R + r) * LDP + lane] = md;
+    tile[(2 * R + r) * LDP + lane] = (__bf16)(rem - (float)md);
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int v = tid + 256 * i;  // (q, c, r): r fastest
-    const int r = v & 31, c = (v >> 5) & 7, q = v >> 8;
-    const int ks = ks0 + (c >> 1);
-    if (ks < KS) planes[(long long)((ks * 3 + q) * 2 + (c & 1)) * lda + m0 + r] = tile[q][c][r];
+  for (int i = 0; i < 6; ++i) {  // 4 K-steps x 3 planes x 2 halves x 64 rows = 6 vectors per thread
+    const int idx = tid + 256 * i;
+    const int r = idx & 63, u = idx >> 6;  // u = (ksl*3 + q)*2 + h
+    const int h = u & 1, q = (u >> 1) % 3, ksl = u / 6;
+    const int ks = ks0 + ksl;
+    if (ks < KS)
+      planes[(long long)((ks * 3 + q) * 2 + h) * lda + m0 + r] =
+          *reinterpret_cast<const bf16x8*>(&tile[(q * R + r) * LDP + ksl * 16 + h * 8]);
   }
 }
 

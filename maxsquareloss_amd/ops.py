@@ -398,30 +398,38 @@ class ResidualGrad:
 
 
 # --------------------------------------------------------------------------- 1x1 conv, per-GEMM dispatch
-def conv1x1_plan(cin, cout, p, form="bf16x6"):
+def conv1x1_plan(cin, cout, p, form="bf16x6", residual=False):
     """Implementation of each of the three GEMMs of a stride-1 1x1 conv: (fwd, dgrad, wgrad), each
     "hip" (the bf16x6 pointwise kernels, fp32 form bf16x6 only), "miopen" or "hipblaslt".
+    `residual`: the data gradient also sums in an identity residual's gradient (ops.ResidualGrad),
+    which the HIP kernel and hipBLASLt do in the GEMM while MIOpen needs a separate add.
 
     Per-GEMM winners of every 1x1 shape the UDA step runs, timed on MI355X in isolation
     (scripts/bench_conv1x1_dispatch.py, profiles/r02_conv1x1_dispatch.txt), as rules:
-      fwd    HIP on the 33k-px layer1 maps with 64 outputs, and at <= 16k px when cin >= 512 and
-             one side is >= 1024 channels (layer3/4 conv1/conv3/downsample); MIOpen elsewhere;
-      dgrad  HIP at <= 16k px when one side is >= 1024 and both >= 256, except the narrowing
-             1024 -> 256 (MIOpen wins there); else hipBLASLt when cout > cin or at 33k px, else MIOpen;
-      wgrad  HIP at 33k px and on the 2048-channel layer4 GEMMs (k_wgrad_x6 with one tap),
-             hipBLASLt addmm elsewhere.
+      fwd    HIP on the 33k-px layer1 maps, and at <= 16k px when cin >= 512 and one side is >= 1024
+             channels (layer3/4 conv1/conv3/downsample); MIOpen elsewhere (256 -> 1024: HIP wins in
+             isolation on some boxes, MIOpen in the full step - scripts/bench_plan_ab.py);
+      dgrad  HIP on the narrowing 33k-px GEMM (256 -> 64), and at <= 16k px when one side is >= 1024
+             and both >= 256, except the narrowing 1024 -> 256 without a residual (MIOpen wins
+             there); else hipBLASLt when cout > cin or at 33k px, else MIOpen;
+      wgrad  HIP at 33k px, on the >= 1024-input and the 2048-channel GEMMs (k_wgrad_x6 with one
+             tap), hipBLASLt addmm elsewhere.
+    With the residual, the narrowing 1024 -> 256 data gradient goes to the HIP kernel too (its
+    accumulating form beats MIOpen + add by 3-4 us on every box measured).  The HIP forward-form
+    GEMMs run the hybrid schedule (SkArgs: data-parallel rounds + a stream-K remainder), which
+    is what makes them win on the >= 512-tile shapes (256 -> 1024: 53 vs 61 us pure stream-K).
     """
     x6 = form == "bf16x6"
     big = p > 16384
-    fwd = "hip" if x6 and ((big and cout <= 64) or (not big and cin >= 512 and max(cin, cout) >= 1024)) \
-        else "miopen"
-    if x6 and not big and max(cin, cout) >= 1024 and min(cin, cout) >= 256 and not (cin > cout and cout < 512):
+    wide = max(cin, cout) >= 1024 and min(cin, cout) >= 256
+    fwd = "hip" if x6 and (big or (wide and cin >= 512)) else "miopen"
+    if x6 and ((big and cin > cout) or (not big and wide and (residual or not (cin > cout and cout < 512)))):
         dgrad = "hip"
     elif cout > cin or big:
         dgrad = "hipblaslt"
     else:
         dgrad = "miopen"
-    wgrad = "hip" if big or (x6 and max(cin, cout) >= 2048) else "hipblaslt"
+    wgrad = "hip" if big or (x6 and (max(cin, cout) >= 2048 or cin >= 1024)) else "hipblaslt"
     return fwd, dgrad, wgrad
 
 
@@ -444,10 +452,10 @@ class _Conv1x1(Function):
         form = f32_form()
         ctx.hold = hold
         ctx.form = form
-        key = (cin, cout, p, form)
+        key = (cin, cout, p, form, hold is not None)
         plan = _PLANS.get(key)
         if plan is None:
-            plan = _PLANS[key] = conv1x1_plan(cin, cout, p, form)
+            plan = _PLANS[key] = conv1x1_plan(cin, cout, p, form, hold is not None)
         if plan[0] == "hip":
             lib = hip.load()
             packed = cache.get([weight], cin, cout, 0)

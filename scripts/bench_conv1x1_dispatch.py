@@ -34,6 +34,8 @@ def t(fn, iters=15):
 
 def main():
     lib = hip.load()
+    if "--sk-hybrid" in sys.argv:  # A/B of the forward-form schedule (msl_conv_set_sk_hybrid)
+        hip.check(lib.msl_conv_set_sk_hybrid(int(sys.argv[sys.argv.index("--sk-hybrid") + 1])), "sk_hybrid")
     table, tot = {}, {"lib": 0.0, "best": 0.0}
     for (cin, cout, h, w), n in SHAPES.items():
         p = h * w
@@ -68,6 +70,16 @@ def main():
             "hip_x6": t(lambda: lib.msl_pconv_wgrad(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), cin, cout, p, 1,
                                                     wsw.data_ptr(), wsw.numel(), s)),
         }
+        # dx += W^T dy (the identity residual's gradient summed by the data-gradient GEMM,
+        # ops.ResidualGrad): separate add after MIOpen vs the accumulating GEMMs
+        res = torch.zeros_like(x)
+        acc = {
+            "miopen+add": t(lambda: res.add_(torch.ops.aten.convolution_backward(
+                gy, x, wt, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1, (True, False, False))[0])),
+            "hipblaslt_addmm": t(lambda: res.view(cin, p).addmm_(w2.t(), g2)),
+            "hip_x6_acc": t(lambda: lib.msl_pconv_dgrad_acc(gy.data_ptr(), packed_d.data_ptr(), res.data_ptr(), cin,
+                                                            cout, p, 1, ctr, wsd.data_ptr(), wsd.numel(), s)),
+        }
         pack = t(lambda: (lib.msl_pconv_pack(wt.data_ptr(), cin, cout, 0, packed.data_ptr(), s),
                           lib.msl_pconv_pack(wt.data_ptr(), cin, cout, 1, packed_d.data_ptr(), s)))
         best = {k: min(v, key=v.get) for k, v in r.items()}
@@ -80,6 +92,8 @@ def main():
         print(f"{cin:5d}->{cout:5d} P {p:6d} x{n:2d} | " + " | ".join(
             f"{k}: " + " ".join(f"{m} {v:6.1f}" for m, v in r[k].items()) for k in r) + f" | packs {pack:5.1f} | best {best}",
             flush=True)
+        print("        dgrad accumulating into the residual gradient: " +
+              " ".join(f"{m} {v:6.1f}" for m, v in acc.items()), flush=True)
     print(f"per UDA step: library mix {tot['lib'] / 1e3:.2f} ms, per-GEMM best {tot['best'] / 1e3:.2f} ms", flush=True)
     print("TABLE " + json.dumps(table), flush=True)
 

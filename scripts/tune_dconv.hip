@@ -88,7 +88,7 @@ float run_fwd_sk(const Shape& sh, const float* x, const float* wp, float* y, flo
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = PW ? 0 : sh.dil; a.dil1 = 0;
   a.ksteps = a.ncb * taps; a.kps = a.ksteps; a.slab = 0; a.taps = taps;
-  SkArgs sk;
+  SkArgs sk{};
   sk.part = ws; sk.flags = flags;
   sk.tiles_m = (sh.cout + BM - 1) / BM; sk.tiles_n = (P + BN - 1) / BN; sk.KS = a.ksteps / G; sk.NW = NW;
   sk.T = sk.tiles_m * sk.tiles_n * sk.KS;
@@ -128,7 +128,7 @@ float run_x6reg(const Shape& sh, const float* x, const float* wp, float* y, floa
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = PW ? 0 : sh.dil; a.dil1 = 0;
   a.ksteps = a.ncb * taps; a.kps = a.ksteps; a.slab = 0; a.taps = taps;
-  SkArgs sk;
+  SkArgs sk{};
   sk.part = ws; sk.flags = nullptr;
   sk.tiles_m = (sh.cout + 127) / 128; sk.tiles_n = (P + 127) / 128; sk.KS = a.ksteps;
   sk.T = sk.tiles_m * sk.tiles_n * sk.KS;
@@ -161,7 +161,7 @@ float run_rg(const Shape& sh, const float* x, const float* wp, float* y, float* 
   a.M = sh.cout; a.lda = lda; a.H = sh.h; a.W = sh.w; a.P = P; a.cimg = sh.cin;
   a.ncb = (sh.cin + 15) / 16; a.dil0 = sh.dil; a.dil1 = 0;
   a.ksteps = a.ncb * 9; a.kps = a.ksteps; a.slab = 0; a.taps = 9;
-  SkArgs sk;
+  SkArgs sk{};
   sk.part = ws; sk.flags = nullptr;
   sk.tiles_m = (sh.cout + BM - 1) / BM; sk.tiles_n = (P + 127) / 128; sk.KS = a.ncb * 3;
   sk.T = sk.tiles_m * sk.tiles_n * sk.KS;
@@ -248,7 +248,7 @@ float run_wgrad_x6(const Shape& sh, const float* x, const float* dy, float* dw, 
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_split_rows, dim3(a.lda / 32, (a.KS + 3) / 4), dim3(256), 0, 0, dy, a.M, P, a.KS, a.lda, planes);
+    hipLaunchKernelGGL(k_split_rows, dim3(a.lda / 64, (a.KS + 3) / 4), dim3(256), 0, 0, dy, a.M, P, a.KS, a.lda, planes);
     if (split_only) continue;
     hipLaunchKernelGGL(k_wgrad_x6, dim3(a.NW), dim3(256), 0, 0, a);
     hipLaunchKernelGGL((k_wsk_reduce<128, 128>), dim3(128 * 128 / 4 * 9 / 256, a.tiles_m * a.tiles_n), dim3(256), 0, 0, a);

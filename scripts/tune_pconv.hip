@@ -50,7 +50,7 @@ float run_sk(const Shape& sh, const float* x, const float* wp, float* y, float* 
   a.ncb = (sh.cimg + 15) / 16; a.dil0 = 0; a.dil1 = 0;
   a.ksteps = a.ncb; a.kps = a.ksteps; a.slab = 0; a.taps = 1;
   if (a.ksteps % G) return 1e9f;
-  SkArgs sk;
+  SkArgs sk{};
   sk.part = ws; sk.flags = flags;
   sk.tiles_m = (sh.M + BM - 1) / BM; sk.tiles_n = (sh.P + BN - 1) / BN; sk.KS = a.ksteps / G;
   sk.T = sk.tiles_m * sk.tiles_n * sk.KS;

@@ -552,3 +552,39 @@ def test_bottleneck_fused_residual_grad(f32_form, monkeypatch):
     assert _rel(out[True][1], out[False][1].double()) < 1e-6
     for a, b in zip(out[True][2], out[False][2]):
         assert _rel(a, b.double()) < 1e-6
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(256, 1024, 65, 129), (512, 2048, 64, 128), (2048, 512, 65, 129),
+                                           (1024, 2048, 17, 33)])
+def test_sk_hybrid_schedule(cin, cout, h, w, f32_form):
+    """Forward-form schedule: data-parallel rounds + a stream-K remainder (default; 528 / 1056
+    tiles leave 16 / 32 split tiles, 2048 x 8192 is exactly 1024 whole tiles and launches no
+    reduce) and pure stream-K (msl_conv_set_sk_hybrid(0)) both match fp64, forward and data
+    gradient."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    g = torch.Generator().manual_seed(cin + 11 * cout)
+    x = torch.randn(1, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 1, 1, generator=g) * 0.05
+    gy = torch.randn(1, cout, h, w, generator=g)
+    xr, wr = x.double().requires_grad_(), wt.double().requires_grad_()
+    yr = F.conv2d(xr, wr)
+    yr.backward(gy.double())
+    outs = []
+    try:
+        for hybrid in (1, 0):
+            assert lib.msl_conv_set_sk_hybrid(hybrid) == 0
+            xg = x.to(DEV).requires_grad_()
+            wg = wt.to(DEV).requires_grad_()
+            y = ops.pconv(xg, wg, ops.PackCache(pointwise=True))
+            y.backward(gy.to(DEV))
+            torch.cuda.synchronize()
+            assert _rel(y, yr) < 1e-5, hybrid
+            assert _rel(xg.grad, xr.grad) < 1e-5, hybrid
+            outs.append((y.detach(), xg.grad))
+    finally:
+        lib.msl_conv_set_sk_hybrid(1)
+    # the two schedules differ only in the fp32 summation order of split tiles
+    assert _rel(outs[0][0], outs[1][0].double()) < 4e-6
+    assert _rel(outs[0][1], outs[1][1].double()) < 4e-6
+    assert lib.msl_conv_set_sk_hybrid(2) != 0

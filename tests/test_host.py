@@ -140,20 +140,32 @@ def test_conv1x1_plan_matches_measured_winners():
     10 % or 4 us of the best: the 20-us GEMMs move by that much from one box to the next)."""
     from maxsquareloss_amd import ops
     table = {}
+    names = {"hip_x6": "hip", "miopen+add": "miopen", "hipblaslt_addmm": "hipblaslt", "hip_x6_acc": "hip"}
+    key = None
     for line in open(os.path.join(ROOT, "profiles", "r02_conv1x1_dispatch.txt")):
         m = re.match(r"\s*(\d+)->\s*(\d+) P\s+(\d+) x\s*\d+ \| (.*) \| packs", line)
-        if not m:
+        if m:
+            key = (int(m.group(1)), int(m.group(2)), int(m.group(3)))
+            table[key] = {}
+            for part in m.group(4).split(" | "):
+                gemm, rest = part.split(": ")
+                vals = rest.split()
+                table[key][gemm] = {names.get(vals[i], vals[i]): float(vals[i + 1]) for i in range(0, len(vals), 2)}
             continue
-        times = {}
-        for part in m.group(4).split(" | "):
-            gemm, rest = part.split(": ")
-            vals = rest.split()
-            times[gemm] = {vals[i].replace("hip_x6", "hip"): float(vals[i + 1]) for i in range(0, len(vals), 2)}
-        table[(int(m.group(1)), int(m.group(2)), int(m.group(3)))] = times
+        m = re.match(r"\s*dgrad accumulating into the residual gradient: (.*)", line)
+        if m and key is not None:  # the same shape's data gradient fused with an identity residual
+            vals = m.group(1).split()
+            table[key]["dgrad_res"] = {names[vals[i]]: float(vals[i + 1]) for i in range(0, len(vals), 2)}
     assert len(table) == 13
+    # the shapes whose data gradient carries an identity residual in the model (Bottleneck.conv1
+    # of blocks 1.. of each layer)
+    res_shapes = {(256, 64), (512, 128), (1024, 256), (2048, 512)}
     for (cin, cout, p), times in table.items():
         plan = dict(zip(("fwd", "dgrad", "wgrad"), ops.conv1x1_plan(cin, cout, p)))
+        plan["dgrad_res"] = ops.conv1x1_plan(cin, cout, p, residual=True)[1]
         for gemm, t in times.items():
+            if gemm == "dgrad_res" and (cin, cout) not in res_shapes:
+                continue
             best = min(t.values())
             assert t[plan[gemm]] <= max(1.10 * best, best + 4.0), (cin, cout, p, gemm, plan[gemm], t)
         # the mfma_f32 form: fwd and dgrad on the libraries (its HIP pointwise kernels are slower)
