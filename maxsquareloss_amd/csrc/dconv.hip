@@ -339,6 +339,15 @@ static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
   return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
 }
 
+// The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
+template <int BM, int G, int ST, int WM, int WN, int MT>
+static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
+  if (accum)
+    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
+  else
+    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, false>), grid, block, 0, st, a, sk);
+}
+
 template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int dil0,
@@ -406,25 +415,25 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
       // the x6 kernel stages its weights from the bf16 planes that pack() split once, behind
       // the fp32 part of the same buffer (M > 64 <=> 128-row tiles)
       a.Ax6 = reinterpret_cast<const __bf16*>(packed + (long long)pl.ksteps * kCB * a.lda);
-      hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 4, 2, 2, false, kMathX6P>), grid, block, 0, st, a, sk);
+      launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
       MSL_CHECK_LAUNCH();
       if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 128) {
       if (pl.G == 2)
-        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 2, 2, 2, 2, false, MT>), grid, block, 0, st, a, sk);
+        launch_sk<128, 2, 2, 2, 2, MT>(accum, grid, block, st, a, sk);
       else
-        hipLaunchKernelGGL((k_igemm_fwd_sk<128, kSkBN, 1, 3, 2, 2, false, MT>), grid, block, 0, st, a, sk);
+        launch_sk<128, 1, 3, 2, 2, MT>(accum, grid, block, st, a, sk);
       MSL_CHECK_LAUNCH();
       if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
       if (pl.G == 2)
-        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 2, 2, 2, 2, false, MS>), grid, block, 0, st, a, sk);
+        launch_sk<64, 2, 2, 2, 2, MS>(accum, grid, block, st, a, sk);
       else
-        hipLaunchKernelGGL((k_igemm_fwd_sk<64, kSkBN, 1, 3, 2, 2, false, MS>), grid, block, 0, st, a, sk);
+        launch_sk<64, 1, 3, 2, 2, MS>(accum, grid, block, st, a, sk);
       MSL_CHECK_LAUNCH();
       if (reduce) hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
     } else {
-      hipLaunchKernelGGL((k_igemm_fwd_sk<32, kSkBN, 2, 2, 1, 4, false, MS>), grid, block, 0, st, a, sk);
+      launch_sk<32, 2, 2, 1, 4, MS>(accum, grid, block, st, a, sk);
       MSL_CHECK_LAUNCH();
       if (reduce) hipLaunchKernelGGL((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
     }

@@ -719,7 +719,7 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
   return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
 }
 
-template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0>
+template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false>
 __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -996,28 +996,26 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
     const bool full_m = m0 + BM <= a.M;
-    auto out_off = [&](int i, int j, int r) {
-      const int n = n0 + wn + j * 32 + (lane & 31);
-      const int mr = m0 + wm + i * 32 + 4 * (lane >> 5) + (r & 3) + 8 * (r >> 2);
-      return (n < a.P && (full_m || mr < a.M)) ? (unsigned)((mr * a.P + n) * 4) : OOB;
-    };
-    if (a.accum) {
-      // accumulate epilogue (msl_pconv_dgrad_acc): every old value is loaded before the first
-      // store, so the loads are in flight together (load-add-store per element serialised each
-      // load behind the previous element's store: +30 us on a 2048 x 8385 output)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            acc[i][j][r] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, out_off(i, j, r), 0, 0));
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn + j * 32 + (lane & 31);
         const int mrow = m0 + wm + i * 32 + 4 * (lane >> 5);
+        const unsigned voff = n < a.P ? (unsigned)((mrow * a.P + n) * 4) : OOB;
+        // ACC (msl_pconv_dgrad_acc, a compile-time form so the plain epilogue keeps its
+        // registers): the fragment's 16 old values are loaded before its first store, so they are
+        // in flight together (load-add-store per element serialised each load behind the
+        // previous element's store: +30 us on a 2048 x 8385 output)
+        float old[16];
+        if constexpr (ACC) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ro = (r & 3) + 8 * (r >> 2);
+            const unsigned off = full_m ? voff + ro * a.P * 4 : (mrow + ro < a.M ? voff + ro * a.P * 4 : OOB);
+            old[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, off, 0, 0));
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ro = (r & 3) + 8 * (r >> 2);
@@ -1027,7 +1025,9 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
             for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + mrow + ro];
             v += bsum;
           }
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, out_off(i, j, r), 0, 0);
+          const unsigned off = full_m ? voff + ro * a.P * 4 : (mrow + ro < a.M ? voff + ro * a.P * 4 : OOB);
+          if constexpr (ACC) v = old[r] + v;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, off, 0, 0);
         }
       }
   }

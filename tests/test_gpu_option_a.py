@@ -7,7 +7,8 @@ the same model, weights and target image.
 
 Tolerances: one forward/backward of the same network from the same state, so the two paths
 differ only by fp32 rounding of the loss arithmetic (torch softmax vs the fused kernel): losses
-1e-5 relative; the IW class histogram (argmax of the two paths' probabilities - torch's softmax
+1e-5 relative, the guidance CE with up to two pixels' share on top (a pixel whose max probability
+sits within rounding of the 0.2 threshold can land on either side of it); the IW class histogram (argmax of the two paths' probabilities - torch's softmax
 vs the kernel's) within 0.05 % of the pixels; the parameter gradients per tensor within 4x the
 distance between two runs of the fused path itself, or 1e-4 of the tensor's norm.  (MIOpen's
 stride-2 1x1 data gradients in layer2 block 0 are not bit-reproducible (~2e-7), and the bs=1 BN
@@ -57,7 +58,11 @@ def _reference_train_target(tr, pred, hard_loss):
     loss_target_2 = tr.args.lambda_seg * tr.args.lambda_target * hard_loss(pred_2, label_2)
     loss_target_ = loss_target_ + loss_target_2
     loss_target_.backward()
-    return loss_target.detach(), loss_target_2.detach(), int(mask.sum())
+    # one pixel's share of loss_target_2 at most (the tolerance for a pixel whose max probability
+    # sits on the threshold and falls on the other side of it in the fused kernel's rounding)
+    ce = F.cross_entropy(pred_2.detach(), label_2, ignore_index=-1, reduction="none")
+    pix = tr.args.lambda_seg * tr.args.lambda_target * ce.max().item() / max(int((label_2 >= 0).sum()), 1)
+    return loss_target.detach(), loss_target_2.detach(), int(mask.sum()), pix
 
 
 def _grads(model):
@@ -86,8 +91,10 @@ def test_reference_train_target_through_drop_in_modules(mode):
     g_ref = _grads(tr.model)
     torch.cuda.synchronize()
     assert ref[2] > 0  # the guidance label has pixels (threshold 0.2)
-    for a, b in zip(fused, ref[:2]):
-        assert a.item() == pytest.approx(b.item(), rel=1e-5), (mode, fused, ref)
+    assert fused[0].item() == pytest.approx(ref[0].item(), rel=1e-5), (mode, fused, ref)
+    # the guidance CE: 1e-5, plus up to two pixels whose mask / argmax flips between torch's
+    # softmax and the kernel's (maxpred within rounding of the threshold)
+    assert abs(fused[1].item() - ref[1].item()) <= 1e-5 * abs(ref[1].item()) + 2 * ref[3], (mode, fused, ref)
     assert len(g_fused) == len(g_ref) == len(g_fused2)
     for i, (a, a2, b) in enumerate(zip(g_fused, g_fused2, g_ref)):
         err, spread = (a - b).norm().item(), (a - a2).norm().item()
