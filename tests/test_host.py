@@ -292,3 +292,30 @@ def test_grad_reducer_two_ranks_gloo():
         assert got[r][2] == pytest.approx(1.0 / world)
         live = got[r][1]
         assert live.sum() == 5  # l0 (w, b), l1 (w, through the sink), l2 (w, b); the dead l3 excluded
+
+
+def test_hot_kernels_keep_their_occupancy():
+    """The compiler's resource report of the last build (Makefile: dconv.o.remarks): the forward-form
+    x6 GEMM and the x6 weight gradient run two workgroups (8 waves) per CU, so they must keep
+    <= 256 VGPRs + AGPRs (2 waves per SIMD), and no msl kernel spills VGPRs to scratch.  (An
+    epilogue change once took the forward to 242 VGPRs and one wave per SIMD: layer3 op 67 -> 90 us.)"""
+    path = os.path.join(ROOT, "maxsquareloss_amd", "_lib", "obj", "dconv.o.remarks")
+    if not os.path.exists(path):
+        pytest.skip("no resource report: build the library first (__graft_entry__.build())")
+    kern, info = None, {}
+    for line in open(path):
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            kern = m.group(1)
+            info[kern] = {}
+            continue
+        m = re.search(r"remark:\s+(VGPRs|AGPRs|Occupancy \[waves/SIMD\]|VGPRs Spill): (\d+)", line)
+        if m and kern:
+            info[kern][m.group(1)] = int(m.group(2))
+    hot = [k for k in info if k.startswith("_ZN3msl14k_igemm_fwd_skILi128ELi128ELi1ELi4ELi2ELi2ELb0ELi3E")
+           or k.startswith("_ZN3msl10k_wgrad_x6")]
+    assert len(hot) == 3, sorted(info)  # the x6 forward (plain, accumulating) and the x6 wgrad
+    for k in hot:
+        assert info[k]["Occupancy [waves/SIMD]"] >= 2, (k, info[k])
+    for k, v in info.items():
+        assert v.get("VGPRs Spill", 0) == 0, (k, v)
