@@ -1033,6 +1033,28 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   }
 }
 
+// sum of pieces w_lo..w_hi in that order (deterministic), eight loads in flight per step: a tile
+// of the 132-tile layer3 GEMMs has 4-6 pieces, a chunked weight-gradient tile 7-14
+template <typename F>
+__device__ __forceinline__ float4 sum_pieces(int w_lo, int w_hi, F&& piece) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int wc = w_lo; wc <= w_hi; wc += 8) {
+    float4 p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (wc + u <= w_hi) p[u] = piece(wc + u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (wc + u <= w_hi) {
+        acc.x += p[u].x;
+        acc.y += p[u].y;
+        acc.z += p[u].z;
+        acc.w += p[u].w;
+      }
+  }
+  return acc;
+}
+
 // Sum of the pieces of every split stream-K tile (worker order: deterministic), + the branch
 // biases, into the output.  grid = (BM*BN / 1024 chunks, tiles - tdp: the stream-K tiles); blocks
 // of unsplit tiles exit.  Pieces are row-major [BM][BN]: one float4 of 4 consecutive pixels per
@@ -1053,18 +1075,7 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
       const int slot = sk_start(wc, sk.T, sk.NW) > tl * sk.KS ? 0 : 1;
       return part[(long long)(wc * 2 + slot) * (PSZ / 4) + g];
     };
-    auto add = [](float4& acc, const float4& v) { acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w; };
-    // four loads in flight per step (the sum stays in worker order)
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int wc = w_lo;
-    for (; wc + 3 <= w_hi; wc += 4) {
-      const float4 p0 = piece(wc), p1 = piece(wc + 1), p2 = piece(wc + 2), p3 = piece(wc + 3);
-      add(acc, p0);
-      add(acc, p1);
-      add(acc, p2);
-      add(acc, p3);
-    }
-    for (; wc <= w_hi; ++wc) add(acc, piece(wc));
+    const float4 acc = sum_pieces(w_lo, w_hi, piece);
     const int m = m0 + (g * 4) / BN, n = n0 + (g * 4) % BN;
     if (m >= a.M) continue;
     float bsum = 0.f;
@@ -1376,6 +1387,10 @@ struct WskArgs {
   // (consecutive items) the same pixel window of every tile: the window's dY and X rows stay in
   // that XCD's L2 across all tiles and taps.
   int nchunk, kchunk, ntiles;
+  // pointwise (taps = 1) with the operands swapped (k_wgrad_x6 pre-splits the operand with fewer
+  // rows): dy = the image [cin][P], x = dY [cout][P], M = cin, N = cout, so the tiles hold dW^T
+  // and k_wsk_reduce writes them transposed into dw [cout][cin]
+  int trans;
 };
 
 constexpr int kWskBK = 64;
@@ -1554,6 +1569,48 @@ __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
   const int br = blockIdx.y / gsz;
   const int rem = blockIdx.y - br * gsz;
   const int tn = rem / a.tiles_m, tm = rem - tn * a.tiles_m;
+  if constexpr (BM == 128 && BN == 128) {
+    if (a.trans) {
+      // dW^T tile (pointwise, operands swapped; taps = nbranch = 1): block = one 32x32 sub-tile,
+      // summed as float4 rows, transposed through LDS, written as 128-B runs of dw rows
+      __shared__ float tt[32][33];
+      const int sr = blockIdx.x >> 2, sc = blockIdx.x & 3;
+      const int t = tn * a.tiles_m + tm;
+      const int r = threadIdx.x >> 3, c4 = (threadIdx.x & 7) * 4;
+      const int g4 = ((sr * 32 + r) * BN + sc * 32 + c4) / 4;
+      const float4* __restrict__ part = reinterpret_cast<const float4*>(a.part);
+      const int w_lo = a.nchunk > 0 ? 0 : sk_worker_of(t * a.KS, a.T, a.NW);
+      const int w_hi = a.nchunk > 0 ? a.nchunk - 1 : sk_worker_of((t + 1) * a.KS - 1, a.T, a.NW);
+      const float4 v = sum_pieces(w_lo, w_hi, [&](int wc) {
+        if (a.nchunk > 0) return part[(long long)(wc * a.ntiles + t) * a.slots * P4 + g4];
+        return part[(long long)(wc * a.slots + t - sk_start(wc, a.T, a.NW) / a.KS) * P4 + g4];
+      });
+      tt[r][c4] = v.x;
+      tt[r][c4 + 1] = v.y;
+      tt[r][c4 + 2] = v.z;
+      tt[r][c4 + 3] = v.w;
+      __syncthreads();
+      // thread -> dW row n = n0 + sc*32 + (tid >> 3) (a cout), columns m = m0 + sr*32 + rr .. + 3
+      const int n = tn * BN + sc * 32 + (threadIdx.x >> 3), rr = (threadIdx.x & 7) * 4;
+      if (n >= a.N) return;
+      float* dst = a.dw + (long long)n * a.M + tm * BM + sr * 32 + rr;
+      const int mm = a.M - (tm * BM + sr * 32 + rr);
+      float vals[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vals[q] = tt[rr + q][threadIdx.x >> 3];
+      if (a.accumulate) {
+        float old[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) old[q] = q < mm ? dst[q] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vals[q] = old[q] + vals[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < mm) dst[q] = vals[q];
+      return;
+    }
+  }
   const int e = blockIdx.x * 256 + threadIdx.x;
   const int tap = e / P4, g4 = e - tap * P4;
   if (tap >= a.taps) return;
@@ -1569,21 +1626,20 @@ __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
     const int slot = t - sk_start(wc, a.T, a.NW) / a.KS;
     return part[(long long)(wc * a.slots + slot) * P4 + g4];
   };
-  auto add = [](float4& s, const float4& x) { s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w; };
-  // four loads in flight per step (the sum stays in worker order)
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  int wc = w_lo;
-  for (; wc + 3 <= w_hi; wc += 4) {
-    const float4 p0 = piece(wc), p1 = piece(wc + 1), p2 = piece(wc + 2), p3 = piece(wc + 3);
-    add(v, p0); add(v, p1); add(v, p2); add(v, p3);
-  }
-  for (; wc <= w_hi; ++wc) add(v, piece(wc));
+  const float4 v = sum_pieces(w_lo, w_hi, piece);
   float* dst = a.dw + br * a.cbranch + ((long long)m * a.N + n) * a.taps + tap;
-  const float vals[4] = {v.x, v.y, v.z, v.w};
+  float vals[4] = {v.x, v.y, v.z, v.w};
   const int nn = min(4, a.N - n);
+  if (a.accumulate) {  // all old values loaded before the first store
+    float old[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) old[c] = c < nn ? dst[c * a.taps] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) vals[c] = old[c] + vals[c];
+  }
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    if (c < nn) dst[c * a.taps] = a.accumulate ? dst[c * a.taps] + vals[c] : vals[c];
+    if (c < nn) dst[c * a.taps] = vals[c];
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -412,8 +412,9 @@ def conv1x1_plan(cin, cout, p, form="bf16x6", residual=False):
       dgrad  HIP on the narrowing 33k-px GEMM (256 -> 64), and at <= 16k px when one side is >= 1024
              and both >= 256, except the narrowing 1024 -> 256 without a residual (MIOpen wins
              there); else hipBLASLt when cout > cin or at 33k px, else MIOpen;
-      wgrad  HIP at 33k px, on the >= 1024-input and the 2048-channel GEMMs (k_wgrad_x6 with one
-             tap), hipBLASLt addmm elsewhere.
+      wgrad  HIP at 33k px and at <= 16k px when one side is >= 1024 channels and both >= 256
+             (k_wgrad_x6 with one tap; with cout > cin on swapped operands, so the narrower
+             operand is the pre-split one), hipBLASLt addmm elsewhere.
     With the residual, the narrowing 1024 -> 256 data gradient goes to the HIP kernel too (its
     accumulating form beats MIOpen + add by 3-4 us on every box measured).  The HIP forward-form
     GEMMs run the hybrid schedule (SkArgs: data-parallel rounds + a stream-K remainder), which
@@ -429,7 +430,7 @@ def conv1x1_plan(cin, cout, p, form="bf16x6", residual=False):
         dgrad = "hipblaslt"
     else:
         dgrad = "miopen"
-    wgrad = "hip" if big or (x6 and (max(cin, cout) >= 2048 or cin >= 1024)) else "hipblaslt"
+    wgrad = "hip" if big or (x6 and wide) else "hipblaslt"
     return fwd, dgrad, wgrad
 
 

@@ -3,6 +3,7 @@ ops.conv1x1_plan replaced by a variant.  Usage: bench_plan_ab.py VARIANT [bench.
   new   the current ops.conv1x1_plan
   old   the rules before the hybrid schedule (fwd HIP only with cin >= 512, 1024->256 residual dgrad
         on MIOpen + add, 1024-input wgrads on hipBLASLt)
+  wgold current rules with the 256 -> 1024 and 512 -> 1024 weight gradients on hipBLASLt
   fwdm  "new" with the 256 -> 1024 forward on MIOpen (adopted after this A/B: profiles/r02_plan_ab.txt)"""
 import os
 import runpy
@@ -34,7 +35,12 @@ def fwdm(cin, cout, p, form="bf16x6", residual=False):
     return (("miopen",) + plan[1:]) if (cin, cout) == (256, 1024) else plan
 
 
-ops.conv1x1_plan = {"new": cur, "old": old, "fwdm": fwdm}[variant]
+def wgold(cin, cout, p, form="bf16x6", residual=False):
+    plan = cur(cin, cout, p, form, residual)
+    return (plan[:2] + ("hipblaslt",)) if (cin, cout) in ((256, 1024), (512, 1024)) else plan
+
+
+ops.conv1x1_plan = {"new": cur, "old": old, "fwdm": fwdm, "wgold": wgold}[variant]
 sys.argv = ["bench.py"] + sys.argv[2:]
 runpy.run_path(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"),
                run_name="__main__")

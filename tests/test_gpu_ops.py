@@ -588,3 +588,29 @@ def test_sk_hybrid_schedule(cin, cout, h, w, f32_form):
     assert _rel(outs[0][0], outs[1][0].double()) < 4e-6
     assert _rel(outs[0][1], outs[1][1].double()) < 4e-6
     assert lib.msl_conv_set_sk_hybrid(2) != 0
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(256, 1024, 65, 129), (512, 2048, 17, 33), (128, 512, 33, 65),
+                                           (1024, 256, 65, 129), (200, 328, 9, 31)])
+def test_pconv_wgrad_accumulate_both_orientations(cin, cout, h, w):
+    """msl_pconv_wgrad, accumulate = 1, bf16x6: with cout > cin the kernel runs on the swapped
+    operands (the image pre-split, dW^T tiles transposed by the reduce); either way dW += dy x^T."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    prev = ops.set_f32_form("bf16x6")
+    try:
+        g = torch.Generator().manual_seed(cin * 5 + cout)
+        p = h * w
+        x = torch.randn(cin, p, generator=g)
+        gy = torch.randn(cout, p, generator=g)
+        dw0 = torch.randn(cout, cin, generator=g)
+        ref = dw0.double() + gy.double() @ x.double().t()
+        xd, gd, dw = x.to(DEV), gy.to(DEV), dw0.to(DEV)
+        wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
+        ws = hip.workspace(wsb, xd.device)
+        assert lib.msl_pconv_wgrad(xd.data_ptr(), gd.data_ptr(), dw.data_ptr(), cin, cout, p, 1, ws.data_ptr(), wsb,
+                                   hip.stream_ptr()) == 0
+        torch.cuda.synchronize()
+        assert _rel(dw, ref) < 1e-5
+    finally:
+        ops.set_f32_form(prev)

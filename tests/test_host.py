@@ -160,11 +160,14 @@ def test_conv1x1_plan_matches_measured_winners():
     # the shapes whose data gradient carries an identity residual in the model (Bottleneck.conv1
     # of blocks 1.. of each layer)
     res_shapes = {(256, 64), (512, 128), (1024, 256), (2048, 512)}
+    # decided by the full-step A/B instead (profiles/r02_plan_ab.txt): the 256 -> 1024 forward
+    # stays on MIOpen, which wins in the step on the boxes where HIP loses in isolation
+    step_ab = {(256, 1024, "fwd")}
     for (cin, cout, p), times in table.items():
         plan = dict(zip(("fwd", "dgrad", "wgrad"), ops.conv1x1_plan(cin, cout, p)))
         plan["dgrad_res"] = ops.conv1x1_plan(cin, cout, p, residual=True)[1]
         for gemm, t in times.items():
-            if gemm == "dgrad_res" and (cin, cout) not in res_shapes:
+            if (gemm == "dgrad_res" and (cin, cout) not in res_shapes) or (cin, cout, gemm) in step_ab:
                 continue
             best = min(t.values())
             assert t[plan[gemm]] <= max(1.10 * best, best + 4.0), (cin, cout, p, gemm, plan[gemm], t)
