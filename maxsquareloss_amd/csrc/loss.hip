@@ -16,6 +16,8 @@
 // transposed (separable) interpolation weights: rows -> T[C][Ho][Wi] ->
 // d logits[C][Hi][Wi], a fixed-order gather (no atomics).
 #include <math.h>
+#include <cmath>
+
 #include "msl_internal.h"
 
 // No FMA contraction in this file: torch-CPU rounds s*o before subtracting floor(s*o), and
@@ -344,7 +346,22 @@ __device__ __forceinline__ void pixel_grad(const float* __restrict__ L1, const f
   }
 }
 
-// One block per hi-res row oy: G[c][ox] in LDS, then T[c][oy][ix] = sum_ox Wx[ox][ix] G[c][ox].
+// first ox with i0(ox) >= t (i0 is monotone in ox), searched in [lo, hi)
+__device__ __forceinline__ int lb_ox(int t, int lo, int hi, const Geo& g) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (lin(mid, g.sw, g.Wi).i0 >= t) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+// Block (oy, j): hi-res row oy, low-res columns ix in [ixa, ixb) (chunk j of gridDim.y).  The
+// pixels that feed those columns, ox with i0(ox) in [ixa - 1, ixb), get their gradient G[c][ox]
+// in LDS, then T[c][oy][ix] = sum_ox Wx[ox][ix] G[c][ox] in ascending ox (fp64).  Chunks of ~33
+// columns (~280 pixels) instead of a whole row per block: 4x the blocks at a quarter of the LDS,
+// so the latency-bound per-pixel softmax has 3-4x the waves in flight (r01: 130 us per loss).
+// A pixel on a chunk border is computed by both neighbours: the same value, so T is unchanged.
 template <int KIND, int CM>
 __global__ void __launch_bounds__(256) k_bwd_rows(const float* __restrict__ L1,
                                                    const float* __restrict__ L2,
@@ -352,58 +369,63 @@ __global__ void __launch_bounds__(256) k_bwd_rows(const float* __restrict__ L1,
                                                    const float* __restrict__ gin_hi, Geo g, float thr,
                                                    const float* __restrict__ stats,
                                                    const float* __restrict__ gout,
-                                                   float* __restrict__ T) {
+                                                   float* __restrict__ T, int wmax) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* G = sm;                               // [C][Wo]
-  float* wx0 = G + g.C * g.Wo;                 // [Wo]
-  float* wx1 = wx0 + g.Wo;                     // [Wo]
-  int* ix0 = reinterpret_cast<int*>(wx1 + g.Wo);  // [Wo]
-  int* bnd = ix0 + g.Wo;                       // [Wi + 1]: first ox with i0(ox) >= ix
+  float* G = sm;                               // [C][wmax]
+  float* wx0 = G + g.C * wmax;                 // [wmax]
+  float* wx1 = wx0 + wmax;                     // [wmax]
+  int* ix0 = reinterpret_cast<int*>(wx1 + wmax);  // [wmax]
 
   const int oy = blockIdx.x;
+  const int nch = gridDim.y, per = (g.Wi + nch - 1) / nch;
+  const int ixa = blockIdx.y * per, ixb = min(g.Wi, ixa + per);
+  if (ixa >= ixb) return;
+  const int ox_lo = lb_ox(ixa - 1, 0, g.Wo, g);
+  const int ox_hi = ixb >= g.Wi ? g.Wo : lb_ox(ixb, ox_lo, g.Wo, g);
+  const int nw = ox_hi - ox_lo;  // <= wmax (host bound)
   const Lin ly = lin(oy, g.sh, g.Hi);
   float sc = 0.f;
   if (KIND == K_CE || KIND == K_MULTI) sc = gout[0] / stats[1];
   else if (KIND == K_MS) sc = -gout[0] / ((float)g.C * stats[1]);
   else if (KIND == K_IW) sc = -2.f * gout[0] / (float)g.C;
 
-  for (int ox = threadIdx.x; ox < g.Wo; ox += 256) {
+  for (int k = threadIdx.x; k < nw; k += 256) {
+    const int ox = ox_lo + k;
     const Lin lx = lin(ox, g.sw, g.Wi);
-    wx0[ox] = lx.w0;
-    wx1[ox] = lx.w1;
-    ix0[ox] = lx.i0;
+    wx0[k] = lx.w0;
+    wx1[k] = lx.w1;
+    ix0[k] = lx.i0;
     float gr[CM];
     pixel_grad<KIND, CM>(L1, L2, labels, gin_hi, g, stats, thr, sc, oy, ox, ly, gr);
 #pragma unroll
     for (int c = 0; c < CM; ++c)
-      if (c < g.C) G[c * g.Wo + ox] = gr[c];
+      if (c < g.C) G[c * wmax + k] = gr[c];
   }
   __syncthreads();
-  for (int ix = threadIdx.x; ix <= g.Wi; ix += 256) {
-    int lo = 0, hi = g.Wo;  // lower_bound of i0(ox) >= ix over the monotone i0
+  auto bnd = [&](int t) {  // first chunk pixel with i0 >= t (t in [ixa - 1, ixb])
+    int lo = 0, hi = nw;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (ix0[mid] >= ix) hi = mid;
+      if (ix0[mid] >= t) hi = mid;
       else lo = mid + 1;
     }
-    bnd[ix] = lo;
-  }
-  __syncthreads();
+    return lo;
+  };
   const long long plane = (long long)g.Ho * g.Wi;
-  for (int e = threadIdx.x; e < g.C * g.Wi; e += 256) {
-    const int c = e / g.Wi, ix = e - c * g.Wi;
-    const int beg = bnd[ix > 0 ? ix - 1 : 0], end = bnd[ix + 1 <= g.Wi ? ix + 1 : g.Wi];
-    const float* Gc = G + c * g.Wo;
+  const int ncol = ixb - ixa;
+  for (int e = threadIdx.x; e < g.C * ncol; e += 256) {
+    const int c = e / ncol, ix = ixa + (e - c * ncol);
+    const int beg = bnd(ix > 0 ? ix - 1 : 0), end = ix + 1 <= g.Wi - 1 ? bnd(ix + 1) : nw;
+    const float* Gc = G + c * wmax;
     double s = 0.0;  // ~2*Wo/Wi terms; fp64 keeps the gather at fp32-rounding accuracy
-    for (int ox = beg; ox < end; ++ox) {
-      const int i0 = ix0[ox];
+    for (int k = beg; k < end; ++k) {
+      const int i0 = ix0[k];
       const int i1 = i0 + (i0 < g.Wi - 1 ? 1 : 0);
       float w = 0.f;
-      if (i0 == ix) w += wx0[ox];
-      if (i1 == ix) w += wx1[ox];
-      s += (double)w * (double)Gc[ox];
+      if (i0 == ix) w += wx0[k];
+      if (i1 == ix) w += wx1[k];
+      s += (double)w * (double)Gc[k];
     }
-    // ox == Wo-1 may have i0 == Wi-1 == ix with bnd[Wi] == Wo: covered since end <= Wo.
     T[c * plane + (long long)oy * g.Wi + ix] = (float)s;
   }
 }
@@ -610,9 +632,17 @@ static size_t part_bytes(int C) {
 
 static size_t t_bytes(int c, int ho, int wi) { return align_up((size_t)c * ho * wi * 4, 256); }
 
-static size_t rows_lds(const Geo& g) {
-  return (size_t)g.C * g.Wo * 4 + (size_t)g.Wo * 12 + (size_t)(g.Wi + 1) * 4;
+// k_bwd_rows: column chunks per hi-res row, and the widest pixel range a chunk can need: the
+// pixels whose i0 is one of the chunk's columns or the one before, at most ceil(1/sw) + 1 per
+// column (sw = (Wi-1)/(Wo-1), fp32 as torch computes it), clamped to the row
+static int rows_chunks(const Geo& g) { return std::max(1, std::min(8, g.Wi / 32)); }
+static int rows_wmax(const Geo& g) {
+  const int per = (g.Wi + rows_chunks(g) - 1) / rows_chunks(g);
+  if (g.Wi < 2 || !(g.sw > 0.f)) return g.Wo;
+  const long long each = (long long)std::ceil(1.0 / (double)g.sw) + 2;
+  return (int)std::min<long long>(g.Wo, (per + 1) * each);
 }
+static size_t rows_lds(const Geo& g) { return (size_t)rows_wmax(g) * (g.C * 4 + 12); }
 
 #define MSL_DISPATCH_C(C, CM, ...)      \
   do {                                  \
@@ -666,8 +696,8 @@ static int loss_bwd(const float* L1, const float* L2, const int64_t* labels, con
   MSL_DISPATCH_C(c, CM, {
     auto kern = k_bwd_rows<KIND, CM>;
     if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(ho), dim3(256), lds, st, L1, L2, labels, gin_hi, g, thr, stats,
-                       gout, T);
+    hipLaunchKernelGGL(kern, dim3(ho, rows_chunks(g)), dim3(256), lds, st, L1, L2, labels, gin_hi, g, thr,
+                       stats, gout, T, rows_wmax(g));
   });
   MSL_CHECK_LAUNCH();
   const int n = c * hi * wi;

@@ -322,3 +322,24 @@ def test_hot_kernels_keep_their_occupancy():
         assert info[k]["Occupancy [waves/SIMD]"] >= 2, (k, info[k])
     for k, v in info.items():
         assert v.get("VGPRs Spill", 0) == 0, (k, v)
+
+
+@pytest.mark.parametrize("hi,wi,ho,wo", [(65, 129, 512, 1024), (33, 65, 256, 512), (81, 161, 640, 1280),
+                                         (96, 161, 760, 1280), (17, 33, 128, 256), (9, 17, 64, 128), (3, 5, 7, 300)])
+def test_loss_bwd_chunk_lds_bound(hi, wi, ho, wo):
+    """k_bwd_rows sizes its LDS for the widest pixel range a column chunk needs (loss.hip
+    rows_wmax): check that bound against the exact ranges, with torch's fp32 source-index rounding."""
+    sw = np.float32((wi - 1) / (wo - 1)) if wo > 1 else np.float32(0)
+    ox = np.arange(wo, dtype=np.float32)
+    i0 = np.minimum(np.floor(sw * ox).astype(np.int64), wi - 1)
+    nch = max(1, min(8, wi // 32))
+    per = (wi + nch - 1) // nch
+    each = int(np.ceil(1.0 / float(sw))) + 2 if wi >= 2 and sw > 0 else None
+    wmax = wo if each is None else min(wo, (per + 1) * each)
+    for j in range(nch):
+        ixa, ixb = j * per, min(wi, (j + 1) * per)
+        if ixa >= ixb:
+            continue
+        lo = int(np.searchsorted(i0, ixa - 1, side="left"))
+        hi_ = wo if ixb >= wi else int(np.searchsorted(i0, ixb, side="left"))
+        assert hi_ - lo <= wmax, (j, hi_ - lo, wmax)
