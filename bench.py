@@ -62,7 +62,7 @@ def parse():
                     help="bf16 = BASELINE config 5's fp16/bf16 MFMA path (fp32 accumulation)")
     ap.add_argument("--bn-form", default="fused", choices=["fused", "split"],
                     help="BN kernels: one fused launch per call (default) or split statistics/apply launches")
-    ap.add_argument("--f32-form", default=None, choices=["mfma_f32", "bf16x6"],
+    ap.add_argument("--f32-form", default=None, choices=["mfma_f32", "bf16x6", "f16x3"],
                     help="matrix-core form of the fp32 convs (default: the library's)")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: iterations after the first replay one captured hipGraph (single process); 0: eager")
@@ -149,8 +149,9 @@ def main():
     form = ops.f32_form() if a.conv_math == "fp32" else "bf16"
     # the bound of the kernel's own arithmetic: FP32 MFMA, BF16 MFMA, or BF16 MFMA at six
     # products per fp32 product (the bf16x6 form): 2500 / 6 = 416.7 fp32-equivalent TFLOP/s
+    # and FP16 MFMA (same rate) at three products per fp32 product (the f16x3 form): 833.3
     peak = {"mfma_f32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
-            "bf16x6": round(BF16_MFMA_PEAK_TFLOPS / 6, 1)}[form]
+            "bf16x6": round(BF16_MFMA_PEAK_TFLOPS / 6, 1), "f16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1)}[form]
     if traffic is not None and json.load(open(a.pmc)).get("form", "mfma_f32") != form:
         traffic = None  # the committed PMC figure belongs to another form of the kernel
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
@@ -159,6 +160,7 @@ def main():
                                    "passes of this kernel (scripts/gpu_bench_prof.sh), not measured in this run; "
                                    "memory-side bytes incl. Infinity-Cache hits") if traffic is not None else None,
                 "frac_of_fp32_spec": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "frac_of_bf16x6_bound": round(achieved / (BF16_MFMA_PEAK_TFLOPS / 6), 4),
                 "kernel": "dconv3x3 fwd layer3 d=2 (one op call: stream-K k_igemm_fwd_sk + k_sk_reduce; the bf16x6 weight planes are split at pack time, once per SGD step)",
                 "form": form, "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}

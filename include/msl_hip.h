@@ -56,8 +56,12 @@ int msl_counter_elems(void);
 /* Matrix-core form of the fp32 conv entry points (msl_dconv_* / msl_pconv_* without _bf16),
  * process-wide: 0 = v_mfma_f32_32x32x2_f32 (exact fmaf chain), 2 = each fp32 operand split
  * into three bf16 terms, six products per 16-deep K slice on v_mfma_f32_32x32x16_bf16 with fp32
- * accumulation (fp32-accurate; the default).  Returns MSL_ERR_ARG for
- * any other value.  Replaces nothing in the reference (its convs are cuDNN fp32). */
+ * accumulation (fp32-accurate), 5 = each operand tensor scaled by a power of two
+ * (its absolute maximum brought to [2^14, 2^15)) and split into two fp16 terms, three products
+ * per slice on v_mfma_f32_32x32x16_f16 with fp32 accumulation, the result unscaled exactly
+ * (fp32-accurate: the 3xTF32 scheme at fp16's 11-bit significand; the default).  Returns MSL_ERR_ARG for
+ * any other value.  Packs are form-specific (form 5 writes fp16 planes and the weights' scale):
+ * repack after changing the form.  Replaces nothing in the reference (its convs are cuDNN fp32). */
 int msl_conv_set_f32_form(int form);
 int msl_conv_f32_form(void);
 /* Weight-pack kernel (process-wide; identical packed bytes either way): 1 = one LDS-transposing
@@ -80,7 +84,8 @@ int msl_conv_set_sk_hybrid(int on);
 
 /* Elements (fp32 units) of the packed operand produced by msl_dconv_pack (for_dgrad = 0:
  * forward layout, 1: transposed + tap-flipped layout for the data gradient): the fp32 K-major
- * pack followed by its bf16x6 planes (split once here, read by the bf16x6 fp32 form).  All
+ * pack followed by its bf16x6 planes (split once here, read by the bf16x6 fp32 form; with form 5,
+ * the fp16 planes and a tail holding the weights' scale).  All
  * nbranch branches are packed by one call (branch b's weights at w + b*branch_stride floats). */
 long long msl_dconv_packed_elems(int nbranch, int cin, int cout, int for_dgrad);
 /* One weight pack of a batch: exactly what msl_dconv_pack (taps 9) / msl_pconv_pack (taps 1,
@@ -154,6 +159,40 @@ int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, i
 size_t msl_pconv_wgrad_workspace(int cin, int cout, int p);
 int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,
                     int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Operand scales of the f16x3 form (msl_conv_set_f32_form(5)).  Each GEMM operand tensor is
+ * scaled by a power of two derived from its absolute maximum, which msl_absmax_partials reduces
+ * into msl_absmax_parts() floats.  The plain fp32 entry points compute the partials of their
+ * image / gradient operands themselves, once per call; the _sc variants below take them from the
+ * caller instead as (pointer, count) - msl_absmax_partials' msl_absmax_parts() floats, or the c
+ * per-channel maxima msl_bn_fwd_am / msl_bn_bwd_am wrote for the tensor (NULL = compute) - so a
+ * tensor read by two GEMMs (x by the forward and the weight gradient, dy by the data and the
+ * weight gradient) is reduced once, or not at all when a BN kernel produced it.  Partials must
+ * describe exactly the tensor passed (same contents); a non-NULL pointer needs count >= 1.  The
+ * other forms ignore them.
+ * ---------------------------------------------------------------------- */
+int msl_absmax_parts(void);
+int msl_absmax_partials(const float* x, long long n, float* part, msl_stream_t stream);
+int msl_dconv_fwd_sc(const float* x, const float* packed, const float* bias, float* y, int nbranch,
+                     int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                     size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart);
+int msl_dconv_dgrad_sc(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
+                       int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                       size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart);
+int msl_dconv_wgrad_sc(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
+                       int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                       size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
+                       const float* dy_part, int dy_npart);
+int msl_pconv_fwd_sc(const float* x, const float* packed, float* y, int cin, int cout, int p,
+                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                     int x_npart);
+int msl_pconv_dgrad_acc_sc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                           int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                           const float* dy_part, int dy_npart);
+int msl_pconv_wgrad_sc(const float* x, const float* dy, float* dw, int cin, int cout, int p,
+                       int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                       int x_npart, const float* dy_part, int dy_npart);
 
 /* ------------------------------------------------------------------------
  * BF16-MFMA forms of the six conv calls above (BASELINE config 5, "fp16/bf16 MFMA
@@ -280,6 +319,20 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
                float* dgamma, float* dbeta, int c, int p, int training, int relu,
                int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream);
+/* msl_bn_fwd / msl_bn_bwd that also write absmax[c] = max |y[c][.]| (forward) or max |dx[c][.]|
+ * (backward; dx required): the per-channel absmax partials (c of them) that the f16x3 conv
+ * entry points (_sc) take for the tensor this BN produced - the next conv's input, or the
+ * gradient of the conv before it - so those GEMMs need no absmax pass of their own.  The fused
+ * kernels reduce it in registers; the split forms add one pass over the output. */
+int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const float* residual,
+                  float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
+                  float* save_mean, float* save_invstd, int c, int p, int training,
+                  int update_running, float momentum, float eps, int relu, void* ws,
+                  size_t ws_bytes, msl_stream_t stream, float* absmax);
+int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* gamma,
+                  const float* save_mean, const float* save_invstd, float* dx, float* dres,
+                  float* dgamma, float* dbeta, int c, int p, int training, int relu,
+                  int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx);
 /* BN kernel form (process-wide): 1 = train-mode layers with p <= 16384 (or p <= 33792 and
  * c >= 128) run one fused statistics+apply launch per call (one block per channel, operands held in registers), 0 =
  * the split statistics / flat-apply launches everywhere.  Returns 0, or MSL_ERR_ARG. */

@@ -100,6 +100,7 @@ struct BnArgs {
   const double* part;
   int C, P, S, chunk, relu, training, update_running;
   float eps, momentum;
+  float* absmax;  // [C] max |y| per channel (msl_bn_fwd_am: the next conv's f16x3 partials) or null
 };
 
 // Flat apply: block b covers elements [b*chunk, (b+1)*chunk) of the [C][P] tensor (possibly
@@ -190,6 +191,7 @@ struct BnBwdArgs {
   float* dbeta;
   double* part;
   int C, P, S, chunk, relu, training, accumulate;
+  float* absmax;  // [C] max |dx| per channel (msl_bn_bwd_am) or null
 };
 
 template <bool VEC>
@@ -294,6 +296,53 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
 // of 3 (4) and one launch instead of two.  Backward: dy, x, y read once, dx (+ dres) written —
 // 4 (5) passes instead of 7 (8).  Same per-element formulas as the flat kernels above.
 constexpr int kBnFusedThreads = 1024;
+
+// max over the block (kBnFusedThreads threads) of m, valid in thread 0
+__device__ __forceinline__ float block_max16(float m, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int i = 1; i < kBnFusedThreads / 64; ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+
+// absmax[c] = max |t[c][p]| over the channel (the split BN forms' absmax output; absmax zeroed
+// beforehand): block (c, s) reduces 4096 elements of channel c (16 per thread, all loads in
+// flight) and folds them in with an integer atomicMax on the float bits (|t| >= 0 orders as its
+// bits).  One block per channel took 31 us for a 64-channel 33k-px map: 64 blocks.
+constexpr int kAbsChunk = 4096;
+__global__ void __launch_bounds__(256) k_absmax_rows(const float* __restrict__ t, int P, float* __restrict__ absmax) {
+  __shared__ float red[4];
+  const float* row = t + (long long)blockIdx.x * P;
+  const int beg = blockIdx.y * kAbsChunk;
+  float v[kAbsChunk / 256];
+#pragma unroll
+  for (int i = 0; i < kAbsChunk / 256; ++i) {
+    const int e = beg + i * 256 + threadIdx.x;
+    v[i] = e < P ? fabsf(row[e]) : 0.f;
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < kAbsChunk / 256; ++i) m = fmaxf(m, v[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned*>(absmax) + blockIdx.x,
+              __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+static int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
+  const hipError_t e = hipMemsetAsync(absmax, 0, (size_t)c * sizeof(float), st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_absmax_rows, dim3(c, cdiv(p, kAbsChunk)), dim3(256), 0, st, t, p, absmax);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
 constexpr int kBnFusedMaxP = 33 * kBnFusedThreads;  // layer1 at 1024x512: 257x129 = 33153 px
 static int g_bn_fused = 1;  // msl_bn_set_fused
 static bool bn_fused_enabled() { return g_bn_fused != 0; }
@@ -369,14 +418,22 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
   const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
   const float bsh = (a.beta ? a.beta[c] : 0.f) - mean * alpha;
   float* yc = a.y + base;
+  float am = 0.f;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
     if (e < P) {
       float v = xv[j] * alpha + bsh;
       v += rv[j];
-      yc[e] = a.relu ? fmaxf(v, 0.f) : v;
+      v = a.relu ? fmaxf(v, 0.f) : v;
+      yc[e] = v;
+      am = fmaxf(am, fabsf(v));
     }
+  }
+  if (a.absmax) {
+    __shared__ float redm[kBnFusedThreads / 64];
+    am = block_max16(am, redm);
+    if (t == 0) a.absmax[c] = am;
   }
 }
 
@@ -414,14 +471,22 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
   }
   const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
   const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
+  float am = 0.f;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
     if (e < P) {
       const float xh = (xv[j] - mean) * invstd;
       if (a.dres) a.dres[base + e] = g[j];
-      if (a.dx) a.dx[base + e] = (g[j] - m1 - xh * m2) * w;
+      const float d = (g[j] - m1 - xh * m2) * w;
+      if (a.dx) a.dx[base + e] = d;
+      am = fmaxf(am, fabsf(d));
     }
+  }
+  if (a.absmax) {
+    __shared__ float redm[kBnFusedThreads / 64];
+    am = block_max16(am, redm);
+    if (t == 0) a.absmax[c] = am;
   }
 }
 
@@ -458,6 +523,16 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
                float* save_mean, float* save_invstd, int c, int p, int training,
                int update_running, float momentum, float eps, int relu, void* ws,
                size_t ws_bytes, msl_stream_t stream) {
+  return msl_bn_fwd_am(x, gamma, beta, residual, y, running_mean, running_var, num_batches_tracked, save_mean,
+                       save_invstd, c, p, training, update_running, momentum, eps, relu, ws, ws_bytes, stream,
+                       nullptr);
+}
+
+int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const float* residual,
+                  float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
+                  float* save_mean, float* save_invstd, int c, int p, int training,
+                  int update_running, float momentum, float eps, int relu, void* ws,
+                  size_t ws_bytes, msl_stream_t stream, float* absmax) {
   if (!x || !y || !save_mean || !save_invstd || c < 1 || p < 1) return MSL_ERR_ARG;
   if ((!training || update_running) && (!running_mean || !running_var)) return MSL_ERR_ARG;
   hipStream_t st = as_stream(stream);
@@ -494,6 +569,7 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   a.update_running = update_running;
   a.eps = eps;
   a.momentum = momentum;
+  a.absmax = absmax;
   if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>, c, p, st, a);
   const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
   if (vec)
@@ -501,6 +577,7 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
   else
     hipLaunchKernelGGL(k_bn_apply<false>, dim3(blocks), dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
+  if (absmax) return absmax_rows(y, c, p, absmax, st);  // the split forms: a pass of its own over y
   return MSL_OK;
 }
 
@@ -508,7 +585,16 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
                float* dgamma, float* dbeta, int c, int p, int training, int relu,
                int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  return msl_bn_bwd_am(dy, x, y, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, training, relu,
+                       accumulate_params, ws, ws_bytes, stream, nullptr);
+}
+
+int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* gamma,
+                  const float* save_mean, const float* save_invstd, float* dx, float* dres,
+                  float* dgamma, float* dbeta, int c, int p, int training, int relu,
+                  int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
   if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || (relu && !y)) return MSL_ERR_ARG;
+  if (absmax_dx && !dx) return MSL_ERR_ARG;
   if (ws_bytes < msl_bn_workspace(c, p)) return MSL_ERR_WORKSPACE;
   hipStream_t st = as_stream(stream);
   const int S = bn_splits(p);
@@ -531,6 +617,7 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
   a.relu = relu;
   a.training = training;
   a.accumulate = accumulate_params;
+  a.absmax = absmax_dx;
   if (training && bn_fused_enabled() && bn_fused_shape(c, p))
     return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
@@ -545,6 +632,7 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
     hipLaunchKernelGGL(k_bn_bwd_apply<false>, dim3(blocks), dim3(256), 0, st, a);
   }
   MSL_CHECK_LAUNCH();
+  if (absmax_dx) return absmax_rows(dx, c, p, absmax_dx, st);  // the split forms: a pass over dx
   return MSL_OK;
 }
 

@@ -107,7 +107,8 @@ template <int TAPS>
 __device__ __forceinline__ void pack_split_block(const float* __restrict__ w, long long branch_stride, int cin,
                                                  int cout, int for_dgrad, int ncb, int lda, int split,
                                                  float* __restrict__ out, __bf16* __restrict__ planes, int mx,
-                                                 int cb, int b, float (*s)[kPackTileM + 1]) {
+                                                 int cb, int b, float (*s)[kPackTileM + 1],
+                                                 float* __restrict__ tail = nullptr) {
   const int m0 = mx * kPackTileM;
   const int cimg = for_dgrad ? cout : cin;
   const int mreal = for_dgrad ? cin : cout;
@@ -138,6 +139,26 @@ __device__ __forceinline__ void pack_split_block(const float* __restrict__ w, lo
     out[k * lda + m0 + ml] = s[cl * TAPS + t][ml];
   }
   if (!split) return;
+  if (tail) {  // f16x3: two fp16 planes of W * sA, sA from the weights' absmax partials (tail[0..])
+    float inv;
+    const float sc = pow2_scale(partials_max(tail, kNPart, threadIdx.x & 63), inv);
+    if (mx == 0 && cb == 0 && b == 0 && threadIdx.x == 0) {
+      tail[kNPart] = sc;
+      tail[kNPart + 1] = inv;
+    }
+    f16x8* pl = reinterpret_cast<f16x8*>(planes);
+    for (int i = threadIdx.x; i < TAPS * 2 * kPackTileM; i += 256) {
+      const int ml = i % kPackTileM, h = (i / kPackTileM) & 1, t = i / (2 * kPackTileM);
+      const long long ks = (long long)(b * TAPS + t) * ncb + cb;
+      Split2h sp;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) split2h_set(sp, j, s[(8 * h + j) * TAPS + t][ml] * sc);
+      const long long row = ((ks * 2) * 2 + h) * lda + m0 + ml;  // plane 0
+      pl[row] = sp.hi;
+      pl[row + 2LL * lda] = sp.lo;
+    }
+    return;
+  }
   bf16x8* pl = reinterpret_cast<bf16x8*>(planes);
   for (int i = threadIdx.x; i < TAPS * 2 * kPackTileM; i += 256) {  // i = (t*2 + h)*16 + ml
     const int ml = i % kPackTileM, h = (i / kPackTileM) & 1, t = i / (2 * kPackTileM);
@@ -156,17 +177,34 @@ template <int TAPS>
 __global__ void __launch_bounds__(256) k_pack_split(const float* __restrict__ w, long long branch_stride,
                                                     int cin, int cout, int for_dgrad, int ncb, int lda,
                                                     int split, float* __restrict__ out,
-                                                    __bf16* __restrict__ planes) {
+                                                    __bf16* __restrict__ planes, float* __restrict__ tail) {
   __shared__ float s[kCB * TAPS][kPackTileM + 1];  // [cl*TAPS + t][ml], t = packed tap index
   pack_split_block<TAPS>(w, branch_stride, cin, cout, for_dgrad, ncb, lda, split, out, planes, blockIdx.x,
-                         blockIdx.y, blockIdx.z, s);
+                         blockIdx.y, blockIdx.z, s, tail);
+}
+
+// Packed-buffer tail (after the fp32 pack and its planes): the f16x3 form's kNPart absmax
+// partials of the weights, then {sA, 1/sA}.
+constexpr long long kPackTail = 320;
+__host__ __device__ inline long long pack_tail_offset(long long f32_elems) { return f32_elems * 5 / 2; }
+
+// f16x3 weight absmax of every job (grid = (kNPart, njobs)) into each job's pack tail
+template <int TAPS>
+__global__ void __launch_bounds__(256) k_absmax_jobs(const msl_pack_job* __restrict__ jobs) {
+  const msl_pack_job jb = jobs[blockIdx.y];
+  const int cimg = jb.for_dgrad ? jb.cout : jb.cin;
+  const int m = jb.for_dgrad ? jb.cin : jb.cout;
+  if (m <= 64) return;  // no planes to split (as msl_*_pack: the tail stays untouched)
+  const long long f32 = (long long)jb.nbranch * ((cimg + kCB - 1) / kCB) * TAPS * kCB * ((m + kPackPad - 1) / kPackPad * kPackPad);
+  absmax_block(jb.w, (long long)jb.cout * jb.cin * TAPS, jb.branch_stride, jb.nbranch, blockIdx.x,
+               jb.packed + pack_tail_offset(f32) + blockIdx.x);
 }
 
 // Every weight pack of a step in one launch (per tap count): block b runs block b - start[j] of
 // job j (start[] ascending, start[njobs] = the total), each job exactly as msl_*_pack would.
 template <int TAPS>
 __global__ void __launch_bounds__(256) k_pack_split_many(const msl_pack_job* __restrict__ jobs,
-                                                         const long long* __restrict__ start, int njobs) {
+                                                         const long long* __restrict__ start, int njobs, int h3) {
   __shared__ float s[kCB * TAPS][kPackTileM + 1];
   const long long b = blockIdx.x;
   int lo = 0, hi = njobs - 1;  // the last job with start <= b
@@ -187,7 +225,8 @@ __global__ void __launch_bounds__(256) k_pack_split_many(const msl_pack_job* __r
   const int cb = (int)(rest % ncb), br = (int)(rest / ncb);
   const long long f32 = (long long)jb.nbranch * ncb * TAPS * kCB * lda;
   pack_split_block<TAPS>(jb.w, jb.branch_stride, jb.cin, jb.cout, jb.for_dgrad, ncb, lda, m > 64, jb.packed,
-                         reinterpret_cast<__bf16*>(jb.packed + f32), mx, cb, br, s);
+                         reinterpret_cast<__bf16*>(jb.packed + f32), mx, cb, br, s,
+                         h3 ? jb.packed + pack_tail_offset(f32) : nullptr);
 }
 
 // ---------------------------------------------------------------- planning
@@ -199,6 +238,12 @@ constexpr int kSkBN = 128, kSkNW = 512;
 // Forward-form schedule (msl_conv_set_sk_hybrid): 1 = data-parallel rounds + stream-K remainder
 // when the tiles outnumber the workers (SkArgs), 0 = pure stream-K.  Process-wide.
 static int g_sk_hybrid = 1;
+// Matrix-core form of the fp32 entry points (msl_conv_set_f32_form): kMathF32 runs
+// v_mfma_f32_32x32x2_f32 (an exact fmaf chain), kMathX6 the three-way bf16 split on the BF16
+// matrix cores (fp32-accurate, dconv_kernels.h; layer3 fwd 78 vs 102 us in the step, err vs fp64
+// 4e-8 vs 6e-8 relative to sum|terms|), kMathH3P the scaled two-way fp16 split (three fp16
+// MFMAs per slice; dconv_kernels.h Split2h).  Process-wide; packs are form-specific.
+static int g_f32_form = kMathH3P;
 constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
 
 struct FwdPlan {
@@ -334,32 +379,46 @@ static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)
 
 // stream-K workspace: the published pieces, NW x 2 x BM*BN floats (summed by k_sk_reduce; no
 // counters, flags or other state survive a call).
+// + (f16x3) the image's kNPart absmax partials at the end of the caller's workspace.
+constexpr size_t kPartBytes = kNPart * sizeof(float);
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
-  if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float);
-  return pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0;
+  if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float) + kPartBytes;
+  return (pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0) + kPartBytes;
+}
+static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials block from the end
+  return reinterpret_cast<float*>((char*)ws + ((ws_bytes - (size_t)k * kPartBytes) & ~(size_t)15));
 }
 
 // The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
 template <int BM, int G, int ST, int WM, int WN, int MT>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
-  if (accum)
-    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
-  else
-    hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, false>), grid, block, 0, st, a, sk);
+  if constexpr (MT == kMathH3P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
+    if (accum)
+      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
+    else
+      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, false, MT, false>), grid, block, 0, st, a, sk);
+  } else {
+    if (accum)
+      hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
+    else
+      hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, false>), grid, block, 0, st, a, sk);
+  }
 }
 
 template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int dil0,
                            int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st,
-                           int accum = 0) {
+                           int accum = 0, const float* img_part = nullptr, int img_npart = 0) {
   const int P = h * w;
   FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
   // The x6 form runs one K-step per stage, three stages deep (scripts/tune_dconv.hip x6, layer3:
   // 87 us vs 115 with two K-steps per stage; f32 is indifferent); its 64- and 32-row tiles stay
   // on exact f32 MFMA (no gain measured there).
-  constexpr int MS = MT == kMathX6 ? kMathF32 : MT;
-  if (MT == kMathX6 && pl.sk && pl.bm == 128) {
+  constexpr bool X6L = MT == kMathX6 || MT == kMathH3P;  // split forms: 128-row tiles only
+  constexpr int MS = X6L ? kMathF32 : MT;
+  constexpr int MB = MT == kMathH3P ? kMathX6 : MT;       // (not reached by the split forms)
+  if (X6L && pl.sk && pl.bm == 128) {
     pl.G = 1;
     pl.bk = kCB;
     pl.kps = pl.ksteps;
@@ -367,6 +426,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   if (ws_bytes < fwd_ws_bytes(pl, M, P)) return MSL_ERR_WORKSPACE;
   FwdArgs a{};
   a.Ax6 = nullptr;
+  a.ascale = nullptr;
+  a.bpart = nullptr;
+  a.bnpart = 0;
   a.accum = accum;
   a.A = packed;
   a.B = img;
@@ -411,18 +473,35 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
     const dim3 rgrid(pl.bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp));
     const bool reduce = T > 0;
-    if (MT == kMathX6 && pl.bm == 128) {
+    if (X6L && pl.bm == 128) {
       // the x6 kernel stages its weights from the bf16 planes that pack() split once, behind
       // the fp32 part of the same buffer (M > 64 <=> 128-row tiles)
-      a.Ax6 = reinterpret_cast<const __bf16*>(packed + (long long)pl.ksteps * kCB * a.lda);
-      launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
+      const long long f32 = (long long)pl.ksteps * kCB * a.lda;
+      a.Ax6 = reinterpret_cast<const __bf16*>(packed + f32);
+      if constexpr (MT == kMathH3P) {
+        // f16x3: the image's absmax partials, then the GEMM with the pack's {sA, 1/sA}
+        if (img_part) {  // the caller's partials of this image (msl_absmax_partials, a BN kernel)
+          a.bpart = img_part;
+          a.bnpart = img_npart;
+        } else {
+          float* part = ws_partials(ws, ws_bytes, 1);
+          hipLaunchKernelGGL(k_absmax, dim3(kNPart), block, 0, st, img, (long long)cimg * P, 0LL, 1, part);
+          MSL_CHECK_LAUNCH();
+          a.bpart = part;
+          a.bnpart = kNPart;
+        }
+        a.ascale = packed + pack_tail_offset(f32) + kNPart;
+        launch_sk<128, 1, 4, 2, 2, kMathH3P>(accum, grid, block, st, a, sk);
+      } else {
+        launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
+      }
       MSL_CHECK_LAUNCH();
       if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 128) {
       if (pl.G == 2)
-        launch_sk<128, 2, 2, 2, 2, MT>(accum, grid, block, st, a, sk);
+        launch_sk<128, 2, 2, 2, 2, MB>(accum, grid, block, st, a, sk);
       else
-        launch_sk<128, 1, 3, 2, 2, MT>(accum, grid, block, st, a, sk);
+        launch_sk<128, 1, 3, 2, 2, MB>(accum, grid, block, st, a, sk);
       MSL_CHECK_LAUNCH();
       if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
@@ -472,7 +551,7 @@ static long long packed_f32_elems(int nbranch, int taps, int cin, int cout, int 
 }
 
 static long long packed_elems(int nbranch, int taps, int cin, int cout, int for_dgrad) {
-  return packed_f32_elems(nbranch, taps, cin, cout, for_dgrad) * 5 / 2;
+  return pack_tail_offset(packed_f32_elems(nbranch, taps, cin, cout, for_dgrad)) + kPackTail;
 }
 
 static int g_pack_form = 1;  // msl_conv_set_pack_form: 1 = k_pack_split, 0 = k_pack + k_split_pack
@@ -485,9 +564,11 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
   const int lda = pad_to(m, kPackPad);
   const int ncb = cdiv(cimg, kCB);
   __bf16* planes = reinterpret_cast<__bf16*>(packed + total);
+  const bool h3 = g_f32_form == kMathH3P && m > 64;
+  float* tail = h3 ? packed + pack_tail_offset(total) : nullptr;
   // M <= 64 has no planes to split, and its 128-row padding is mostly zeros, which k_pack's
   // fully coalesced rows write faster (ASPP fwd 2048 -> 19: 5.2 vs 9.5 us)
-  if (g_pack_form == 0 || m <= 64) {  // element-wise gather, then a separate split
+  if ((g_pack_form == 0 && !h3) || m <= 64) {  // element-wise gather, then a separate split
     const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
     hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
                        ncb, lda, taps, total, packed);
@@ -504,14 +585,18 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
   static_assert(kPackPad % kPackTileM == 0, "pack tiles must cover lda");
   const dim3 grid(lda / kPackTileM, ncb, nbranch);
   const int split = m > 64;
+  if (taps != 9 && taps != 1) return MSL_ERR_ARG;
+  if (h3) {
+    hipLaunchKernelGGL(k_absmax, dim3(kNPart), dim3(256), 0, st, w, (long long)cout * cin * taps, branch_stride,
+                       nbranch, tail);
+    MSL_CHECK_LAUNCH();
+  }
   if (taps == 9)
     hipLaunchKernelGGL(k_pack_split<9>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
-                       lda, split, packed, planes);
-  else if (taps == 1)
-    hipLaunchKernelGGL(k_pack_split<1>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
-                       lda, split, packed, planes);
+                       lda, split, packed, planes, tail);
   else
-    return MSL_ERR_ARG;
+    hipLaunchKernelGGL(k_pack_split<1>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
+                       lda, split, packed, planes, tail);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
@@ -531,24 +616,30 @@ static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P, in
                         : plan_wgrad(nbranch, taps, cin, cout, P, x6 != 0, w);
       b = std::max(b, wgrad_piece_bytes(pl) + wgrad_planes_bytes(pl));
     }
-  return b;
+  return b + 2 * kPartBytes + 16;  // + (f16x3) both operands' absmax partials
 }
 
 template <int MT>
 static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
                         int taps, int cin, int cout, int h, int w, int dil0, int dil1,
-                        int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
+                        int accumulate, void* ws, size_t ws_bytes, hipStream_t st,
+                        const float* x_part = nullptr, int x_npart = 0, const float* dy_part = nullptr,
+                        int dy_npart = 0) {
   const int P = h * w;
-  constexpr int MS = MT == kMathX6 ? kMathF32 : MT;  // x6 only on 128x128 tiles (plan_wgrad)
+  constexpr bool X6L = MT == kMathX6 || MT == kMathH3P;
+  constexpr int MS = X6L ? kMathF32 : MT;  // the split forms only on 128x128 tiles (plan_wgrad)
+  constexpr int MB = MT == kMathH3P ? kMathX6 : MT;  // k_wgrad_sk has no f16x3 form: x6 there
   if (ws_bytes < wgrad_ws_bytes(nbranch, taps, cin, cout, P, w)) return MSL_ERR_WORKSPACE;
-  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, MT == kMathX6, w);
+  WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, X6L, w);
   bool trans = false;
-  if (MT == kMathX6 && wgrad_swaps(nbranch, taps, cin, cout) && !dbias) {
+  if (X6L && wgrad_swaps(nbranch, taps, cin, cout) && !dbias) {
     WgradPlan ps = plan_wgrad(nbranch, taps, cout, cin, P, true, w);
     if (ps.rx6) {  // dW^T = image . dY^T: M = cin (pre-split), N = cout
       pl = ps;
       trans = true;
       std::swap(x, dy);
+      std::swap(x_part, dy_part);
+      std::swap(x_npart, dy_npart);
       std::swap(cin, cout);
     }
   }
@@ -583,19 +674,50 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   a.kchunk = pl.kchunk;
   a.ntiles = pl.tiles_m * pl.tiles_n * pl.ntap;
   a.trans = trans ? 1 : 0;
+  a.apart = nullptr;
+  a.bpart = nullptr;
+  a.anpart = a.bnpart = 0;
   const dim3 grid(pl.nw), block(256);
   const dim3 rgrid(cdiv((long long)pl.bm * pl.bn / 4 * taps, 256), pl.tiles_m * pl.tiles_n * nbranch), rblock(256);
   if (pl.rx6) {
     bf16x8* planes = reinterpret_cast<bf16x8*>((char*)ws + wgrad_piece_bytes(pl));
     a.dyx6 = planes;
-    hipLaunchKernelGGL(k_split_rows, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P, pl.KS,
-                       pl.lda, planes);
-    MSL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_wgrad_x6, grid, block, 0, st, a);
+    if constexpr (MT == kMathH3P) {  // both operands' absmax partials, then the scaled split
+      const float* ap = dy_part;
+      const float* bp = x_part;
+      int an = dy_npart, bn = x_npart;
+      if (!ap) {
+        float* w2 = ws_partials(ws, ws_bytes, 2);
+        hipLaunchKernelGGL(k_absmax, dim3(kNPart), block, 0, st, dy, (long long)cout * P, 0LL, 1, w2);
+        MSL_CHECK_LAUNCH();
+        ap = w2;
+        an = kNPart;
+      }
+      if (!bp) {
+        float* w1 = ws_partials(ws, ws_bytes, 1);
+        hipLaunchKernelGGL(k_absmax, dim3(kNPart), block, 0, st, x, (long long)cin * P, 0LL, 1, w1);
+        MSL_CHECK_LAUNCH();
+        bp = w1;
+        bn = kNPart;
+      }
+      a.apart = ap;
+      a.bpart = bp;
+      a.anpart = an;
+      a.bnpart = bn;
+      hipLaunchKernelGGL(k_split_rows<kMathH3P>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
+                         pl.KS, pl.lda, planes, ap, an);
+      MSL_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_wgrad_x6<kMathH3P>, grid, block, 0, st, a);
+    } else {
+      hipLaunchKernelGGL(k_split_rows<kMathX6>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
+                         pl.KS, pl.lda, planes, (const float*)nullptr, 0);
+      MSL_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_wgrad_x6<kMathX6>, grid, block, 0, st, a);
+    }
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
   } else if (pl.bm == 128) {
-    hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2, MT>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2, MB>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
   } else if (pl.bm == 64) {
@@ -616,19 +738,15 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   return MSL_OK;
 }
 
-// Matrix-core form of the fp32 entry points (msl_conv_set_f32_form): kMathF32 runs
-// v_mfma_f32_32x32x2_f32 (an exact fmaf chain), kMathX6 the three-way bf16 split on the BF16
-// matrix cores (fp32-accurate, dconv_kernels.h; the default: layer3 fwd 78 vs 102 us in the
-// step, err vs fp64 4e-8 vs 6e-8 relative to sum|terms|).  Process-wide.
-static int g_f32_form = kMathX6;
-
 template <typename... Args>
 static int fwd_f32(Args... args) {
+  if (g_f32_form == kMathH3P) return launch_fwd_form<kMathH3P>(args...);
   return g_f32_form == kMathX6 ? launch_fwd_form<kMathX6>(args...) : launch_fwd_form<kMathF32>(args...);
 }
 
 template <typename... Args>
 static int wgrad_f32(Args... args) {
+  if (g_f32_form == kMathH3P) return launch_wgrad<kMathH3P>(args...);
   return g_f32_form == kMathX6 ? launch_wgrad<kMathX6>(args...) : launch_wgrad<kMathF32>(args...);
 }
 
@@ -643,7 +761,7 @@ int msl_abi_version(void) { return MSL_ABI_VERSION; }
 int msl_counter_elems(void) { return kMaxCounters; }
 
 int msl_conv_set_f32_form(int form) {
-  if (form != kMathF32 && form != kMathX6) return MSL_ERR_ARG;
+  if (form != kMathF32 && form != kMathX6 && form != kMathH3P) return MSL_ERR_ARG;
   g_f32_form = form;
   return MSL_OK;
 }
@@ -696,10 +814,20 @@ int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, i
       (taps != 1 && taps != 9))
     return MSL_ERR_ARG;
   hipStream_t st = as_stream(stream);
+  const int h3 = g_f32_form == kMathH3P;
+  if (h3) {  // the weights' absmax partials first (jobs with M > 64: the split packs)
+    if (taps == 9)
+      hipLaunchKernelGGL(k_absmax_jobs<9>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
+    else
+      hipLaunchKernelGGL(k_absmax_jobs<1>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
+    MSL_CHECK_LAUNCH();
+  }
   if (taps == 9)
-    hipLaunchKernelGGL(k_pack_split_many<9>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs);
+    hipLaunchKernelGGL(k_pack_split_many<9>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs,
+                       h3);
   else
-    hipLaunchKernelGGL(k_pack_split_many<1>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs);
+    hipLaunchKernelGGL(k_pack_split_many<1>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs,
+                       h3);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
@@ -795,6 +923,78 @@ int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, i
                    as_stream(stream));
   return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
                  as_stream(stream), 1);
+}
+
+int msl_absmax_parts(void) { return kNPart; }
+
+static bool bad_parts(const float* p, int n) { return p && n < 1; }
+
+int msl_absmax_partials(const float* x, long long n, float* part, msl_stream_t stream) {
+  if (!x || !part || n < 0) return MSL_ERR_ARG;
+  hipLaunchKernelGGL(k_absmax, dim3(kNPart), dim3(256), 0, as_stream(stream), x, n, 0LL, 1, part);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+int msl_dconv_fwd_sc(const float* x, const float* packed, const float* bias, float* y, int nbranch,
+                     int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                     size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart) {
+  if (bad_parts(x_part, x_npart)) return MSL_ERR_ARG;
+  if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return fwd_f32(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1, counters, ws, ws_bytes,
+                 as_stream(stream), 0, x_part, x_npart);
+}
+
+int msl_dconv_dgrad_sc(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
+                       int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                       size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart) {
+  if (bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
+  if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1, counters, ws,
+                 ws_bytes, as_stream(stream), 0, dy_part, dy_npart);
+}
+
+int msl_dconv_wgrad_sc(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
+                       int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                       size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
+                       const float* dy_part, int dy_npart) {
+  if (bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
+  if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
+      (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return wgrad_f32(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws, ws_bytes,
+                   as_stream(stream), x_part, x_npart, dy_part, dy_npart);
+}
+
+int msl_pconv_fwd_sc(const float* x, const float* packed, float* y, int cin, int cout, int p,
+                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                     int x_npart) {
+  if (bad_parts(x_part, x_npart)) return MSL_ERR_ARG;
+  if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
+  return fwd_f32(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+                 as_stream(stream), 0, x_part, x_npart);
+}
+
+int msl_pconv_dgrad_acc_sc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                           int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                           const float* dy_part, int dy_npart) {
+  if (bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
+  if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+                 as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart);
+}
+
+int msl_pconv_wgrad_sc(const float* x, const float* dy, float* dw, int cin, int cout, int p,
+                       int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                       int x_npart, const float* dy_part, int dy_npart) {
+  if (bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
+  if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
+  return wgrad_f32(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes, as_stream(stream),
+                   x_part, x_npart, dy_part, dy_npart);
 }
 
 size_t msl_pconv_wgrad_workspace(int cin, int cout, int p) {

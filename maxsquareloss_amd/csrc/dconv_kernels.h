@@ -24,6 +24,11 @@ struct FwdArgs {
   const void* Ax6;    // kMathX6P/PP: A split into bf16 planes [ks][plane][k half][lda][8] (k_split_pack)
   const void* Bx6;    // kMathX6PP: B split into bf16 planes [cb][plane][k half][P][8] (k_split_act)
   int accum;          // stream-K forms: C = C_old + result (the fused residual-gradient sum)
+  // kMathH3P: Ax6 holds A * sA as two fp16 planes [ks][plane][k half][lda][8]; ascale = {sA,
+  // 1/sA} (written by the pack); bpart = the kNPart absmax partials of B (k_absmax)
+  const float* ascale;
+  const float* bpart;
+  int bnpart;  // partials in bpart
 };
 
 struct WgradArgs {
@@ -164,6 +169,104 @@ __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.hi, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.mid, c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, c, 0, 0, 0);
+}
+
+// FP32 GEMM on the FP16 matrix cores ("f16x3", kMathH3P, r02): each operand tensor is scaled by
+// a power of two s (its absolute maximum brought to [2^14, 2^15): k_absmax partials, pow2_scale)
+// and split into two fp16 terms, v*s = hi + lo + e (RNE; the remainder v*s - hi is exact in fp32,
+// |lo| <= 2^-11 |v*s|, |e| <= 2^-22 |v*s|).  The three products lo*hi, hi*lo, hi*hi go through
+// v_mfma_f32_32x32x16_f16 (an fp16 x fp16 product is exact in fp32, fp32 accumulation); the
+// dropped lo*lo and the residuals are <= 2^-22 of each product, random in sign, so over a K-deep
+// dot product they stay below fp32 accumulation's own rounding (the same argument as 3xTF32:
+// TF32 also carries 11 significant bits).  The result is multiplied by 1/(sA sB), exactly.  The
+// per-tensor scale keeps both terms inside fp16's exponent range (weights ~1e-2 and gradients
+// ~1e-7 would otherwise lose the lo term to subnormals).  Half the MFMAs of x6 per 16-deep slice.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kMathH3P = 5;
+constexpr int kNPart = 256;  // absmax partials per operand tensor (k_absmax blocks)
+
+struct Split2h {
+  f16x8 hi, lo;
+};
+
+__device__ __forceinline__ void split2h_set(Split2h& s, int j, float v) {  // v already scaled
+  const _Float16 h = (_Float16)v;
+  s.hi[j] = h;
+  s.lo[j] = (_Float16)(v - (float)h);
+}
+
+__device__ __forceinline__ f32x16 mfma_h3(const Split2h& a, const Split2h& b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.lo, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.lo, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.hi, c, 0, 0, 0);
+}
+
+// 2^k with k = clamp(141 - biased exponent of mx, -100, 100): mx * 2^k in [2^14, 2^15) (fp16's
+// largest finite value is 65504); a zero / fp32-subnormal maximum gives 2^100, inf / NaN 2^-100.
+// `inv` = 2^-k.  Powers of two: scaling and unscaling are exact.
+__device__ __forceinline__ float pow2_scale(float mx, float& inv) {
+  const int e = (int)((__float_as_uint(mx) >> 23) & 0xffu);
+  const int k = min(100, max(-100, 141 - e));
+  inv = __uint_as_float((unsigned)(127 - k) << 23);
+  return __uint_as_float((unsigned)(127 + k) << 23);
+}
+
+// max over the n absmax partials of one tensor (kNPart from k_absmax, or one per channel from
+// the BN kernels that produced it), by every wave on its own (wave-uniform): float4 loads, four
+// in flight per lane (2048 partials: two rounds)
+__device__ __forceinline__ float partials_max(const float* __restrict__ part, int n, int lane) {
+  float m = 0.f;
+  if ((n & 3) == 0 && ((uintptr_t)part & 15) == 0) {
+    const float4* p4 = reinterpret_cast<const float4*>(part);
+    const int n4 = n >> 2;
+    for (int i = lane; i < n4; i += 256) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i + 64 * u < n4 ? p4[i + 64 * u] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) m = fmaxf(m, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+    }
+  } else {
+    for (int i = lane; i < n; i += 64) m = fmaxf(m, part[i]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(m)));
+}
+
+// Block b of kNPart writes max |x| over its share of nbranch rows of n floats (row r at
+// x + r * stride) to part[b]: coalesced float loads, a block reduce through LDS.
+__device__ __forceinline__ void absmax_block(const float* __restrict__ x, long long n, long long stride,
+                                             int nbranch, int b, float* __restrict__ out) {
+  __shared__ float red[4];
+  constexpr long long NT = (long long)kNPart * 256;  // threads of the grid
+  float m = 0.f;
+  for (int r = 0; r < nbranch; ++r) {
+    const float* row = x + r * stride;
+    // float4 body with eight loads in flight per thread (one load at a time was latency-bound:
+    // ~10 us for an 8.6 MB tensor), then the scalar tail (or all of a misaligned row)
+    const long long n4 = ((uintptr_t)row & 15) == 0 ? n / 4 : 0;
+    const float4* r4 = reinterpret_cast<const float4*>(row);
+    for (long long i = (long long)b * 256 + threadIdx.x; i < n4; i += 8 * NT) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = i + u * NT < n4 ? r4[i + u * NT] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+    }
+    for (long long i = n4 * 4 + (long long)b * 256 + threadIdx.x; i < n; i += NT) m = fmaxf(m, fabsf(row[i]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+__global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, long long n, long long stride,
+                                                int nbranch, float* __restrict__ part) {
+  absmax_block(x, n, stride, nbranch, blockIdx.x, part + blockIdx.x);
 }
 
 // Operand fragment of a bf16 matrix-core form and its MFMA step (32x32x16: 8 k per lane).
@@ -316,6 +419,37 @@ __device__ __forceinline__ void mfma_stage_x6p(const float* __restrict__ As, con
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int t = 0; t < TN; ++t) acc[i][t] = mfma_x6(av[i], bv[t], acc[i][t]);
+    if (kk == 0) mid();
+  }
+}
+
+// f16x3 stage: A fragments from the pre-split fp16 planes (one LDS stage = G K-steps of
+// [plane][half][BM][8] fp16, 16*BM floats each), B fragments scaled by sB and split as they are read.
+template <int G, int TM, int TN, int BM, int LDB_S, typename F>
+__device__ __forceinline__ void mfma_stage_h3p(const float* __restrict__ As, const float* __restrict__ Bs,
+                                               int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid,
+                                               float sB) {
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int kk = 0; kk < G; ++kk) {
+    const f16x8* Ab = reinterpret_cast<const f16x8*>(As + kk * 16 * BM);
+    Split2h av[TM], bv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = wm + i * 32 + l32;
+      av[i].hi = Ab[h * BM + m];
+      av[i].lo = Ab[(2 + h) * BM + m];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kr = kk * 16 + 8 * h + j;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) split2h_set(bv[t], j, Bs[kr * LDB_S + wn + t * 32 + l32] * sB);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) acc[i][t] = mfma_h3(av[i], bv[t], acc[i][t]);
     if (kk == 0) mid();
   }
 }
@@ -720,7 +854,7 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
 }
 
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false>
-__global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
+__device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
   // is 128 contiguous pixels and moves as dwordx4 (4 pixels per lane) instead of dwords.
@@ -728,14 +862,16 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   static_assert(BN % 64 == 0 && BM % 32 == 0, "tiles");
-  constexpr bool APRE = MT == kMathX6P || MT == kMathX6PP;  // A from pre-split bf16 planes
-  constexpr bool BPRE = MT == kMathX6PP;                      // B from pre-split bf16 planes
+  constexpr bool H3 = MT == kMathH3P;                                 // f16x3: two fp16 planes
+  constexpr bool APRE = MT == kMathX6P || MT == kMathX6PP || H3;  // A from pre-split planes
+  constexpr bool BPRE = MT == kMathX6PP;                            // B from pre-split bf16 planes
+  constexpr int NQ = H3 ? 4 : 6;  // (plane, k half) blocks of one pre-split K-step
   static_assert(!APRE || BM % 64 == 0, "pre-split A: 64-row DMA pieces");
   static_assert(!BPRE || (!PW && BN % 64 == 0), "pre-split B: 64-pixel DMA pieces");
-  constexpr int A_STAGE = APRE ? G * 24 * BM : BK * BM;
+  constexpr int A_STAGE = APRE ? G * 4 * NQ * BM : BK * BM;
   constexpr int STAGE = A_STAGE + (BPRE ? G * 24 * BN : BK * BN);
   constexpr int A_ROWS_PER_INST = 256 / BM;
-  constexpr int A_INST = APRE ? G * 6 * (BM / 64) : BK / A_ROWS_PER_INST;
+  constexpr int A_INST = APRE ? G * NQ * (BM / 64) : BK / A_ROWS_PER_INST;
   constexpr int A_INST_W = A_INST / 4;
   constexpr int NH = BN / 64;
 #ifdef MSL_SK_FAKEX4
@@ -771,11 +907,17 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * 6 * a.lda * 16), 0x00020000);
+      (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * NQ * a.lda * 16), 0x00020000);
   const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.Bx6, (short)0, (int)min(0x7fffffffLL, (long long)a.ncb * 6 * a.P * 16), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
   const unsigned chan_bytes = (unsigned)a.P * 4u;
+  // f16x3: B's scale from its absmax partials, A's from the pack; the result is unscaled by both
+  float sB = 1.f, iA = 1.f, iB = 1.f;
+  if constexpr (H3) {
+    sB = pow2_scale(partials_max(a.bpart, a.bnpart, lane), iB);
+    iA = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a.ascale[1])));
+  }
 
   f32x16 acc[TM][TN];
   while (true) {
@@ -846,14 +988,14 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
       if constexpr (APRE) {
-        // piece inst = (g, plane*2 + half, 64-row block): planes row ((ks*3+q)*2+h)*lda + m
+        // piece inst = (g, plane*2 + half, 64-row block): planes row ((ks*NP+q)*2+h)*lda + m
 #pragma unroll
         for (int i = 0; i < A_INST_W; ++i) {
           const int inst = wid * A_INST_W + i;
-          const int g = inst / (6 * (BM / 64)), r = inst % (6 * (BM / 64));
+          const int g = inst / (NQ * (BM / 64)), r = inst % (NQ * (BM / 64));
           const int qh = r / (BM / 64), mb = (r % (BM / 64)) * 64;
           const int ks = s * G + g;
-          dma_b128(rx, As + inst * 256, (unsigned)(((ks * 6 + qh) * a.lda + m0 + mb + lane) * 16));
+          dma_b128(rx, As + inst * 256, (unsigned)(((ks * NQ + qh) * a.lda + m0 + mb + lane) * 16));
         }
       } else {
         const unsigned a_base = (unsigned)s * a_stage_bytes;
@@ -956,11 +1098,21 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
         mfma_stage_x6p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (MT == kMathX6PP)
         mfma_stage_x6pp<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
+      else if constexpr (H3)
+        mfma_stage_h3p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid, sB);
       else
         mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
+    if constexpr (H3) {  // exact: both factors are powers of two
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * iA * iB;
+    }
     constexpr int PSZ = BM * BN;
 #ifdef MSL_SK_NOFIX  // tuning-harness experiment only: every piece stores as if it were the whole tile
     if (false) {
@@ -1031,6 +1183,18 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
         }
       }
   }
+}
+
+template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false>
+__global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
+  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC>(a, sk);
+}
+
+// The same kernel held to two waves per SIMD (<= 256 VGPRs + AGPRs): the f16x3 form, left to the
+// compiler's default budget, takes 199 VGPRs + 64 AGPRs and one wave per SIMD.
+template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false>
+__global__ void __launch_bounds__(256, 2) k_igemm_fwd_sk2(FwdArgs a, SkArgs sk) {
+  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC>(a, sk);
 }
 
 // sum of pieces w_lo..w_hi in that order (deterministic), eight loads in flight per step: a tile
@@ -1391,6 +1555,10 @@ struct WskArgs {
   // rows): dy = the image [cin][P], x = dY [cout][P], M = cin, N = cout, so the tiles hold dW^T
   // and k_wsk_reduce writes them transposed into dw [cout][cin]
   int trans;
+  // k_wgrad_x6<kMathH3P>: the kNPart absmax partials of the pre-split operand (dy) and of x
+  const float* apart;
+  const float* bpart;
+  int anpart, bnpart;  // partials in apart / bpart
 };
 
 constexpr int kWskBK = 64;
@@ -1671,14 +1839,20 @@ constexpr int kWx6BK = 16;
 // every (K-step, plane, half) as 64 consecutive rows of 16-B vectors (ds_read_b128 at a 144-B
 // stride: conflict-free).  The r01 form (32 rows, 8 scalar loads per thread at a 32-B stride
 // across lanes) ran 8.3 us on a 256 x 8385 dY.  grid = (lda / 64, ceil(KS / 4)).
+// MT = kMathH3P: two fp16 planes of src * s, s = pow2_scale of src's absmax partials `part`.
+template <int MT = kMathX6>
 __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ src, int M, int P, int KS, int lda,
-                                                     bf16x8* __restrict__ planes) {
-  constexpr int R = 64, LDP = 72;  // rows per block, LDS row stride in bf16 (64 pixels + 8)
-  __shared__ __attribute__((aligned(16))) __bf16 tile[3 * R * LDP];
+                                                     bf16x8* __restrict__ planes, const float* __restrict__ part,
+                                                     int npart) {
+  constexpr int R = 64, LDP = 72;  // rows per block, LDS row stride in 16-bit terms (64 pixels + 8)
+  constexpr int NP = MT == kMathH3P ? 2 : 3;
+  __shared__ __attribute__((aligned(16))) unsigned short tile[NP * R * LDP];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int m0 = blockIdx.x * R, ks0 = blockIdx.y * 4;
   const int p = ks0 * kWx6BK + lane;
   const bool pin = p < P;
+  float sc = 1.f, inv;
+  if constexpr (MT == kMathH3P) sc = pow2_scale(partials_max(part, npart, lane), inv);
   float v[R / 4];
 #pragma unroll
   for (int i = 0; i < R / 4; ++i) {
@@ -1688,33 +1862,48 @@ __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ sr
 #pragma unroll
   for (int i = 0; i < R / 4; ++i) {
     const int r = wv + 4 * i;
-    const __bf16 h = (__bf16)v[i];
-    const float rem = v[i] - (float)h;
-    const __bf16 md = (__bf16)rem;
-    tile[(0 * R + r) * LDP + lane] = h;
-    tile[(1 * R + r) * LDP + lane] = md;
-    tile[(2 * R + r) * LDP + lane] = (__bf16)(rem - (float)md);
+    if constexpr (MT == kMathH3P) {
+      const float x = v[i] * sc;
+      const _Float16 h = (_Float16)x;
+      const _Float16 l = (_Float16)(x - (float)h);
+      tile[(0 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, h);
+      tile[(1 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, l);
+    } else {
+      const __bf16 h = (__bf16)v[i];
+      const float rem = v[i] - (float)h;
+      const __bf16 md = (__bf16)rem;
+      tile[(0 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, h);
+      tile[(1 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, md);
+      tile[(2 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, (__bf16)(rem - (float)md));
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {  // 4 K-steps x 3 planes x 2 halves x 64 rows = 6 vectors per thread
+  for (int i = 0; i < 2 * NP; ++i) {  // 4 K-steps x NP planes x 2 halves x 64 rows: 2*NP vectors per thread
     const int idx = tid + 256 * i;
-    const int r = idx & 63, u = idx >> 6;  // u = (ksl*3 + q)*2 + h
-    const int h = u & 1, q = (u >> 1) % 3, ksl = u / 6;
+    const int r = idx & 63, u = idx >> 6;  // u = (ksl*NP + q)*2 + h
+    const int h = u & 1, q = (u >> 1) % NP, ksl = u / (2 * NP);
     const int ks = ks0 + ksl;
     if (ks < KS)
-      planes[(long long)((ks * 3 + q) * 2 + h) * lda + m0 + r] =
+      planes[(long long)((ks * NP + q) * 2 + h) * lda + m0 + r] =
           *reinterpret_cast<const bf16x8*>(&tile[(q * R + r) * LDP + ksl * 16 + h * 8]);
   }
 }
 
+// MT = kMathH3P (f16x3): dY (the pre-split operand) as two fp16 planes scaled by k_split_rows<H3>,
+// X scaled by its own pow2_scale (absmax partials bpart) and split into two fp16 planes; the
+// pieces are unscaled by both before they are stored.
+template <int MT = kMathX6>
 __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
+  constexpr bool H3 = MT == kMathH3P;
+  constexpr int NP = H3 ? 2 : 3;      // planes per operand
   constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
   constexpr int RB = 128 * 16 + 32;   // bytes per (plane, k half) block of 128 rows, padded
-  constexpr int KVB = 6 * RB;         // one K-step's B planes
+  constexpr int KVB = 2 * NP * RB;    // one K-step's B planes
   constexpr int STAGEB = 2 * KVB;     // two K-steps
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGEB];  // 48.75 KB: the only LDS object
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGEB];  // 48.75 KB (x6): the only LDS object
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1734,7 +1923,12 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
   }
 
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.dyx6, (short)0, (int)min(0x7fffffffLL, (long long)a.KS * 6 * a.lda * 16), 0x00020000);
+      (void*)a.dyx6, (short)0, (int)min(0x7fffffffLL, (long long)a.KS * 2 * NP * a.lda * 16), 0x00020000);
+  float sX = 1.f, iA = 1.f, iB = 1.f;
+  if constexpr (H3) {
+    sX = pow2_scale(partials_max(a.bpart, a.bnpart, lane), iB);
+    pow2_scale(partials_max(a.apart, a.anpart, lane), iA);
+  }
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.x, (short)0, (int)min(0x7fffffffLL, (long long)a.N * a.P * 4), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
@@ -1804,8 +1998,25 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
         for (int j = 0; j < 4; ++j) rbv[4 * i + j] = (mb >> j) & 1u ? c.f[j] : 0.f;
       }
     };
-    auto storeB = [&](int buf) {  // split once, three 8-B plane quarters per chunk
+    auto storeB = [&](int buf) {  // split once, NP 8-B plane quarters per chunk
       char* base = smem + buf * STAGEB + wofs;
+      if constexpr (H3) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f16x4 hi, lo;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float v = rbv[4 * i + j] * sX;
+            const _Float16 h = (_Float16)v;
+            hi[j] = h;
+            lo[j] = (_Float16)(v - (float)h);
+          }
+          char* dst = base + i * 32 * 16;
+          *reinterpret_cast<f16x4*>(dst) = hi;
+          *reinterpret_cast<f16x4*>(dst + 2 * RB) = lo;
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         bf16x4 hi, mid, lo;
@@ -1826,16 +2037,35 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       }
     };
     const unsigned a_voff = (unsigned)((kh * a.lda + m0 + wm + l32) * 16);
-    u32x4 A0[TM][3], A1[TM][3];
-    auto loadA = [&](u32x4 (&A)[TM][3], int ks) {
+    u32x4 A0[TM][NP], A1[TM][NP];
+    auto loadA = [&](u32x4 (&A)[TM][NP], int ks) {
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii)
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+        for (int q = 0; q < NP; ++q)
           A[ii][q] = __builtin_amdgcn_raw_buffer_load_b128(rA, a_voff + ii * 512,
-                                                           (int)((unsigned)(ks * 6 + 2 * q) * a_plane_bytes), 0);
+                                                           (int)((unsigned)(ks * 2 * NP + 2 * q) * a_plane_bytes), 0);
     };
-    auto compute = [&](const char* Bs, const u32x4 (&A)[TM][3]) {
+    auto compute = [&](const char* Bs, const u32x4 (&A)[TM][NP]) {
+      if constexpr (H3) {
+        Split2h bv[TN];
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) {
+          const char* src = Bs + kh * RB + (wn + jj * 32 + l32) * 16;
+          bv[jj].hi = *reinterpret_cast<const f16x8*>(src);
+          bv[jj].lo = *reinterpret_cast<const f16x8*>(src + 2 * RB);
+        }
+#pragma unroll
+        for (int ii = 0; ii < TM; ++ii) {
+          union { u32x4 u; f16x8 h; } c0, c1;
+          c0.u = A[ii][0]; c1.u = A[ii][1];
+          Split2h av;
+          av.hi = c0.h; av.lo = c1.h;
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj) acc[ii][jj] = mfma_h3(av, bv[jj], acc[ii][jj]);
+        }
+        return;
+      }
       Split3 bv[TN];
 #pragma unroll
       for (int jj = 0; jj < TN; ++jj) {
@@ -1847,7 +2077,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) {
         union { u32x4 u; bf16x8 h; } c0, c1, c2;
-        c0.u = A[ii][0]; c1.u = A[ii][1]; c2.u = A[ii][2];
+        c0.u = A[ii][0]; c1.u = A[ii][1]; c2.u = A[ii][NP - 1];
         Split3 av;
         av.hi = c0.h; av.mid = c1.h; av.lo = c2.h;
 #pragma unroll
@@ -1881,6 +2111,14 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       }
       if (more) storeB((s + 1) & 1);
       __syncthreads();
+    }
+    if constexpr (H3) {  // exact: both factors are powers of two
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * iA * iB;
     }
     // every tile leaves its piece(s) in `part` (k_wsk_reduce<128, 128>, as k_wgrad_sk)
     constexpr int PSZ = BM * BN;

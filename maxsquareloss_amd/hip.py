@@ -43,6 +43,14 @@ SIGNATURES = {
     "msl_pconv_dgrad_acc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_wgrad_workspace": (c_sz, [c_int] * 3),
     "msl_pconv_wgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
+    "msl_absmax_parts": (c_int, []),
+    "msl_absmax_partials": (c_int, [c_p, c_ll, c_p, c_p]),
+    "msl_dconv_fwd_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_dconv_dgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_dconv_wgrad_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_pconv_fwd_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_pconv_dgrad_acc_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_pconv_wgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
     "msl_dconv_fwd_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_wgrad_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p]),
@@ -73,6 +81,8 @@ SIGNATURES = {
     "msl_bn_workspace": (c_sz, [c_int, c_int]),
     "msl_bn_fwd": (c_int, [c_p] * 10 + [c_int] * 4 + [c_f, c_f, c_int, c_p, c_sz, c_p]),
     "msl_bn_bwd": (c_int, [c_p] * 10 + [c_int] * 5 + [c_p, c_sz, c_p]),
+    "msl_bn_fwd_am": (c_int, [c_p] * 10 + [c_int] * 4 + [c_f, c_f, c_int, c_p, c_sz, c_p, c_p]),
+    "msl_bn_bwd_am": (c_int, [c_p] * 10 + [c_int] * 5 + [c_p, c_sz, c_p, c_p]),
     "msl_image_transform": (c_int, [c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p, c_p]),
     "msl_label_transform": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
     "msl_sgd_block_elems": (c_int, []),

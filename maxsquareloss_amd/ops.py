@@ -29,8 +29,18 @@ def set_conv_math(math):
 # Matrix-core form of the fp32 conv math, held process-wide by the library
 # (msl_conv_set_f32_form): "mfma_f32" = v_mfma_f32_32x32x2_f32, an exact fmaf chain; "bf16x6" =
 # each operand split into three bf16 terms, six products per 16-deep K slice on
-# v_mfma_f32_32x32x16_bf16 with fp32 sums (fp32-accurate; csrc/dconv_kernels.h Split3).
-F32_FORMS = {"mfma_f32": 0, "bf16x6": 2}
+# v_mfma_f32_32x32x16_bf16 with fp32 sums (fp32-accurate; csrc/dconv_kernels.h Split3); "f16x3" =
+# each operand tensor scaled by a power of two and split into two fp16 terms, three products per
+# slice on v_mfma_f32_32x32x16_f16 with fp32 sums (fp32-accurate; dconv_kernels.h Split2h).
+F32_FORMS = {"mfma_f32": 0, "bf16x6": 2, "f16x3": 5}
+SPLIT_FORMS = ("bf16x6", "f16x3")  # the forms the HIP pointwise / 128-row kernels run split
+_FORM = [None]  # the library's current form code, mirrored for the pack-cache keys
+
+
+def _form_code():
+    if _FORM[0] is None:
+        _FORM[0] = hip.load(require_gpu=False).msl_conv_f32_form()
+    return _FORM[0]
 
 
 def set_f32_form(form):
@@ -40,6 +50,7 @@ def set_f32_form(form):
     lib = hip.load(require_gpu=False)
     prev = lib.msl_conv_f32_form()
     hip.check(lib.msl_conv_set_f32_form(F32_FORMS[form]), "msl_conv_set_f32_form")
+    _FORM[0] = F32_FORMS[form]  # packs are form-specific: the cache keys change with it
     return {v: k for k, v in F32_FORMS.items()}[prev]
 
 
@@ -59,6 +70,56 @@ def f32_form():
 
 def _fn(lib, name, math):
     return getattr(lib, name + "_bf16") if math == "bf16" else getattr(lib, name)
+
+
+def _h3(math="fp32"):
+    return math == "fp32" and _form_code() == F32_FORMS["f16x3"]
+
+
+def _tag_absmax(t, part):
+    """Attach the per-channel absmax partials a BN kernel wrote for its output `t` (msl_bn_*_am)."""
+    t._msl_absmax = (part, t._version)
+
+
+def _parts(t, math="fp32", compute=True):
+    """The absmax partials of an operand tensor for the f16x3 form, as (tensor, count): the ones the
+    BN kernel that produced `t` wrote (msl_bn_fwd_am / msl_bn_bwd_am: one per channel, no pass of
+    their own), else - when `compute` - msl_absmax_partials, so that a tensor two GEMMs read (x:
+    forward and weight gradient; dy: data and weight gradient) is reduced once.  None in the other
+    forms (the kernels ignore them), or when not worth a launch (the entry point then reduces the
+    operand itself if its kernel needs it)."""
+    if not _h3(math):
+        return None
+    rec = getattr(t, "_msl_absmax", None)
+    if rec is not None and rec[1] == t._version:
+        return rec[0], rec[0].numel()
+    if not compute:
+        return None
+    lib = hip.load()
+    part = torch.empty(lib.msl_absmax_parts(), dtype=_f32, device=t.device)
+    hip.check(lib.msl_absmax_partials(t.data_ptr(), t.numel(), part.data_ptr(), hip.stream_ptr()),
+              "msl_absmax_partials")
+    return part, part.numel()
+
+
+def _pp(q):
+    """(pointer, count) of _parts' result for the _sc entry points."""
+    return (None, 0) if q is None else (q[0].data_ptr(), q[1])
+
+
+def _conv_call(lib, name, math, args, parts):
+    """fp32: the _sc entry point, given the operands' absmax partials (None = the call reduces them
+    itself; ignored outside f16x3); bf16: the _bf16 entry point."""
+    if math == "bf16":
+        return getattr(lib, name + "_bf16")(*args)
+    return getattr(lib, name + "_sc")(*args, *(v for q in parts for v in _pp(q)))
+
+
+def _split_gemm(m, k_other):
+    """Whether a forward-form GEMM with M output rows runs a split (f16x3) kernel that scales its
+    image operand (128-row tiles: M > 64), or a weight gradient of these channel counts the pre-split
+    kernel (both >= 128): a partials launch only pays off where one of them reads the tensor."""
+    return m > 64 or min(m, k_other) >= 128
 
 
 def _check_act(x, name):
@@ -107,7 +168,7 @@ class PackCache:
 
     @staticmethod
     def key_of(weights):
-        return tuple((w.data_ptr(), w._version) for w in weights)
+        return (_form_code(),) + tuple((w.data_ptr(), w._version) for w in weights)
 
     def get(self, weights, cin, cout, for_dgrad):
         key = self.key_of(weights)
@@ -265,16 +326,18 @@ class _DConv3x3(Function):
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         math = CONV_MATH
-        hip.check(_fn(lib, "msl_dconv_fwd", math)(x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb,
-                                    cin, cout, h, w, dil0, dil1 if nb > 1 else 0,
-                                    hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
-                                    hip.stream_ptr()), "msl_dconv_fwd")
+        xpart = _parts(x, math, compute=_split_gemm(cout, cin))
+        hip.check(_conv_call(lib, "msl_dconv_fwd", math,
+                             (x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb, cin, cout, h, w, dil0,
+                              dil1 if nb > 1 else 0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                              hip.stream_ptr()), (xpart,)), "msl_dconv_fwd")
         if probe is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             probe.append((ev0, ev1))
         ctx.save_for_backward(x, *weights)
         ctx.meta = (nb, cin, cout, h, w, dil0, dil1, b0 is not None, cache, math)
+        ctx.xpart = xpart
         return y
 
     @staticmethod
@@ -286,27 +349,32 @@ class _DConv3x3(Function):
         s = hip.stream_ptr()
         d1 = dil1 if nb > 1 else 0
         dx = None
+        gpart = _parts(gy, math, compute=_split_gemm(cin, cout))
+        xpart = ctx.xpart
         if ctx.needs_input_grad[0]:
             packed_d = cache.get(weights, cin, cout, 1)
             dx = torch.empty_like(x)
             wsb = lib.msl_dconv_dgrad_workspace(nb, cin, cout, h, w)
             ws = hip.workspace(wsb, x.device)
-            hip.check(_fn(lib, "msl_dconv_dgrad", math)(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin,
-                                          cout, h, w, dil0, d1, hip.counters(x.device).data_ptr(),
-                                          ws.data_ptr(), wsb, s), "msl_dconv_dgrad")
+            hip.check(_conv_call(lib, "msl_dconv_dgrad", math,
+                                 (gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin, cout, h, w, dil0, d1,
+                                  hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (gpart,)),
+                      "msl_dconv_dgrad")
         sink = grad_sink(weights[0]) if (nb == 1 and not has_bias and ctx.needs_input_grad[1]) else None
         wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w)
         ws = hip.workspace(wsb, x.device)
         if sink is not None:
             g, fg, i = sink
-            hip.check(_fn(lib, "msl_dconv_wgrad", math)(x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w,
-                                          dil0, 0, 1, ws.data_ptr(), wsb, s), "msl_dconv_wgrad")
+            hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
+                                 (x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w, dil0, 0, 1,
+                                  ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
             fg.notify(i)
             return dx, None, None, None, None, None, None, None
         dw_all = torch.empty((nb, cout, cin, 3, 3), dtype=_f32, device=x.device)
         db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
-        hip.check(_fn(lib, "msl_dconv_wgrad", math)(x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb,
-                                      cin, cout, h, w, dil0, d1, 0, ws.data_ptr(), wsb, s), "msl_dconv_wgrad")
+        hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
+                             (x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb, cin, cout, h, w,
+                              dil0, d1, 0, ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
         dw0 = dw_all[0]
         dw1 = dw_all[1] if nb > 1 else None
         db0 = db_all[0] if has_bias else None
@@ -342,11 +410,14 @@ class _PConv(Function):
         wsb = lib.msl_pconv_fwd_workspace(cin, cout, p)
         ws = hip.workspace(wsb, x.device)
         math = CONV_MATH
-        hip.check(_fn(lib, "msl_pconv_fwd", math)(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
-                                    hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
-                                    hip.stream_ptr()), "msl_pconv_fwd")
+        xpart = _parts(x, math, compute=_split_gemm(cout, cin))
+        hip.check(_conv_call(lib, "msl_pconv_fwd", math,
+                             (x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
+                              hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()), (xpart,)),
+                  "msl_pconv_fwd")
         ctx.save_for_backward(x, weight)
         ctx.meta = (cin, cout, p, cache, math)
+        ctx.xpart = xpart
         return y
 
     @staticmethod
@@ -357,22 +428,29 @@ class _PConv(Function):
         lib = hip.load()
         s = hip.stream_ptr()
         dx = None
+        gpart = _parts(gy, math, compute=_split_gemm(cin, cout))
         if ctx.needs_input_grad[0]:
             packed_d = cache.get([weight], cin, cout, 1)
             dx = torch.empty_like(x)
             wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
             ws = hip.workspace(wsb, x.device)
-            hip.check(_fn(lib, "msl_pconv_dgrad", math)(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
-                                          hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s),
-                      "msl_pconv_dgrad")
+            if math == "bf16":
+                hip.check(lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
+                                                   hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s),
+                          "msl_pconv_dgrad")
+            else:
+                hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
+                                                     0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s,
+                                                     *_pp(gpart)), "msl_pconv_dgrad")
         if not ctx.needs_input_grad[1]:
             return dx, None, None
         sink = grad_sink(weight)
         dst = sink[0] if sink is not None else torch.empty_like(weight)
         wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
         ws = hip.workspace(wsb, x.device)
-        hip.check(_fn(lib, "msl_pconv_wgrad", math)(x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p,
-                                                   int(sink is not None), ws.data_ptr(), wsb, s), "msl_pconv_wgrad")
+        hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
+                             (x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p, int(sink is not None),
+                              ws.data_ptr(), wsb, s), (ctx.xpart, gpart)), "msl_pconv_wgrad")
         if sink is None:
             return dx, dst, None
         sink[1].notify(sink[2])
@@ -419,12 +497,16 @@ def conv1x1_plan(cin, cout, p, form="bf16x6", residual=False):
     accumulating form beats MIOpen + add by 3-4 us on every box measured).  The HIP forward-form
     GEMMs run the hybrid schedule (SkArgs: data-parallel rounds + a stream-K remainder), which
     is what makes them win on the >= 512-tile shapes (256 -> 1024: 53 vs 61 us pure stream-K).
+    In the f16x3 form (profiles/r02_conv1x1_dispatch_f16x3.txt) the HIP kernels win every GEMM of
+    the wide shapes outright (256 -> 1024 fwd 35 vs 50 us MIOpen, 1024 -> 256 dgrad 35 vs 45), so
+    there the wide forward and data gradient are HIP whatever the direction or residual.
     """
-    x6 = form == "bf16x6"
+    x6 = form in SPLIT_FORMS
+    h3 = form == "f16x3"
     big = p > 16384
     wide = max(cin, cout) >= 1024 and min(cin, cout) >= 256
-    fwd = "hip" if x6 and (big or (wide and cin >= 512)) else "miopen"
-    if x6 and ((big and cin > cout) or (not big and wide and (residual or not (cin > cout and cout < 512)))):
+    fwd = "hip" if x6 and (big or (wide and (cin >= 512 or h3))) else "miopen"
+    if x6 and ((big and cin > cout) or (not big and wide and (h3 or residual or not (cin > cout and cout < 512)))):
         dgrad = "hip"
     elif cout > cin or big:
         dgrad = "hipblaslt"
@@ -457,15 +539,17 @@ class _Conv1x1(Function):
         plan = _PLANS.get(key)
         if plan is None:
             plan = _PLANS[key] = conv1x1_plan(cin, cout, p, form, hold is not None)
+        # f16x3: x's absmax partials once for the HIP forward and the HIP weight gradient
+        ctx.xpart = _parts(x, compute=plan[0] == "hip" and plan[2] == "hip")
         if plan[0] == "hip":
             lib = hip.load()
             packed = cache.get([weight], cin, cout, 0)
             y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
             wsb = lib.msl_pconv_fwd_workspace(cin, cout, p)
             ws = hip.workspace(wsb, x.device)
-            hip.check(lib.msl_pconv_fwd(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
-                                        hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()),
-                      "msl_pconv_fwd")
+            hip.check(lib.msl_pconv_fwd_sc(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
+                                           hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr(),
+                                           *_pp(ctx.xpart)), "msl_pconv_fwd")
         else:
             y = F.conv2d(x, weight)
         ctx.save_for_backward(x, weight)
@@ -486,6 +570,9 @@ class _Conv1x1(Function):
         w2 = weight.view(cout, cin)
         dx = None
         hold = ctx.hold
+        # f16x3: dy's absmax partials once for the HIP data and weight gradients
+        gpart = _parts(gy, compute=dplan == "hip" and wplan == "hip" and ctx.needs_input_grad[0]
+                       and ctx.needs_input_grad[1])
         if ctx.needs_input_grad[0] and hold is not None and hold.g is not None:
             # dx = (the residual's gradient) + W^T dy, accumulated by the GEMM itself
             dx, hold.g = hold.g, None
@@ -494,9 +581,9 @@ class _Conv1x1(Function):
                 packed_d = ctx.cache.get([weight], cin, cout, 1)
                 wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
                 ws = hip.workspace(wsb, x.device)
-                hip.check(lib.msl_pconv_dgrad_acc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, 1,
-                                                  hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
-                                                  hip.stream_ptr()), "msl_pconv_dgrad_acc")
+                hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
+                                                     1, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                                                     hip.stream_ptr(), *_pp(gpart)), "msl_pconv_dgrad_acc")
             elif dplan == "hipblaslt":
                 dx.view(cin, p).addmm_(w2.t(), g2)
             else:  # MIOpen's data gradient has no accumulate form: the add stays a kernel of its own
@@ -509,9 +596,9 @@ class _Conv1x1(Function):
                 dx = torch.empty_like(x)
                 wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
                 ws = hip.workspace(wsb, x.device)
-                hip.check(lib.msl_pconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
-                                              hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
-                                              hip.stream_ptr()), "msl_pconv_dgrad")
+                hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
+                                                     0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                                                     hip.stream_ptr(), *_pp(gpart)), "msl_pconv_dgrad")
             elif dplan == "hipblaslt":
                 dx = torch.mm(w2.t(), g2).view(1, cin, h, w)
             else:
@@ -526,9 +613,9 @@ class _Conv1x1(Function):
             dst = sink[0] if sink is not None else torch.empty_like(weight)
             wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
             ws = hip.workspace(wsb, x.device)
-            hip.check(lib.msl_pconv_wgrad(x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p,
-                                          int(sink is not None), ws.data_ptr(), wsb, hip.stream_ptr()),
-                      "msl_pconv_wgrad")
+            hip.check(lib.msl_pconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p,
+                                             int(sink is not None), ws.data_ptr(), wsb, hip.stream_ptr(),
+                                             *_pp(ctx.xpart), *_pp(gpart)), "msl_pconv_wgrad")
             if sink is None:
                 return dx, dst, None, None
         elif sink is not None:
@@ -859,11 +946,15 @@ class _BNAct(Function):
         wsb = lib.msl_bn_workspace(c, p)
         ws = hip.workspace(wsb, x.device)
         update = bool(training) and running_mean is not None
-        hip.check(lib.msl_bn_fwd(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
-                                 hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
-                                 save_mean.data_ptr(), save_invstd.data_ptr(), c, p, int(bool(training)), int(update),
-                                 float(momentum), float(eps), int(bool(relu)), ws.data_ptr(), wsb, hip.stream_ptr()),
-                  "msl_bn_fwd")
+        # f16x3: the per-channel absmax of y for the convs that read it (their operand scales)
+        am = torch.empty(c, dtype=_f32, device=x.device) if _h3(CONV_MATH) else None
+        hip.check(lib.msl_bn_fwd_am(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
+                                    hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
+                                    save_mean.data_ptr(), save_invstd.data_ptr(), c, p, int(bool(training)),
+                                    int(update), float(momentum), float(eps), int(bool(relu)), ws.data_ptr(), wsb,
+                                    hip.stream_ptr(), hip.ptr(am)), "msl_bn_fwd")
+        if am is not None:
+            _tag_absmax(y, am)
         ctx.save_for_backward(x, weight, y if relu else None, save_mean, save_invstd)
         ctx.bias = bias
         ctx.meta = (c, p, bool(training), bool(relu))
@@ -890,10 +981,14 @@ class _BNAct(Function):
             dbeta = torch.empty(c, dtype=_f32, device=x.device) if nig[2] else None
         wsb = lib.msl_bn_workspace(c, p)
         ws = hip.workspace(wsb, x.device)
-        hip.check(lib.msl_bn_bwd(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight), save_mean.data_ptr(),
-                                 save_invstd.data_ptr(), hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta),
-                                 c, p, int(training), int(relu), int(direct), ws.data_ptr(), wsb, hip.stream_ptr()),
-                  "msl_bn_bwd")
+        # f16x3: the per-channel absmax of dx, the gradient the conv before this BN reads twice
+        am = torch.empty(c, dtype=_f32, device=x.device) if (dx is not None and _h3(CONV_MATH)) else None
+        hip.check(lib.msl_bn_bwd_am(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight), save_mean.data_ptr(),
+                                    save_invstd.data_ptr(), hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma),
+                                    hip.ptr(dbeta), c, p, int(training), int(relu), int(direct), ws.data_ptr(), wsb,
+                                    hip.stream_ptr(), hip.ptr(am)), "msl_bn_bwd")
+        if am is not None:
+            _tag_absmax(dx, am)
         if direct:
             sw[1].notify(sw[2])
             sb[1].notify(sb[2])

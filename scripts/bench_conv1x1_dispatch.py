@@ -1,6 +1,6 @@
 """Per-GEMM timing of every stride-1 1x1 conv of the model (1024x512 input): each of the three GEMMs
 (y = W x, dx = W^T dy, dW += dy x^T) on every implementation available - MIOpen, hipBLASLt
-(torch.mm / addmm_) and the HIP bf16x6 pointwise kernels - weighted by how often the UDA step runs
+(torch.mm / addmm_) and the HIP pointwise kernels (hip_x6 = the split fp32 form in use: bf16x6 or f16x3) - weighted by how often the UDA step runs
 it.  Prints the per-GEMM winners as the dispatch table of ops._Conv1x1 (profiles/)."""
 import json
 import os
@@ -36,6 +36,10 @@ def main():
     lib = hip.load()
     if "--sk-hybrid" in sys.argv:  # A/B of the forward-form schedule (msl_conv_set_sk_hybrid)
         hip.check(lib.msl_conv_set_sk_hybrid(int(sys.argv[sys.argv.index("--sk-hybrid") + 1])), "sk_hybrid")
+    if "--form" in sys.argv:  # the fp32 form of the HIP kernels (default: the library's)
+        ops.set_f32_form(sys.argv[sys.argv.index("--form") + 1])
+    print(f"fp32 form of the HIP GEMMs: {ops.f32_form()} (f16x3: the operands' absmax partials computed once, "
+          "outside the timed calls, as the BN kernels hand them over in the step)", flush=True)
     table, tot = {}, {"lib": 0.0, "best": 0.0}
     for (cin, cout, h, w), n in SHAPES.items():
         p = h * w
@@ -51,24 +55,30 @@ def main():
         wsd = hip.workspace(lib.msl_pconv_dgrad_workspace(cin, cout, p), x.device)
         wsw = hip.workspace(lib.msl_pconv_wgrad_workspace(cin, cout, p), x.device)
         y, dx, dw = torch.empty(1, cout, h, w, device="cuda"), torch.empty_like(x), torch.zeros_like(wt)
+        npart = lib.msl_absmax_parts()
+        xp, gp = torch.empty(npart, device="cuda"), torch.empty(npart, device="cuda")
+        lib.msl_absmax_partials(x.data_ptr(), x.numel(), xp.data_ptr(), s)
+        lib.msl_absmax_partials(gy.data_ptr(), gy.numel(), gp.data_ptr(), s)
         r = {}
         r["fwd"] = {
             "miopen": t(lambda: F.conv2d(x, wt)),
             "hipblaslt": t(lambda: torch.mm(w2, x2)),
-            "hip_x6": t(lambda: lib.msl_pconv_fwd(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p, ctr,
-                                                  wsf.data_ptr(), wsf.numel(), s)),
+            "hip_x6": t(lambda: lib.msl_pconv_fwd_sc(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p, ctr,
+                                                     wsf.data_ptr(), wsf.numel(), s, xp.data_ptr(), npart)),
         }
         r["dgrad"] = {
             "miopen": t(lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (1, 1), (0, 0), (1, 1), False,
                                                                      (0, 0), 1, (True, False, False))),
             "hipblaslt": t(lambda: torch.mm(w2.t(), g2)),
-            "hip_x6": t(lambda: lib.msl_pconv_dgrad(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
-                                                    ctr, wsd.data_ptr(), wsd.numel(), s)),
+            "hip_x6": t(lambda: lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout,
+                                                           p, 0, ctr, wsd.data_ptr(), wsd.numel(), s, gp.data_ptr(),
+                                                           npart)),
         }
         r["wgrad"] = {
             "hipblaslt": t(lambda: dw.view(cout, cin).addmm_(g2, x2.t())),
-            "hip_x6": t(lambda: lib.msl_pconv_wgrad(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), cin, cout, p, 1,
-                                                    wsw.data_ptr(), wsw.numel(), s)),
+            "hip_x6": t(lambda: lib.msl_pconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), cin, cout, p, 1,
+                                                       wsw.data_ptr(), wsw.numel(), s, xp.data_ptr(), npart,
+                                                       gp.data_ptr(), npart)),
         }
         # dx += W^T dy (the identity residual's gradient summed by the data-gradient GEMM,
         # ops.ResidualGrad): separate add after MIOpen vs the accumulating GEMMs
@@ -77,8 +87,9 @@ def main():
             "miopen+add": t(lambda: res.add_(torch.ops.aten.convolution_backward(
                 gy, x, wt, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1, (True, False, False))[0])),
             "hipblaslt_addmm": t(lambda: res.view(cin, p).addmm_(w2.t(), g2)),
-            "hip_x6_acc": t(lambda: lib.msl_pconv_dgrad_acc(gy.data_ptr(), packed_d.data_ptr(), res.data_ptr(), cin,
-                                                            cout, p, 1, ctr, wsd.data_ptr(), wsd.numel(), s)),
+            "hip_x6_acc": t(lambda: lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), res.data_ptr(), cin,
+                                                               cout, p, 1, ctr, wsd.data_ptr(), wsd.numel(), s,
+                                                               gp.data_ptr(), npart)),
         }
         pack = t(lambda: (lib.msl_pconv_pack(wt.data_ptr(), cin, cout, 0, packed.data_ptr(), s),
                           lib.msl_pconv_pack(wt.data_ptr(), cin, cout, 1, packed_d.data_ptr(), s)))

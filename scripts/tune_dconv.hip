@@ -248,9 +248,9 @@ float run_wgrad_x6(const Shape& sh, const float* x, const float* dy, float* dw, 
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int it = -2; it < iters; ++it) {
     if (it == 0) CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_split_rows, dim3(a.lda / 64, (a.KS + 3) / 4), dim3(256), 0, 0, dy, a.M, P, a.KS, a.lda, planes);
+    hipLaunchKernelGGL(k_split_rows<kMathX6>, dim3(a.lda / 64, (a.KS + 3) / 4), dim3(256), 0, 0, dy, a.M, P, a.KS, a.lda, planes, (const float*)nullptr);
     if (split_only) continue;
-    hipLaunchKernelGGL(k_wgrad_x6, dim3(a.NW), dim3(256), 0, 0, a);
+    hipLaunchKernelGGL(k_wgrad_x6<kMathX6>, dim3(a.NW), dim3(256), 0, 0, a);
     hipLaunchKernelGGL((k_wsk_reduce<128, 128>), dim3(128 * 128 / 4 * 9 / 256, a.tiles_m * a.tiles_n), dim3(256), 0, 0, a);
   }
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));

@@ -17,9 +17,9 @@ from maxsquareloss_amd import ops  # noqa: E402
 DEV = "cuda"
 
 
-@pytest.fixture(params=["mfma_f32", "bf16x6"])
+@pytest.fixture(params=["mfma_f32", "bf16x6", "f16x3"])
 def f32_form(request):
-    """Both matrix-core forms of the fp32 convs are held to the same fp64 tolerance."""
+    """Every matrix-core form of the fp32 convs is held to the same fp64 tolerance."""
     prev = ops.set_f32_form(request.param)
     yield request.param
     ops.set_f32_form(prev)
@@ -425,10 +425,21 @@ def test_pack_forms_identical(kind, nb, cin, cout, for_dgrad):
     assert torch.equal(bufs[0].view(torch.int32), bufs[1].view(torch.int32))
 
 
-def test_pack_batch_matches_per_conv_packs():
+def _defined(buf, form):
+    """The defined part of a packed buffer (fp32 pack F, planes region 1.5 F, 320-float tail): the
+    bf16x6 planes fill their region; the f16x3 ones its first F floats, and that form writes the
+    weights' absmax partials (256) and {scale, 1/scale} into the tail."""
+    f32 = (buf.numel() - 320) * 2 // 5
+    if form != "f16x3":
+        return buf[:buf.numel() - 320].view(torch.int32)
+    return torch.cat([buf[:2 * f32], buf[buf.numel() - 320:buf.numel() - 62]]).view(torch.int32)
+
+
+def test_pack_batch_matches_per_conv_packs(f32_form):
     """ops.PackBatch (msl_conv_pack_many: every pack of a step in one launch per tap count) writes
     exactly the bytes of the per-conv msl_*_pack calls, for 9- and 1-tap packs, both directions,
-    a 2-branch ASPP pack and M <= 64 (no planes) - exactly the stale ones."""
+    a 2-branch ASPP pack and M <= 64 (no planes) - exactly the stale ones - in every fp32 form
+    (f16x3: the fp16 planes and the weights' scale too)."""
     import torch.nn as nn
     g = torch.Generator().manual_seed(5)
 
@@ -474,7 +485,7 @@ def test_pack_batch_matches_per_conv_packs():
     assert batch.run() and batch.launches == 1
     torch.cuda.synchronize()
     for d in (0, 1):
-        assert torch.equal(hs[0]._pack.buf[d].view(torch.int32), ref[0][d].view(torch.int32))
+        assert torch.equal(_defined(hs[0]._pack.buf[d], f32_form), _defined(ref[0][d], f32_form))
     with torch.no_grad():
         for h in hs:
             for w in h.ws:
@@ -495,8 +506,12 @@ def test_pack_batch_matches_per_conv_packs():
             total = ops.hip.load().msl_dconv_packed_elems(len(h.ws), h.dims[0], h.dims[1], d) if not h._pack.pointwise \
                 else ops.hip.load().msl_pconv_packed_elems(h.dims[0], h.dims[1], d)
             m = h.dims[1] if d == 0 else h.dims[0]
-            n = total if m > 64 else total * 2 // 5  # M <= 64: no planes behind the fp32 pack
-            assert torch.equal(h._pack.buf[d][:n].view(torch.int32), r[d][:n].view(torch.int32)), (h.dims, d)
+            # M <= 64: no planes (and no f16x3 tail) behind the fp32 pack
+            n = (total - 320) * 2 // 5
+            if m > 64:
+                assert torch.equal(_defined(h._pack.buf[d], f32_form), _defined(r[d], f32_form)), (h.dims, d)
+            else:
+                assert torch.equal(h._pack.buf[d][:n].view(torch.int32), r[d][:n].view(torch.int32)), (h.dims, d)
             # the per-conv calls never touch the planes region of an M <= 64 pack; neither does the batch
             if m <= 64:
                 assert torch.isnan(h._pack.buf[d][n:]).all()
@@ -592,12 +607,15 @@ def test_sk_hybrid_schedule(cin, cout, h, w, f32_form):
 
 @pytest.mark.parametrize("cin,cout,h,w", [(256, 1024, 65, 129), (512, 2048, 17, 33), (128, 512, 33, 65),
                                            (1024, 256, 65, 129), (200, 328, 9, 31)])
-def test_pconv_wgrad_accumulate_both_orientations(cin, cout, h, w):
-    """msl_pconv_wgrad, accumulate = 1, bf16x6: with cout > cin the kernel runs on the swapped
-    operands (the image pre-split, dW^T tiles transposed by the reduce); either way dW += dy x^T."""
+@pytest.mark.parametrize("form", ["bf16x6", "f16x3"])
+def test_pconv_wgrad_accumulate_both_orientations(cin, cout, h, w, form):
+    """msl_pconv_wgrad, accumulate = 1, in both split forms: with cout > cin the kernel runs on the
+    swapped operands (the image pre-split, dW^T tiles transposed by the reduce); either way
+    dW += dy x^T.  f16x3: msl_pconv_wgrad_sc given the operands' absmax partials
+    (msl_absmax_partials) writes exactly the bytes of the plain call, which reduces them itself."""
     from maxsquareloss_amd import hip
     lib = hip.load()
-    prev = ops.set_f32_form("bf16x6")
+    prev = ops.set_f32_form(form)
     try:
         g = torch.Generator().manual_seed(cin * 5 + cout)
         p = h * w
@@ -612,5 +630,113 @@ def test_pconv_wgrad_accumulate_both_orientations(cin, cout, h, w):
                                    hip.stream_ptr()) == 0
         torch.cuda.synchronize()
         assert _rel(dw, ref) < 1e-5
+        if form == "f16x3":
+            np_ = lib.msl_absmax_parts()
+            xp, gp = torch.empty(np_, device=DEV), torch.empty(np_, device=DEV)
+            for t, q in ((xd, xp), (gd, gp)):
+                assert lib.msl_absmax_partials(t.data_ptr(), t.numel(), q.data_ptr(), hip.stream_ptr()) == 0
+            assert xp.max().item() == x.abs().max().item() and gp.max().item() == gy.abs().max().item()
+            dw2 = dw0.to(DEV)
+            assert lib.msl_pconv_wgrad_sc(xd.data_ptr(), gd.data_ptr(), dw2.data_ptr(), cin, cout, p, 1, ws.data_ptr(),
+                                          wsb, hip.stream_ptr(), xp.data_ptr(), np_, gp.data_ptr(), np_) == 0
+            torch.cuda.synchronize()
+            assert torch.equal(dw2, dw)
     finally:
         ops.set_f32_form(prev)
+
+
+def _elem_err(out, ref, bound):
+    """max over elements of |out - ref| / (the same conv of |operands|): the error relative to the
+    element's own sum of |terms|, the measure fp32 accumulation is judged by."""
+    out, ref, bound = (t.detach().double().cpu() for t in (out, ref, bound))
+    return ((out - ref).abs() / bound.clamp_min(1e-300)).max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xs,gs", [(1.0, 1.0), (1e-20, 1e15), (3e4, 1e-30)])
+@pytest.mark.parametrize("cin,cout,h,w,d", [(256, 256, 33, 65, 2), (512, 512, 17, 33, 4)])
+def test_f16x3_is_fp32_accurate(cin, cout, h, w, d, xs, gs):
+    """The f16x3 form (per-tensor power-of-two scale, two fp16 terms, three fp16 MFMAs) against fp64,
+    per element relative to the element's sum of |terms|, next to the exact fp32 MFMA and bf16x6 on
+    the same operands: fwd, data and weight gradients, at unit scale and at operand scales far
+    outside fp16's range (weights ~1e-2, the 1e-20 / 1e-30 / 3e4 / 1e15 factors exercise the
+    scaling).  Bar: within 2x the exact fp32 MFMA's error, and below 2e-7."""
+    g = torch.Generator().manual_seed(cin + h)
+    x = torch.relu(torch.randn(1, cin, h, w, generator=g)) * xs
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.01
+    gy = torch.randn(1, cout, h, w, generator=g) * gs
+    xr, wr = x.double().requires_grad_(), wt.double().requires_grad_()
+    yr = F.conv2d(xr, wr, padding=d, dilation=d)
+    yr.backward(gy.double())
+    # sums of |terms| of every output element (conv of the absolute operands)
+    xa, wa, ga = x.double().abs().requires_grad_(), wt.double().abs().requires_grad_(), gy.double().abs()
+    ya = F.conv2d(xa, wa, padding=d, dilation=d)
+    ya.backward(ga)
+    errs = {}
+    for form in ("mfma_f32", "bf16x6", "f16x3"):
+        prev = ops.set_f32_form(form)
+        try:
+            xg = x.to(DEV).requires_grad_()
+            wg = wt.to(DEV).requires_grad_()
+            y = ops.dconv3x3(xg, wg, d, ops.PackCache())
+            y.backward(gy.to(DEV))
+            torch.cuda.synchronize()
+            errs[form] = (_elem_err(y, yr, ya), _elem_err(xg.grad, xr.grad, xa.grad),
+                          _elem_err(wg.grad, wr.grad, wa.grad))
+        finally:
+            ops.set_f32_form(prev)
+    for i, what in enumerate(("fwd", "dgrad", "wgrad")):
+        e, ref = errs["f16x3"][i], errs["mfma_f32"][i]
+        assert e < 2e-7 and e <= 2.0 * max(ref, 1e-8), (what, errs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("c,h,w,res,relu", [(256, 65, 129, True, True), (64, 129, 257, False, True),
+                                             (1024, 33, 65, False, False)])
+def test_bn_absmax_outputs(c, h, w, res, relu, fused):
+    """msl_bn_fwd_am / msl_bn_bwd_am: the same y / dx / dres / dgamma / dbeta bytes as msl_bn_fwd /
+    msl_bn_bwd, plus absmax[c] = max |y[c]| (forward) and max |dx[c]| (backward) exactly, in the
+    fused and the split kernel forms (the f16x3 convs' operand partials)."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    prev = ops.set_bn_fused(fused)
+    try:
+        g = torch.Generator().manual_seed(c * 3 + h)
+        p = h * w
+        x = (torch.randn(c, p, generator=g) * 3 + 1).to(DEV)
+        r = torch.randn(c, p, generator=g).to(DEV) if res else None
+        gamma = (torch.rand(c, generator=g) + 0.5).to(DEV)
+        beta = torch.randn(c, generator=g).to(DEV)
+        gy = torch.randn(c, p, generator=g).to(DEV)
+        wsb = lib.msl_bn_workspace(c, p)
+        ws = hip.workspace(wsb, x.device)
+        s = hip.stream_ptr()
+        outs = []
+        for am in (False, True):
+            rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+            y, sm, si = torch.empty_like(x), torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+            dx, dres = torch.empty_like(x), torch.empty_like(x)
+            dg, db = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+            fa, ba = torch.full((c,), -1.0, device=DEV), torch.full((c,), -1.0, device=DEV)
+            fargs = (x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), hip.ptr(r), y.data_ptr(), rm.data_ptr(),
+                     rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, 1, 1, 0.1, 1e-5, int(relu), ws.data_ptr(),
+                     wsb, s)
+            bargs = (gy.data_ptr(), x.data_ptr(), y.data_ptr(), gamma.data_ptr(), sm.data_ptr(), si.data_ptr(),
+                     dx.data_ptr(), dres.data_ptr(), dg.data_ptr(), db.data_ptr(), c, p, 1, int(relu), 0, ws.data_ptr(),
+                     wsb, s)
+            if am:
+                assert lib.msl_bn_fwd_am(*fargs, fa.data_ptr()) == 0
+                assert lib.msl_bn_bwd_am(*bargs, ba.data_ptr()) == 0
+            else:
+                assert lib.msl_bn_fwd(*fargs) == 0
+                assert lib.msl_bn_bwd(*bargs) == 0
+            torch.cuda.synchronize()
+            outs.append((y, dx, dres, dg, db, fa, ba))
+        for a, b in zip(outs[0][:5], outs[1][:5]):
+            assert torch.equal(a, b)
+        y, dx, _, _, _, fa, ba = outs[1]
+        assert torch.equal(fa, y.abs().amax(dim=1))
+        assert torch.equal(ba, dx.abs().amax(dim=1))
+    finally:
+        ops.set_bn_fused(prev)

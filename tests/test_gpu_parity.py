@@ -42,7 +42,7 @@ def _rel(a, b):
     return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
 
 
-@pytest.fixture(params=["mfma_f32", "bf16x6"])
+@pytest.fixture(params=["mfma_f32", "bf16x6", "f16x3"])
 def f32_form(request):
     prev = ops.set_f32_form(request.param)
     yield request.param

@@ -48,10 +48,11 @@ def test_pure_host_entry_points():
     lib = hip.load(require_gpu=False)
     assert lib.msl_abi_version() == hip.ABI_VERSION
     assert lib.msl_status_string(-2) == b"workspace too small"
-    # packed-weight sizes: [nbranch][ceil(cimg/16)][9][16] rows x round_up(m, 128)
-    assert lib.msl_dconv_packed_elems(1, 256, 256, 0) == 16 * 9 * 16 * 256 * 5 // 2
-    assert lib.msl_dconv_packed_elems(2, 2048, 19, 0) == 2 * 128 * 9 * 16 * 128 * 5 // 2
-    assert lib.msl_dconv_packed_elems(2, 2048, 19, 1) == 2 * 2 * 9 * 16 * 2048 * 5 // 2
+    # packed-weight sizes: [nbranch][ceil(cimg/16)][9][16] rows x round_up(m, 128), x 2.5 for the
+    # planes, + the 320-float tail (the f16x3 form's weight absmax partials and scale)
+    assert lib.msl_dconv_packed_elems(1, 256, 256, 0) == 16 * 9 * 16 * 256 * 5 // 2 + 320
+    assert lib.msl_dconv_packed_elems(2, 2048, 19, 0) == 2 * 128 * 9 * 16 * 128 * 5 // 2 + 320
+    assert lib.msl_dconv_packed_elems(2, 2048, 19, 1) == 2 * 2 * 9 * 16 * 2048 * 5 // 2 + 320
     assert lib.msl_dconv_fwd_workspace(1, 256, 256, 65, 129) > 0  # split-K slabs at this size
     assert lib.msl_loss_stats_elems() == 64
     be = lib.msl_sgd_block_elems()
@@ -61,11 +62,13 @@ def test_pure_host_entry_points():
     off = np.zeros(8, np.int64)
     n = lib.msl_sgd_plan(numels.ctypes.data, 4, ent.ctypes.data, off.ctypes.data, 8)
     assert n == 4 and list(ent[:4]) == [0, 1, 2, 2] and list(off[:4]) == [0, 0, 0, be]
-    # matrix-core form of the fp32 convs: bf16x6 (2) by default, f32 MFMA (0) selectable, others refused
-    assert lib.msl_conv_f32_form() == 2
+    # matrix-core form of the fp32 convs: f16x3 (5) by default, f32 MFMA (0) and bf16x6 (2)
+    # selectable, others refused
+    assert lib.msl_conv_f32_form() == 5
     assert lib.msl_conv_set_f32_form(1) == -3 and lib.msl_conv_set_f32_form(7) == -3
     assert lib.msl_conv_set_f32_form(0) == 0 and lib.msl_conv_f32_form() == 0
     assert lib.msl_conv_set_f32_form(2) == 0 and lib.msl_conv_f32_form() == 2
+    assert lib.msl_conv_set_f32_form(5) == 0 and lib.msl_conv_f32_form() == 5
     assert lib.msl_bn_fused() == 1 and lib.msl_bn_set_fused(2) == -3
     assert lib.msl_bn_set_fused(0) == 0 and lib.msl_bn_fused() == 0
     assert lib.msl_bn_set_fused(1) == 0 and lib.msl_bn_fused() == 1
@@ -134,15 +137,18 @@ def test_bench_feature_geometry():
     assert bench.feat_hw(640) == 81 and bench.feat_hw(760) == 96 and bench.feat_hw(1280) == 161
 
 
-def test_conv1x1_plan_matches_measured_winners():
+@pytest.mark.parametrize("form,path", [("bf16x6", "r02_conv1x1_dispatch.txt"),
+                                       ("f16x3", "r02_conv1x1_dispatch_f16x3.txt")])
+def test_conv1x1_plan_matches_measured_winners(form, path):
     """ops.conv1x1_plan reproduces the per-GEMM winners measured on MI355X for every 1x1 shape of
-    the UDA step (profiles/r02_conv1x1_dispatch.txt), with near-ties allowed either way (within
-    10 % or 4 us of the best: the 20-us GEMMs move by that much from one box to the next)."""
+    the UDA step (profiles/r02_conv1x1_dispatch*.txt, per fp32 form of the HIP kernels), with
+    near-ties allowed either way (within 10 % or 4 us of the best: the 20-us GEMMs move by that
+    much from one box to the next)."""
     from maxsquareloss_amd import ops
     table = {}
     names = {"hip_x6": "hip", "miopen+add": "miopen", "hipblaslt_addmm": "hipblaslt", "hip_x6_acc": "hip"}
     key = None
-    for line in open(os.path.join(ROOT, "profiles", "r02_conv1x1_dispatch.txt")):
+    for line in open(os.path.join(ROOT, "profiles", path)):
         m = re.match(r"\s*(\d+)->\s*(\d+) P\s+(\d+) x\s*\d+ \| (.*) \| packs", line)
         if m:
             key = (int(m.group(1)), int(m.group(2)), int(m.group(3)))
@@ -162,10 +168,10 @@ def test_conv1x1_plan_matches_measured_winners():
     res_shapes = {(256, 64), (512, 128), (1024, 256), (2048, 512)}
     # decided by the full-step A/B instead (profiles/r02_plan_ab.txt): the 256 -> 1024 forward
     # stays on MIOpen, which wins in the step on the boxes where HIP loses in isolation
-    step_ab = {(256, 1024, "fwd")}
+    step_ab = {(256, 1024, "fwd")} if form == "bf16x6" else set()
     for (cin, cout, p), times in table.items():
-        plan = dict(zip(("fwd", "dgrad", "wgrad"), ops.conv1x1_plan(cin, cout, p)))
-        plan["dgrad_res"] = ops.conv1x1_plan(cin, cout, p, residual=True)[1]
+        plan = dict(zip(("fwd", "dgrad", "wgrad"), ops.conv1x1_plan(cin, cout, p, form)))
+        plan["dgrad_res"] = ops.conv1x1_plan(cin, cout, p, form, residual=True)[1]
         for gemm, t in times.items():
             if (gemm == "dgrad_res" and (cin, cout) not in res_shapes) or (cin, cout, gemm) in step_ab:
                 continue
@@ -299,7 +305,7 @@ def test_grad_reducer_two_ranks_gloo():
 
 def test_hot_kernels_keep_their_occupancy():
     """The compiler's resource report of the last build (Makefile: dconv.o.remarks): the forward-form
-    x6 GEMM and the x6 weight gradient run two workgroups (8 waves) per CU, so they must keep
+    x6 / f16x3 GEMMs and weight gradients run two workgroups (8 waves) per CU, so they must keep
     <= 256 VGPRs + AGPRs (2 waves per SIMD), and no msl kernel spills VGPRs to scratch.  (An
     epilogue change once took the forward to 242 VGPRs and one wave per SIMD: layer3 op 67 -> 90 us.)"""
     path = os.path.join(ROOT, "maxsquareloss_amd", "_lib", "obj", "dconv.o.remarks")
@@ -316,8 +322,10 @@ def test_hot_kernels_keep_their_occupancy():
         if m and kern:
             info[kern][m.group(1)] = int(m.group(2))
     hot = [k for k in info if k.startswith("_ZN3msl14k_igemm_fwd_skILi128ELi128ELi1ELi4ELi2ELi2ELb0ELi3E")
+           or k.startswith("_ZN3msl15k_igemm_fwd_sk2ILi128ELi128ELi1ELi4ELi2ELi2ELb0ELi5E")
            or k.startswith("_ZN3msl10k_wgrad_x6")]
-    assert len(hot) == 3, sorted(info)  # the x6 forward (plain, accumulating) and the x6 wgrad
+    # the x6 and f16x3 forwards (plain, accumulating) and the x6 / f16x3 weight gradients
+    assert len(hot) == 6, sorted(info)
     for k in hot:
         assert info[k]["Occupancy [waves/SIMD]"] >= 2, (k, info[k])
     for k, v in info.items():
