@@ -14,6 +14,11 @@ g = torch.Generator(device="cuda").manual_seed(0)
 x = torch.randn(1, 256, 65, 129, device="cuda", generator=g)
 w = torch.randn(256, 256, 3, 3, device="cuda", generator=g) * 0.02
 cache = ops.PackCache()
+# f16x3: in the step the input's absmax partials come from the BN kernel that produced it, so the
+# op launches no absmax pass; the same here (computed once, outside the profiled loop's op calls)
+q = ops._parts(x)
+if q is not None:
+    ops._tag_absmax(x, q[0])
 with torch.no_grad():
     for _ in range(n):
         y = ops.dconv3x3(x, w, 2, cache)
