@@ -390,13 +390,13 @@ static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials 
 }
 
 // The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
-template <int BM, int G, int ST, int WM, int WN, int MT>
+template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
   if constexpr (MT == kMathH3P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
     if (accum)
-      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
+      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true>), grid, block, 0, st, a, sk);
     else
-      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, false, MT, false>), grid, block, 0, st, a, sk);
+      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false>), grid, block, 0, st, a, sk);
   } else {
     if (accum)
       hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
@@ -491,7 +491,13 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
           a.bnpart = kNPart;
         }
         a.ascale = packed + pack_tail_offset(f32) + kNPart;
-        launch_sk<128, 1, 4, 2, 2, kMathH3P>(accum, grid, block, st, a, sk);
+        // pointwise: B rows are unshifted, so they move as dwordx4 (4 pixels per lane: 2 DMAs per
+        // wave and K-step instead of 8 dword ones): 1-4 us per call on the wide 1x1 GEMMs
+        // (profiles/r02_f16x3_pw_dma.txt)
+        if (taps == 1 && dil0 == 0)
+          launch_sk<128, 1, 4, 2, 2, kMathH3P, true>(accum, grid, block, st, a, sk);
+        else
+          launch_sk<128, 1, 4, 2, 2, kMathH3P>(accum, grid, block, st, a, sk);
       } else {
         launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
       }
