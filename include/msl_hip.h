@@ -333,6 +333,9 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
                   const float* save_mean, const float* save_invstd, float* dx, float* dres,
                   float* dgamma, float* dbeta, int c, int p, int training, int relu,
                   int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx);
+/* 1 if msl_bn_fwd / msl_bn_bwd run the fused one-block-per-channel kernels for this shape (their
+ * _am absmax output is then free; the split forms add a pass over the output). */
+int msl_bn_uses_fused(int c, int p, int training);
 /* BN kernel form (process-wide): 1 = train-mode layers with p <= 16384 (or p <= 33792 and
  * c >= 128) run one fused statistics+apply launch per call (one block per channel, operands held in registers), 0 =
  * the split statistics / flat-apply launches everywhere.  Returns 0, or MSL_ERR_ARG. */

@@ -514,6 +514,10 @@ int msl_bn_set_fused(int fused) {
 
 int msl_bn_fused(void) { return g_bn_fused; }
 
+int msl_bn_uses_fused(int c, int p, int training) {
+  return training && bn_fused_enabled() && c >= 1 && p >= 1 && bn_fused_shape(c, p) ? 1 : 0;
+}
+
 size_t msl_bn_workspace(int c, int p) {
   return align_up((size_t)c * bn_splits(p) * 2 * sizeof(double), 256);
 }

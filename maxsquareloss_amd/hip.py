@@ -78,6 +78,7 @@ SIGNATURES = {
     "msl_confusion_accumulate": (c_int, [c_p, c_p, c_int, ctypes.c_longlong, c_p, c_p, c_p]),
     "msl_bn_set_fused": (c_int, [c_int]),
     "msl_bn_fused": (c_int, []),
+    "msl_bn_uses_fused": (c_int, [c_int, c_int, c_int]),
     "msl_bn_workspace": (c_sz, [c_int, c_int]),
     "msl_bn_fwd": (c_int, [c_p] * 10 + [c_int] * 4 + [c_f, c_f, c_int, c_p, c_sz, c_p]),
     "msl_bn_bwd": (c_int, [c_p] * 10 + [c_int] * 5 + [c_p, c_sz, c_p]),

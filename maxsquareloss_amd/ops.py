@@ -946,8 +946,11 @@ class _BNAct(Function):
         wsb = lib.msl_bn_workspace(c, p)
         ws = hip.workspace(wsb, x.device)
         update = bool(training) and running_mean is not None
-        # f16x3: the per-channel absmax of y for the convs that read it (their operand scales)
-        am = torch.empty(c, dtype=_f32, device=x.device) if _h3(CONV_MATH) else None
+        # f16x3: the per-channel absmax of y for the convs that read it (their operand scales), where
+        # the fused kernel has it in registers; after a split-form BN (stem, 64-channel layer1) a
+        # conv that needs it reduces it itself (its first consumer is often an exact-f32 GEMM)
+        am = torch.empty(c, dtype=_f32, device=x.device) if (
+            _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(bool(training)))) else None
         hip.check(lib.msl_bn_fwd_am(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
                                     hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
                                     save_mean.data_ptr(), save_invstd.data_ptr(), c, p, int(bool(training)),
@@ -982,7 +985,8 @@ class _BNAct(Function):
         wsb = lib.msl_bn_workspace(c, p)
         ws = hip.workspace(wsb, x.device)
         # f16x3: the per-channel absmax of dx, the gradient the conv before this BN reads twice
-        am = torch.empty(c, dtype=_f32, device=x.device) if (dx is not None and _h3(CONV_MATH)) else None
+        am = torch.empty(c, dtype=_f32, device=x.device) if (
+            dx is not None and _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(training))) else None
         hip.check(lib.msl_bn_bwd_am(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight), save_mean.data_ptr(),
                                     save_invstd.data_ptr(), hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma),
                                     hip.ptr(dbeta), c, p, int(training), int(relu), int(direct), ws.data_ptr(), wsb,
