@@ -729,7 +729,14 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   } else if (pl.bm == 64) {
     hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2, MS>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_wsk_reduce<64, 64>), rgrid, rblock, 0, st, a);
+    // few tiles with many pieces each (the 33k-px 1x1 gradients: 4 tiles x ~128 pieces): 8 threads
+    // per output float4 (k_wsk_reduce_wide) instead of one serial chain of every piece
+    const long long pieces = cdiv((long long)pl.nw, std::max(1LL, pl.T / pl.KS));  // per (tile, tap)
+    if ((long long)rgrid.x * rgrid.y < 256 && pieces >= 16)
+      hipLaunchKernelGGL((k_wsk_reduce_wide<64, 64, 8>), dim3(cdiv((long long)64 * 64 / 4 * taps, 32), rgrid.y), rblock,
+                         0, st, a);
+    else
+      hipLaunchKernelGGL((k_wsk_reduce<64, 64>), rgrid, rblock, 0, st, a);
   } else {
     hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4, MS>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();

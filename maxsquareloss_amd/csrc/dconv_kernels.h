@@ -1810,6 +1810,67 @@ __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
     if (c < nn) dst[c * a.taps] = vals[c];
 }
 
+// k_wsk_reduce's generic form for tiles with many pieces and few tiles (the 33k-px 1x1 weight
+// gradients on 64x64 tiles: 4 tiles x ~128 pieces, 16 blocks of k_wsk_reduce, 27 us): S threads per
+// float4 output, thread s summing pieces w_lo + s, w_lo + s + S, ... in order, the S partial sums
+// then added in s order through LDS (deterministic; a different but fixed association).
+// grid = (ceil(BM*BN/4 * taps / (256/S)), tiles_m * tiles_n * nbranch); stream-K pieces only.
+template <int BM, int BN, int S>
+__global__ void __launch_bounds__(256) k_wsk_reduce_wide(WskArgs a) {
+  constexpr int PSZ = BM * BN, P4 = PSZ / 4, OPB = 256 / S;  // float4 outputs per block
+  __shared__ float4 red[256];
+  const int gsz = a.tiles_m * a.tiles_n;
+  const int br = blockIdx.y / gsz;
+  const int rem = blockIdx.y - br * gsz;
+  const int tn = rem / a.tiles_m, tm = rem - tn * a.tiles_m;
+  const int o = threadIdx.x / S, sl = threadIdx.x - o * S;
+  const int e = blockIdx.x * OPB + o;
+  const int tap = e / P4, g4 = e - tap * P4;
+  const bool live = tap < a.taps;
+  const int t = ((br * a.taps + (live ? tap : 0)) * a.tiles_n + tn) * a.tiles_m + tm;
+  const float4* __restrict__ part = reinterpret_cast<const float4*>(a.part);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    const int w_lo = sk_worker_of(t * a.KS, a.T, a.NW);
+    const int w_hi = sk_worker_of((t + 1) * a.KS - 1, a.T, a.NW);
+    for (int wc = w_lo + sl; wc <= w_hi; wc += S) {
+      const int slot = t - sk_start(wc, a.T, a.NW) / a.KS;
+      const float4 v = part[(long long)(wc * a.slots + slot) * P4 + g4];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (sl != 0 || !live) return;
+  float4 v = red[o * S];
+#pragma unroll
+  for (int q = 1; q < S; ++q) {
+    const float4 u = red[o * S + q];
+    v.x += u.x;
+    v.y += u.y;
+    v.z += u.z;
+    v.w += u.w;
+  }
+  const int m = tm * BM + (g4 * 4) / BN, n = tn * BN + (g4 * 4) % BN;
+  if (m >= a.M || n >= a.N) return;
+  float* dst = a.dw + br * a.cbranch + ((long long)m * a.N + n) * a.taps + tap;
+  float vals[4] = {v.x, v.y, v.z, v.w};
+  const int nn = min(4, a.N - n);
+  if (a.accumulate) {  // all old values loaded before the first store
+    float old[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) old[c] = c < nn ? dst[c * a.taps] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) vals[c] = old[c] + vals[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (c < nn) dst[c * a.taps] = vals[c];
+}
+
 // ---------------------------------------------------------------------------------------------
 // bf16x6 weight gradient, register-staged (the layer2-4 and ASPP-free x6 path).
 //
