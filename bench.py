@@ -58,8 +58,8 @@ def parse():
     ap.add_argument("--multi", default="False")
     ap.add_argument("--lambda-target", type=float, default=0.1)
     ap.add_argument("--num-classes", type=int, default=19)
-    ap.add_argument("--conv-math", default="fp32", choices=["fp32", "bf16"],
-                    help="bf16 = BASELINE config 5's fp16/bf16 MFMA path (fp32 accumulation)")
+    ap.add_argument("--conv-math", default="fp32", choices=["fp32", "fp16", "bf16"],
+                    help="fp16 / bf16 = BASELINE config 5's fp16 MFMA path (fp16: scaled fp16 operands; fp32 accumulation)")
     ap.add_argument("--bn-form", default="fused", choices=["fused", "split"],
                     help="BN kernels: one fused launch per call (default) or split statistics/apply launches")
     ap.add_argument("--f32-form", default=None, choices=["mfma_f32", "bf16x6", "f16x3"],
@@ -152,11 +152,11 @@ def main():
             traffic = json.load(open(a.pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    form = ops.f32_form() if a.conv_math == "fp32" else "bf16"
+    form = ops.f32_form() if a.conv_math == "fp32" else a.conv_math
     # the bound of the kernel's own arithmetic: FP32 MFMA, BF16 MFMA, or BF16 MFMA at six
     # products per fp32 product (the bf16x6 form): 2500 / 6 = 416.7 fp32-equivalent TFLOP/s
     # and FP16 MFMA (same rate) at three products per fp32 product (the f16x3 form): 833.3
-    peak = {"mfma_f32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
+    peak = {"mfma_f32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "fp16": BF16_MFMA_PEAK_TFLOPS,
             "bf16x6": round(BF16_MFMA_PEAK_TFLOPS / 6, 1), "f16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1)}[form]
     if traffic is not None and json.load(open(a.pmc)).get("form", "mfma_f32") != form:
         traffic = None  # the committed PMC figure belongs to another form of the kernel
@@ -200,7 +200,7 @@ def main():
     line = {
         "metric": METRIC, "value": round(images / elapsed, 3), "unit": "images/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if a.conv_math == "fp32" else "bf16 (conv MFMA), fp32",
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if a.conv_math == "fp32" else f"{a.conv_math} (conv MFMA), fp32",
         "data": "synthetic (counter-generated uint8 images -> BGR-mean, uniform labels; random-init weights)",
         "config": {"workload": f"{'SYNTHIA' if C == 16 else 'GTA5'}->Cityscapes {args.target_mode} UDA step "
                                f"(solve_gta5.py), {W}x{H}, bs=1/GPU",

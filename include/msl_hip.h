@@ -217,6 +217,34 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
                          int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * FP16-MFMA forms (BASELINE config 5's fp16 MFMA path): each operand tensor scaled by a power of
+ * two (its absolute maximum into [2^14, 2^15)) and rounded to fp16 once - the weights at pack
+ * time, as the hi planes of the f16x3 packs, so the packs must be made in the f16x3 fp32 form
+ * (msl_conv_set_f32_form(5), the default; MSL_ERR_ARG otherwise) - then one
+ * v_mfma_f32_32x32x16_f16 per 16-deep K slice with fp32 accumulation, the result unscaled
+ * exactly.  GEMMs with M <= 64 (64- / 32-row tiles) run exact f32 MFMA.  Operand partials as in
+ * the _sc entry points ((pointer, count), NULL = computed); msl_pconv_dgrad_f16 carries the
+ * accumulate flag of msl_pconv_dgrad_acc.  Same workspaces and results layout.
+ * ---------------------------------------------------------------------- */
+int msl_dconv_fwd_f16(const float* x, const float* packed, const float* bias, float* y, int nbranch, int cin,
+                      int cout, int h, int w, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                      msl_stream_t stream, const float* x_part, int x_npart);
+int msl_dconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin, int cout,
+                        int h, int w, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                        msl_stream_t stream, const float* dy_part, int dy_npart);
+int msl_dconv_wgrad_f16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin, int cout,
+                        int h, int w, int dil0, int dil1, int accumulate, void* ws, size_t ws_bytes,
+                        msl_stream_t stream, const float* x_part, int x_npart, const float* dy_part, int dy_npart);
+int msl_pconv_fwd_f16(const float* x, const float* packed, float* y, int cin, int cout, int p, int* counters,
+                      void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart);
+int msl_pconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                        int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                        const float* dy_part, int dy_npart);
+int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int cout, int p, int accumulate,
+                        void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
+                        const float* dy_part, int dy_npart);
+
+/* ------------------------------------------------------------------------
  * Bilinear upsample, align_corners=True (F.interpolate at deeplab_multi.py:124,
  * :128).  The forward reproduces torch-CPU's rounding bit for bit.
  * ---------------------------------------------------------------------- */

@@ -392,7 +392,7 @@ static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials 
 // The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
 template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
-  if constexpr (MT == kMathH3P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
+  if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
     if (accum)
       hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true>), grid, block, 0, st, a, sk);
     else
@@ -415,9 +415,11 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   // The x6 form runs one K-step per stage, three stages deep (scripts/tune_dconv.hip x6, layer3:
   // 87 us vs 115 with two K-steps per stage; f32 is indifferent); its 64- and 32-row tiles stay
   // on exact f32 MFMA (no gain measured there).
-  constexpr bool X6L = MT == kMathX6 || MT == kMathH3P;  // split forms: 128-row tiles only
+  // split forms (and the fp16 math, which reads the f16x3 packs' hi planes): 128-row tiles only
+  constexpr bool F16 = MT == kMathH3P || MT == kMathH1P;
+  constexpr bool X6L = MT == kMathX6 || F16;
   constexpr int MS = X6L ? kMathF32 : MT;
-  constexpr int MB = MT == kMathH3P ? kMathX6 : MT;       // (not reached by the split forms)
+  constexpr int MB = F16 ? kMathX6 : MT;       // (not reached by the split forms)
   if (X6L && pl.sk && pl.bm == 128) {
     pl.G = 1;
     pl.bk = kCB;
@@ -478,8 +480,8 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
       // the fp32 part of the same buffer (M > 64 <=> 128-row tiles)
       const long long f32 = (long long)pl.ksteps * kCB * a.lda;
       a.Ax6 = reinterpret_cast<const __bf16*>(packed + f32);
-      if constexpr (MT == kMathH3P) {
-        // f16x3: the image's absmax partials, then the GEMM with the pack's {sA, 1/sA}
+      if constexpr (F16) {
+        // f16x3 / fp16: the image's absmax partials, then the GEMM with the pack's {sA, 1/sA}
         if (img_part) {  // the caller's partials of this image (msl_absmax_partials, a BN kernel)
           a.bpart = img_part;
           a.bnpart = img_npart;
@@ -495,9 +497,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // wave and K-step instead of 8 dword ones): 1-4 us per call on the wide 1x1 GEMMs
         // (profiles/r02_f16x3_pw_dma.txt)
         if (taps == 1 && dil0 == 0)
-          launch_sk<128, 1, 4, 2, 2, kMathH3P, true>(accum, grid, block, st, a, sk);
+          launch_sk<128, 1, 4, 2, 2, MT, true>(accum, grid, block, st, a, sk);
         else
-          launch_sk<128, 1, 4, 2, 2, kMathH3P>(accum, grid, block, st, a, sk);
+          launch_sk<128, 1, 4, 2, 2, MT>(accum, grid, block, st, a, sk);
       } else {
         launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
       }
@@ -632,9 +634,10 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
                         const float* x_part = nullptr, int x_npart = 0, const float* dy_part = nullptr,
                         int dy_npart = 0) {
   const int P = h * w;
-  constexpr bool X6L = MT == kMathX6 || MT == kMathH3P;
+  constexpr bool F16 = MT == kMathH3P || MT == kMathH1P;
+  constexpr bool X6L = MT == kMathX6 || F16;
   constexpr int MS = X6L ? kMathF32 : MT;  // the split forms only on 128x128 tiles (plan_wgrad)
-  constexpr int MB = MT == kMathH3P ? kMathX6 : MT;  // k_wgrad_sk has no f16x3 form: x6 there
+  constexpr int MB = F16 ? kMathX6 : MT;   // k_wgrad_sk has no f16 form: x6 there
   if (ws_bytes < wgrad_ws_bytes(nbranch, taps, cin, cout, P, w)) return MSL_ERR_WORKSPACE;
   WgradPlan pl = plan_wgrad(nbranch, taps, cin, cout, P, X6L, w);
   bool trans = false;
@@ -688,7 +691,7 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   if (pl.rx6) {
     bf16x8* planes = reinterpret_cast<bf16x8*>((char*)ws + wgrad_piece_bytes(pl));
     a.dyx6 = planes;
-    if constexpr (MT == kMathH3P) {  // both operands' absmax partials, then the scaled split
+    if constexpr (F16) {  // both operands' absmax partials, then the scaled split
       const float* ap = dy_part;
       const float* bp = x_part;
       int an = dy_npart, bn = x_npart;
@@ -710,10 +713,10 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
       a.bpart = bp;
       a.anpart = an;
       a.bnpart = bn;
-      hipLaunchKernelGGL(k_split_rows<kMathH3P>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
+      hipLaunchKernelGGL(k_split_rows<MT>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, ap, an);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_wgrad_x6<kMathH3P>, grid, block, 0, st, a);
+      hipLaunchKernelGGL(k_wgrad_x6<MT>, grid, block, 0, st, a);
     } else {
       hipLaunchKernelGGL(k_split_rows<kMathX6>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, (const float*)nullptr, 0);
@@ -1075,6 +1078,71 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
   return launch_wgrad<kMathBf16>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
                       as_stream(stream));
+}
+
+// ------------------------------------------------------------------ FP16-MFMA forms
+// BASELINE config 5's fp16 MFMA path on the f16x3 machinery: each operand tensor scaled by its
+// power of two and rounded to fp16 once (the weights at pack time: the f16x3 packs' hi planes,
+// so packs must be made in the f16x3 fp32 form, the default), one v_mfma_f32_32x32x16_f16 per
+// 16-deep slice, fp32 sums, the result unscaled exactly.  The 64- / 32-row tiles (M <= 64) run
+// exact f32 MFMA.  Partials as in the _sc entry points ((pointer, count), NULL = computed).
+static bool f16_ready() { return g_f32_form == kMathH3P; }
+
+int msl_dconv_fwd_f16(const float* x, const float* packed, const float* bias, float* y, int nbranch, int cin,
+                      int cout, int h, int w, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                      msl_stream_t stream, const float* x_part, int x_npart) {
+  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y ||
+      dil0 < 1 || (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1, counters,
+                                   ws, ws_bytes, as_stream(stream), 0, x_part, x_npart);
+}
+
+int msl_dconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin, int cout,
+                        int h, int w, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                        msl_stream_t stream, const float* dy_part, int dy_npart) {
+  if (!f16_ready() || bad_parts(dy_part, dy_npart) || bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad ||
+      !dx || dil0 < 1 || (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+                                   counters, ws, ws_bytes, as_stream(stream), 0, dy_part, dy_npart);
+}
+
+int msl_dconv_wgrad_f16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin, int cout,
+                        int h, int w, int dil0, int dil1, int accumulate, void* ws, size_t ws_bytes,
+                        msl_stream_t stream, const float* x_part, int x_npart, const float* dy_part, int dy_npart) {
+  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart) ||
+      bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 || (nbranch == 2 && dil1 < 1))
+    return MSL_ERR_ARG;
+  return launch_wgrad<kMathH1P>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws, ws_bytes,
+                                as_stream(stream), x_part, x_npart, dy_part, dy_npart);
+}
+
+int msl_pconv_fwd_f16(const float* x, const float* packed, float* y, int cin, int cout, int p, int* counters,
+                      void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart) {
+  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_dims(1, cin, cout, 1, p) || !x || !packed || !y)
+    return MSL_ERR_ARG;
+  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+                                   as_stream(stream), 0, x_part, x_npart);
+}
+
+int msl_pconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                        int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                        const float* dy_part, int dy_npart) {
+  if (!f16_ready() || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx)
+    return MSL_ERR_ARG;
+  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws,
+                                   ws_bytes, as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart);
+}
+
+int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int cout, int p, int accumulate,
+                        void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
+                        const float* dy_part, int dy_npart) {
+  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) ||
+      !x || !dy || !dw)
+    return MSL_ERR_ARG;
+  return launch_wgrad<kMathH1P>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+                                as_stream(stream), x_part, x_npart, dy_part, dy_npart);
 }
 
 }  // extern "C"

@@ -183,6 +183,10 @@ __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x
 // ~1e-7 would otherwise lose the lo term to subnormals).  Half the MFMAs of x6 per 16-deep slice.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr int kMathH3P = 5;
+// kMathH1P: the fp16 conv math (BASELINE config 5's fp16 MFMA path): the f16x3 operands' hi terms
+// only - each operand tensor scaled by its power of two and rounded to fp16 once, one
+// v_mfma_f32_32x32x16_f16 per 16-deep slice, fp32 sums, the result unscaled exactly.
+constexpr int kMathH1P = 8;
 constexpr int kNPart = 256;  // absmax partials per operand tensor (k_absmax blocks)
 
 struct Split2h {
@@ -450,6 +454,33 @@ __device__ __forceinline__ void mfma_stage_h3p(const float* __restrict__ As, con
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int t = 0; t < TN; ++t) acc[i][t] = mfma_h3(av[i], bv[t], acc[i][t]);
+    if (kk == 0) mid();
+  }
+}
+
+// fp16 stage: A fragments from the pack's hi plane (G K-steps of [half][BM][8] fp16, 8*BM floats
+// each), B fragments scaled by sB and rounded to fp16 as they are read.
+template <int G, int TM, int TN, int BM, int LDB_S, typename F>
+__device__ __forceinline__ void mfma_stage_h1p(const float* __restrict__ As, const float* __restrict__ Bs,
+                                               int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid,
+                                               float sB) {
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int kk = 0; kk < G; ++kk) {
+    const f16x8* Ab = reinterpret_cast<const f16x8*>(As + kk * 8 * BM);
+    f16x8 av[TM], bv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kr = kk * 16 + 8 * h + j;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) bv[t][j] = (_Float16)(Bs[kr * LDB_S + wn + t * 32 + l32] * sB);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bv[t], acc[i][t], 0, 0, 0);
     if (kk == 0) mid();
   }
 }
@@ -862,16 +893,18 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   static_assert(BN % 64 == 0 && BM % 32 == 0, "tiles");
-  constexpr bool H3 = MT == kMathH3P;                                 // f16x3: two fp16 planes
+  constexpr bool H1 = MT == kMathH1P;                                 // fp16: the hi plane only
+  constexpr bool H3 = MT == kMathH3P || H1;                           // f16x3: two fp16 planes
   constexpr bool APRE = MT == kMathX6P || MT == kMathX6PP || H3;  // A from pre-split planes
   constexpr bool BPRE = MT == kMathX6PP;                            // B from pre-split bf16 planes
-  constexpr int NQ = H3 ? 4 : 6;  // (plane, k half) blocks of one pre-split K-step
+  constexpr int NQ = H3 ? 4 : 6;  // (plane, k half) blocks of one pre-split K-step in the pack
+  constexpr int NQL = H1 ? 2 : NQ;  // of them staged (fp16 math: plane 0's two halves)
   static_assert(!APRE || BM % 64 == 0, "pre-split A: 64-row DMA pieces");
   static_assert(!BPRE || (!PW && BN % 64 == 0), "pre-split B: 64-pixel DMA pieces");
-  constexpr int A_STAGE = APRE ? G * 4 * NQ * BM : BK * BM;
+  constexpr int A_STAGE = APRE ? G * 4 * NQL * BM : BK * BM;
   constexpr int STAGE = A_STAGE + (BPRE ? G * 24 * BN : BK * BN);
   constexpr int A_ROWS_PER_INST = 256 / BM;
-  constexpr int A_INST = APRE ? G * NQ * (BM / 64) : BK / A_ROWS_PER_INST;
+  constexpr int A_INST = APRE ? G * NQL * (BM / 64) : BK / A_ROWS_PER_INST;
   constexpr int A_INST_W = A_INST / 4;
   constexpr int NH = BN / 64;
 #ifdef MSL_SK_FAKEX4
@@ -992,7 +1025,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
 #pragma unroll
         for (int i = 0; i < A_INST_W; ++i) {
           const int inst = wid * A_INST_W + i;
-          const int g = inst / (NQ * (BM / 64)), r = inst % (NQ * (BM / 64));
+          const int g = inst / (NQL * (BM / 64)), r = inst % (NQL * (BM / 64));
           const int qh = r / (BM / 64), mb = (r % (BM / 64)) * 64;
           const int ks = s * G + g;
           dma_b128(rx, As + inst * 256, (unsigned)(((ks * NQ + qh) * a.lda + m0 + mb + lane) * 16));
@@ -1098,6 +1131,8 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         mfma_stage_x6p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (MT == kMathX6PP)
         mfma_stage_x6pp<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
+      else if constexpr (H1)
+        mfma_stage_h1p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid, sB);
       else if constexpr (H3)
         mfma_stage_h3p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid, sB);
       else
@@ -1906,14 +1941,15 @@ __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ sr
                                                      bf16x8* __restrict__ planes, const float* __restrict__ part,
                                                      int npart) {
   constexpr int R = 64, LDP = 72;  // rows per block, LDS row stride in 16-bit terms (64 pixels + 8)
-  constexpr int NP = MT == kMathH3P ? 2 : 3;
+  constexpr bool F16 = MT == kMathH3P || MT == kMathH1P;
+  constexpr int NP = MT == kMathH1P ? 1 : F16 ? 2 : 3;
   __shared__ __attribute__((aligned(16))) unsigned short tile[NP * R * LDP];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int m0 = blockIdx.x * R, ks0 = blockIdx.y * 4;
   const int p = ks0 * kWx6BK + lane;
   const bool pin = p < P;
   float sc = 1.f, inv;
-  if constexpr (MT == kMathH3P) sc = pow2_scale(partials_max(part, npart, lane), inv);
+  if constexpr (F16) sc = pow2_scale(partials_max(part, npart, lane), inv);
   float v[R / 4];
 #pragma unroll
   for (int i = 0; i < R / 4; ++i) {
@@ -1923,12 +1959,14 @@ __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ sr
 #pragma unroll
   for (int i = 0; i < R / 4; ++i) {
     const int r = wv + 4 * i;
-    if constexpr (MT == kMathH3P) {
+    if constexpr (MT == kMathH1P) {
+      tile[r * LDP + lane] = __builtin_bit_cast(unsigned short, (_Float16)(v[i] * sc));
+    } else if constexpr (MT == kMathH3P) {
       const float x = v[i] * sc;
       const _Float16 h = (_Float16)x;
       const _Float16 l = (_Float16)(x - (float)h);
       tile[(0 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, h);
-      tile[(1 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, l);
+      tile[((NP - 1) * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, l);
     } else {
       const __bf16 h = (__bf16)v[i];
       const float rem = v[i] - (float)h;
@@ -1956,8 +1994,9 @@ __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ sr
 // pieces are unscaled by both before they are stored.
 template <int MT = kMathX6>
 __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
-  constexpr bool H3 = MT == kMathH3P;
-  constexpr int NP = H3 ? 2 : 3;      // planes per operand
+  constexpr bool H1 = MT == kMathH1P;  // fp16 math: the hi planes only
+  constexpr bool H3 = MT == kMathH3P || H1;
+  constexpr int NP = H1 ? 1 : H3 ? 2 : 3;  // planes per operand
   constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
   constexpr int RB = 128 * 16 + 32;   // bytes per (plane, k half) block of 128 rows, padded
   constexpr int KVB = 2 * NP * RB;    // one K-step's B planes
@@ -2061,7 +2100,16 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
     };
     auto storeB = [&](int buf) {  // split once, NP 8-B plane quarters per chunk
       char* base = smem + buf * STAGEB + wofs;
-      if constexpr (H3) {
+      if constexpr (H1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f16x4 hi;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hi[j] = (_Float16)(rbv[4 * i + j] * sX);
+          *reinterpret_cast<f16x4*>(base + i * 32 * 16) = hi;
+        }
+        return;
+      } else if constexpr (H3) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           f16x4 hi, lo;
@@ -2108,7 +2156,21 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
                                                            (int)((unsigned)(ks * 2 * NP + 2 * q) * a_plane_bytes), 0);
     };
     auto compute = [&](const char* Bs, const u32x4 (&A)[TM][NP]) {
-      if constexpr (H3) {
+      if constexpr (H1) {
+        f16x8 bv[TN];
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj)
+          bv[jj] = *reinterpret_cast<const f16x8*>(Bs + kh * RB + (wn + jj * 32 + l32) * 16);
+#pragma unroll
+        for (int ii = 0; ii < TM; ++ii) {
+          union { u32x4 u; f16x8 h; } c0;
+          c0.u = A[ii][0];
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj)
+            acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(c0.h, bv[jj], acc[ii][jj], 0, 0, 0);
+        }
+        return;
+      } else if constexpr (H3) {
         Split2h bv[TN];
 #pragma unroll
         for (int jj = 0; jj < TN; ++jj) {
@@ -2119,7 +2181,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
         for (int ii = 0; ii < TM; ++ii) {
           union { u32x4 u; f16x8 h; } c0, c1;
-          c0.u = A[ii][0]; c1.u = A[ii][1];
+          c0.u = A[ii][0]; c1.u = A[ii][NP - 1];
           Split2h av;
           av.hi = c0.h; av.lo = c1.h;
 #pragma unroll
@@ -2138,7 +2200,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) {
         union { u32x4 u; bf16x8 h; } c0, c1, c2;
-        c0.u = A[ii][0]; c1.u = A[ii][1]; c2.u = A[ii][NP - 1];
+        c0.u = A[ii][0]; c1.u = A[ii][NP > 1 ? 1 : 0]; c2.u = A[ii][NP - 1];
         Split3 av;
         av.hi = c0.h; av.mid = c1.h; av.lo = c2.h;
 #pragma unroll

@@ -51,6 +51,12 @@ SIGNATURES = {
     "msl_pconv_fwd_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_dgrad_acc_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_wgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_dconv_fwd_f16": (c_int, [c_p] * 4 + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_dconv_dgrad_f16": (c_int, [c_p] * 3 + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_dconv_wgrad_f16": (c_int, [c_p] * 4 + [c_int] * 8 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_pconv_fwd_f16": (c_int, [c_p] * 3 + [c_int] * 3 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_pconv_dgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_pconv_wgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
     "msl_dconv_fwd_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_wgrad_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p]),

@@ -13,16 +13,18 @@ from . import hip
 
 _f32 = torch.float32
 
-# Conv MFMA precision: "fp32" (v_mfma_f32_32x32x2_f32, the reference's arithmetic) or "bf16"
-# (v_mfma_f32_32x32x16_bf16 on operands rounded to bf16, fp32 sums: BASELINE config 5's
-# fp16/bf16 MFMA path).  Activations, BN, losses and the optimizer stay fp32 either way.
+# Conv MFMA precision: "fp32" (fp32-accurate, in the library's fp32 form below), "fp16"
+# (v_mfma_f32_32x32x16_f16 on operands scaled by a power of two and rounded to fp16, fp32 sums:
+# BASELINE config 5's fp16 MFMA path; needs the f16x3 fp32 form's packs) or "bf16"
+# (v_mfma_f32_32x32x16_bf16 on operands rounded to bf16, fp32 sums).  Activations, BN, losses
+# and the optimizer stay fp32 in every case.
 CONV_MATH = "fp32"
 
 
 def set_conv_math(math):
     global CONV_MATH
-    if math not in ("fp32", "bf16"):
-        raise ValueError(f"conv math must be 'fp32' or 'bf16', got {math!r}")
+    if math not in ("fp32", "fp16", "bf16"):
+        raise ValueError(f"conv math must be 'fp32', 'fp16' or 'bf16', got {math!r}")
     CONV_MATH = math
 
 
@@ -73,7 +75,8 @@ def _fn(lib, name, math):
 
 
 def _h3(math="fp32"):
-    return math == "fp32" and _form_code() == F32_FORMS["f16x3"]
+    """Whether the conv GEMMs of this math scale their operands (and so read absmax partials)."""
+    return math == "fp16" or (math == "fp32" and _form_code() == F32_FORMS["f16x3"])
 
 
 def _tag_absmax(t, part):
@@ -112,7 +115,8 @@ def _conv_call(lib, name, math, args, parts):
     itself; ignored outside f16x3); bf16: the _bf16 entry point."""
     if math == "bf16":
         return getattr(lib, name + "_bf16")(*args)
-    return getattr(lib, name + "_sc")(*args, *(v for q in parts for v in _pp(q)))
+    suffix = "_f16" if math == "fp16" else "_sc"
+    return getattr(lib, name + suffix)(*args, *(v for q in parts for v in _pp(q)))
 
 
 def _split_gemm(m, k_other):
@@ -438,6 +442,10 @@ class _PConv(Function):
                 hip.check(lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
                                                    hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s),
                           "msl_pconv_dgrad")
+            elif math == "fp16":
+                hip.check(lib.msl_pconv_dgrad_f16(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
+                                                  0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s,
+                                                  *_pp(gpart)), "msl_pconv_dgrad")
             else:
                 hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
                                                      0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s,

@@ -233,9 +233,10 @@ def add_train_args(arg_parser):
     a("--multi", default=True, type=str2bool)
     a("--lambda_seg", type=float, default=0.1)
     a("--synthetic_images", type=int, default=4, help="synthetic items per domain (no datasets offline)")
-    a("--conv_math", default="fp32", choices=["fp32", "bf16"],
-      help="conv MFMA precision (not in the reference, which is fp32): bf16 = BASELINE config 5's "
-           "fp16/bf16 MFMA path (bf16 products, fp32 sums; BN, losses, SGD stay fp32)")
+    a("--conv_math", default="fp32", choices=["fp32", "fp16", "bf16"],
+      help="conv MFMA precision (not in the reference, which is fp32): fp16 = BASELINE config 5's "
+           "fp16 MFMA path (scaled fp16 operands, fp32 sums), bf16 = bf16 products, fp32 sums; BN, "
+           "losses, SGD stay fp32")
     a("--f32_form", default=None, choices=["mfma_f32", "bf16x6", "f16x3"],
       help="matrix-core form of the fp32 convs (default: the library's): mfma_f32 = "
            "v_mfma_f32_32x32x2_f32; bf16x6 = three-way bf16 split, six products, fp32-accurate")

@@ -393,6 +393,59 @@ def test_conv_bf16_math(kind, cin, cout, h, w, d):
     assert _rel(wg.grad, wr.grad) < 1e-5
 
 
+# ----------------------------------------------------------------------------- fp16 conv math
+def _f16(t):
+    """The operand as the fp16 kernels see it: scaled by its tensor's power of two (absmax into
+    [2^14, 2^15), dconv_kernels.h pow2_scale), rounded to fp16, unscaled - exact in fp64."""
+    e = torch.frexp(t.abs().max()).exponent.item()
+    sc = 2.0 ** (15 - e)
+    return (t * sc).half().double() / sc
+
+
+@pytest.mark.parametrize("kind,cin,cout,h,w,d", [
+    ("dconv", 256, 256, 17, 33, 2), ("dconv", 512, 512, 17, 33, 4), ("dconv", 64, 64, 33, 65, 1),
+    ("pconv", 256, 1024, 17, 33, 0), ("pconv", 1024, 256, 17, 33, 0)])
+def test_conv_fp16_math(kind, cin, cout, h, w, d):
+    """BASELINE config 5's fp16 MFMA path (msl_*_f16): products of fp16-rounded, per-tensor scaled
+    operands summed in fp32 on the 128-row tiles (M > 64; the weight gradient where both sides have
+    >= 128 channels), exact f32 MFMA below.  Reference: the same conv in fp64 on the operands as
+    the kernels see them, so the only admissible difference is the fp32 accumulation (1e-5 of
+    max|ref|, as the fp32 kernels); operand scales far from 1 (weights 1e-2, gradients 1e-6)."""
+    g = torch.Generator().manual_seed(cin + 13 * cout + d)
+    k = 1 if kind == "pconv" else 3
+    x = torch.relu(torch.randn(1, cin, h, w, generator=g))
+    wt = torch.randn(cout, cin, k, k, generator=g) * 0.01
+    gy = torch.randn(1, cout, h, w, generator=g) * 1e-6
+    ops.set_conv_math("fp16")
+    try:
+        xg = x.to(DEV).requires_grad_()
+        wg = wt.to(DEV).requires_grad_()
+        if kind == "dconv":
+            y = ops.dconv3x3(xg, wg, d, ops.PackCache())
+        else:
+            y = ops.pconv(xg, wg, ops.PackCache(pointwise=True))
+        y.backward(gy.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        ops.set_conv_math("fp32")
+    pad = 0 if kind == "pconv" else d
+    dil = 1 if kind == "pconv" else d
+    exact = lambda t: t.double()  # noqa: E731
+
+    def conv(xx, ww):
+        return F.conv2d(xx, ww, padding=pad, dilation=dil)
+
+    rf, rd, rw = (_f16 if cout > 64 else exact), (_f16 if cin > 64 else exact), \
+        (_f16 if min(cin, cout) >= 128 else exact)
+    assert _rel(y, conv(rf(x), rf(wt))) < 1e-5
+    xr = rd(x).requires_grad_()
+    conv(xr, rd(wt)).backward(rd(gy))
+    assert _rel(xg.grad, xr.grad) < 1e-5
+    wr = rw(wt).requires_grad_()
+    conv(rw(x), wr).backward(rw(gy))
+    assert _rel(wg.grad, wr.grad) < 1e-5
+
+
 # ----------------------------------------------------------------------------- weight packs
 @pytest.mark.parametrize("kind,nb,cin,cout,for_dgrad", [
     ("d", 1, 256, 256, 0), ("d", 1, 256, 256, 1), ("d", 2, 2048, 19, 0), ("d", 2, 2048, 19, 1),

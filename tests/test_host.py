@@ -323,9 +323,10 @@ def test_hot_kernels_keep_their_occupancy():
             info[kern][m.group(1)] = int(m.group(2))
     hot = [k for k in info if k.startswith("_ZN3msl14k_igemm_fwd_skILi128ELi128ELi1ELi4ELi2ELi2ELb0ELi3E")
            or k.startswith("_ZN3msl15k_igemm_fwd_sk2ILi128ELi128ELi1ELi4ELi2ELi2ELb0ELi5E")
+           or k.startswith("_ZN3msl15k_igemm_fwd_sk2ILi128ELi128ELi1ELi4ELi2ELi2ELb0ELi8E")
            or k.startswith("_ZN3msl10k_wgrad_x6")]
-    # the x6 and f16x3 forwards (plain, accumulating) and the x6 / f16x3 weight gradients
-    assert len(hot) == 6, sorted(info)
+    # the x6, f16x3 and fp16 forwards (plain, accumulating) and the three weight-gradient forms
+    assert len(hot) == 9, sorted(info)
     for k in hot:
         assert info[k]["Occupancy [waves/SIMD]"] >= 2, (k, info[k])
     for k, v in info.items():
