@@ -496,10 +496,13 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // pointwise: B rows are unshifted, so they move as dwordx4 (4 pixels per lane: 2 DMAs per
         // wave and K-step instead of 8 dword ones): 1-4 us per call on the wide 1x1 GEMMs
         // (profiles/r02_f16x3_pw_dma.txt)
+        // waves 1 x 4 (each 128 rows x 32 pixels): every wave splits only its own B columns
+        // (2 x 2 waves split each column twice); step 40.5 vs 40.9 ms on one box
+        // (profiles/r02_f16x3_waves.txt)
         if (taps == 1 && dil0 == 0)
-          launch_sk<128, 1, 4, 2, 2, MT, true>(accum, grid, block, st, a, sk);
+          launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk);
         else
-          launch_sk<128, 1, 4, 2, 2, MT>(accum, grid, block, st, a, sk);
+          launch_sk<128, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk);
       } else {
         launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
       }
