@@ -438,22 +438,38 @@ __device__ __forceinline__ void mfma_stage_h3p(const float* __restrict__ As, con
   for (int kk = 0; kk < G; ++kk) {
     const f16x8* Ab = reinterpret_cast<const f16x8*>(As + kk * 16 * BM);
     Split2h av[TM], bv[TN];
+    float braw[TN][8];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = wm + i * 32 + l32;
-      av[i].hi = Ab[h * BM + m];
-      av[i].lo = Ab[(2 + h) * BM + m];
-    }
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kr = kk * 16 + 8 * h + j;
+      for (int t = 0; t < TN; ++t) braw[t][j] = Bs[(kk * 16 + 8 * h + j) * LDB_S + wn + t * 32 + l32];
 #pragma unroll
-      for (int t = 0; t < TN; ++t) split2h_set(bv[t], j, Bs[kr * LDB_S + wn + t * 32 + l32] * sB);
-    }
+    for (int i = 0; i < TM; ++i) av[i].lo = Ab[(2 + h) * BM + wm + i * 32 + l32];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
+    // every LDS read of the K-step issues before the B split's VALU work
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) split2h_set(bv[t], j, braw[t][j] * sB);
+    // product-major order: the TM*TN accumulators of one product are independent, so its MFMAs
+    // issue back to back, and every A fragment is in registers before the first one
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int t = 0; t < TN; ++t) acc[i][t] = mfma_h3(av[i], bv[t], acc[i][t]);
+      for (int t = 0; t < TN; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bv[t].hi, acc[i][t], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv[t].lo, acc[i][t], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv[t].hi, acc[i][t], 0, 0, 0);
     if (kk == 0) mid();
   }
 }
@@ -469,14 +485,18 @@ __device__ __forceinline__ void mfma_stage_h1p(const float* __restrict__ As, con
   for (int kk = 0; kk < G; ++kk) {
     const f16x8* Ab = reinterpret_cast<const f16x8*>(As + kk * 8 * BM);
     f16x8 av[TM], bv[TN];
+    float braw[TN][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) braw[t][j] = Bs[(kk * 16 + 8 * h + j) * LDB_S + wn + t * 32 + l32];
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
+    __builtin_amdgcn_sched_barrier(0);  // every LDS read of the K-step issues before the VALU work
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kr = kk * 16 + 8 * h + j;
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int t = 0; t < TN; ++t) bv[t][j] = (_Float16)(Bs[kr * LDB_S + wn + t * 32 + l32] * sB);
-    }
+      for (int t = 0; t < TN; ++t) bv[t][j] = (_Float16)(braw[t][j] * sB);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
