@@ -80,7 +80,7 @@ def main():
     argv = ["--crop_size", f"{a.width},{a.height}", "--target_crop_size", f"{a.width},{a.height}",
             "--imagenet_pretrained", "False", "--save_dir", "", "--num_classes", str(a.num_classes),
             "--target_mode", a.target_mode, "--multi", a.multi, "--lambda_target", str(a.lambda_target),
-            "--iter_max", "200000", "--conv_math", a.conv_math, "--graph", str(bool(a.graph and world == 1))]
+            "--iter_max", "200000", "--conv_math", a.conv_math, "--graph", str(bool(a.graph))]
     if a.f32_form:
         argv += ["--f32_form", a.f32_form]
     args, _, _ = init_args(build_parser().parse_args(argv))

@@ -161,6 +161,32 @@ int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cou
                     int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * The stem and the strided glue of ResNetMulti (csrc/stem.hip), all gather forms without atomics
+ * (bit-reproducible).  Replaces the last library kernels of the training step:
+ *   - conv1 7x7 / stride 2 / pad 3 (deeplab_multi.py:73-74, 114) = msl_im2col into a
+ *     [c*kh*kw][ho*wo] column matrix + msl_pconv_fwd with the [cout][c*kh*kw] weight (the conv
+ *     weight as laid out); its weight gradient msl_pconv_wgrad on the same columns; its data
+ *     gradient msl_pconv_dgrad into columns + msl_col2im (sums the columns back, i-major, j-minor);
+ *   - MaxPool2d(3, 2, 1, ceil_mode=True) (deeplab_multi.py:77, 114): window [o*s - pad, +k) clipped
+ *     to the image, first max in row-major scan (a NaN replaces), idx = y*w + x of the max; the
+ *     caller passes ho/wo (torch's ceil-mode output size); the backward sums dy over the windows
+ *     whose idx is the pixel, in (oy, ox) order (torch-CPU's order: bit-exact);
+ *   - x[:, :, ::s, ::s] (the stride of layer2.0's 1x1 conv1 and downsample, deeplab_multi.py:12-13,
+ *     96-99) and its transpose (zeros elsewhere) for the gradient.
+ * ---------------------------------------------------------------------- */
+int msl_im2col(const float* x, int c, int h, int w, int kh, int kw, int stride, int pad, int dil, int ho, int wo,
+               float* col, msl_stream_t stream);
+int msl_col2im(const float* col, int c, int h, int w, int kh, int kw, int stride, int pad, int dil, int ho, int wo,
+               float* x, msl_stream_t stream);
+int msl_maxpool_fwd(const float* x, int c, int h, int w, int k, int stride, int pad, int ho, int wo, float* y,
+                    int32_t* idx, msl_stream_t stream);
+int msl_maxpool_bwd(const float* dy, const int32_t* idx, int c, int h, int w, int k, int stride, int pad, int ho,
+                    int wo, float* dx, msl_stream_t stream);
+int msl_subsample(const float* x, int c, int h, int w, int stride, int ho, int wo, float* y, msl_stream_t stream);
+int msl_subsample_bwd(const float* dy, int c, int h, int w, int stride, int ho, int wo, float* dx,
+                      msl_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * Operand scales of the f16x3 form (msl_conv_set_f32_form(5)).  Each GEMM operand tensor is
  * scaled by a power of two derived from its absolute maximum, which msl_absmax_partials reduces
  * into msl_absmax_parts() floats.  The plain fp32 entry points compute the partials of their

@@ -1,0 +1,238 @@
+// The stem and the strided glue of ResNetMulti on HIP, so the
+// training step runs no library kernel and is bit-reproducible run to run:
+//   - conv1 7x7 / stride 2 / pad 3 (deeplab_multi.py:73-74, 114): im2col into a [cin*49][P] column
+//     matrix, then the pointwise GEMM kernels of dconv.hip (the 7x7 weight [64][3][7][7] is a
+//     [64][147] pointwise weight as laid out); data gradient = pointwise dgrad + col2im (gather);
+//   - maxpool 3x3 / stride 2 / pad 1 / ceil_mode (deeplab_multi.py:77, 114): first-max (NaN wins)
+//     window scan in torch-CPU's order, the argmax index kept; backward as a gather over the
+//     windows covering each input pixel, summed in torch-CPU's scatter order (bit-exact);
+//   - x[:, :, ::s, ::s] for layer2.0's stride-2 1x1 conv1 and downsample (deeplab_multi.py:12-13,
+//     96-99: Caffe-style, the stride sits on the 1x1 convs), and its transpose for the gradient.
+// Every kernel is a plain gather: one thread per output element, no atomics, no float reordering.
+#include "msl_internal.h"
+
+namespace msl {
+
+// col[(c*KH + i)*KW + j][oy*WO + ox] = x[c][oy*S - PAD + i*D][ox*S - PAD + j*D] (0 outside the image).
+// Thread per (row k, output row oy, 4 output columns): the 4 stores are one float4 when WO % 4 == 0.
+__global__ void __launch_bounds__(256) k_im2col(const float* __restrict__ x, int H, int W, int KH, int KW, int S,
+                                                int PAD, int D, int HO, int WO, int K, float* __restrict__ col) {
+  const int wq = (WO + 3) >> 2;
+  const long long total = (long long)K * HO * wq;
+  const long long P = (long long)HO * WO;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int q = (int)(e % wq);
+    const long long r = e / wq;
+    const int oy = (int)(r % HO);
+    const int k = (int)(r / HO);
+    const int j = k % KW, i = (k / KW) % KH, c = k / (KW * KH);
+    const int iy = oy * S - PAD + i * D;
+    const bool rowok = (unsigned)iy < (unsigned)H;
+    const float* src = x + ((long long)c * H + (rowok ? iy : 0)) * W;
+    float v[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ox = q * 4 + t;
+      const int ix = ox * S - PAD + j * D;
+      v[t] = (rowok && ox < WO && (unsigned)ix < (unsigned)W) ? src[ix] : 0.f;
+    }
+    float* dst = col + (long long)k * P + (long long)oy * WO + q * 4;
+    if ((WO & 3) == 0) {
+      *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      for (int t = 0; t < 4 && q * 4 + t < WO; ++t) dst[t] = v[t];
+    }
+  }
+}
+
+// x[c][y][xx] = sum over (i, j) (i-major) of col[(c*KH + i)*KW + j][oy][ox] for every window
+// position that maps (oy, ox) onto (y, xx).
+__global__ void __launch_bounds__(256) k_col2im(const float* __restrict__ col, int C, int H, int W, int KH, int KW,
+                                                int S, int PAD, int D, int HO, int WO, float* __restrict__ x) {
+  const long long total = (long long)C * H * W;
+  const long long P = (long long)HO * WO;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int xx = (int)(e % W);
+    const long long r = e / W;
+    const int y = (int)(r % H);
+    const int c = (int)(r / H);
+    float s = 0.f;
+    for (int i = 0; i < KH; ++i) {
+      const int ty = y + PAD - i * D;
+      if (ty < 0 || ty % S) continue;
+      const int oy = ty / S;
+      if (oy >= HO) continue;
+      for (int j = 0; j < KW; ++j) {
+        const int tx = xx + PAD - j * D;
+        if (tx < 0 || tx % S) continue;
+        const int ox = tx / S;
+        if (ox >= WO) continue;
+        s += col[((long long)(c * KH + i) * KW + j) * P + (long long)oy * WO + ox];
+      }
+    }
+    x[e] = s;
+  }
+}
+
+// torch-CPU max_pool2d (aten/native/cpu/MaxPoolKernel.cpp): window [oy*S - PAD, +K) clipped to the
+// image, scanned row-major, `val > max || isnan(val)` replaces, max starts at -inf with the index
+// of the window's first element.  idx = y*W + x within the channel.
+__global__ void __launch_bounds__(256) k_maxpool_fwd(const float* __restrict__ x, int H, int W, int K, int S, int PAD,
+                                                     int HO, int WO, long long total, float* __restrict__ y,
+                                                     int32_t* __restrict__ idx) {
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int ox = (int)(e % WO);
+    const long long r = e / WO;
+    const int oy = (int)(r % HO);
+    const long long c = r / HO;
+    int y0 = oy * S - PAD, x0 = ox * S - PAD;
+    const int y1 = min(y0 + K, H), x1 = min(x0 + K, W);
+    y0 = max(y0, 0);
+    x0 = max(x0, 0);
+    const float* src = x + c * H * W;
+    float best = -INFINITY;
+    int bi = y0 * W + x0;
+    for (int yy = y0; yy < y1; ++yy)
+      for (int xx = x0; xx < x1; ++xx) {
+        const float v = src[yy * W + xx];
+        if (v > best || v != v) {
+          best = v;
+          bi = yy * W + xx;
+        }
+      }
+    y[e] = best;
+    idx[e] = bi;
+  }
+}
+
+// dx[c][y][x] = sum of dy over the windows whose argmax is (y, x), in output scan order (oy, then
+// ox, ascending) - the order torch-CPU's backward adds them in (bit-exact).
+__global__ void __launch_bounds__(256) k_maxpool_bwd(const float* __restrict__ dy, const int32_t* __restrict__ idx,
+                                                     int H, int W, int K, int S, int PAD, int HO, int WO,
+                                                     long long total, float* __restrict__ dx) {
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int xx = (int)(e % W);
+    const long long r = e / W;
+    const int y = (int)(r % H);
+    const long long c = r / H;
+    const int me = y * W + xx;
+    // windows covering y: oy*S - PAD <= y <= oy*S - PAD + K - 1
+    const int ly = y + PAD - (K - 1), lx = xx + PAD - (K - 1);
+    const int oy0 = ly <= 0 ? 0 : (ly + S - 1) / S, oy1 = min((y + PAD) / S, HO - 1);
+    const int ox0 = lx <= 0 ? 0 : (lx + S - 1) / S, ox1 = min((xx + PAD) / S, WO - 1);
+    const long long base = c * HO * WO;
+    float s = 0.f;
+    for (int oy = oy0; oy <= oy1; ++oy)
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const long long o = base + (long long)oy * WO + ox;
+        if (idx[o] == me) s += dy[o];
+      }
+    dx[e] = s;
+  }
+}
+
+// y[c][oy][ox] = x[c][oy*S][ox*S]   (fwd)      x[c][y][xx] = (y % S || xx % S) ? 0 : y'[..]  (bwd)
+__global__ void __launch_bounds__(256) k_subsample(const float* __restrict__ x, int H, int W, int S, int HO, int WO,
+                                                   long long total, float* __restrict__ y) {
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int ox = (int)(e % WO);
+    const long long r = e / WO;
+    const int oy = (int)(r % HO);
+    const long long c = r / HO;
+    y[e] = x[(c * H + (long long)oy * S) * W + (long long)ox * S];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_subsample_bwd(const float* __restrict__ dy, int H, int W, int S, int HO,
+                                                       int WO, long long total, float* __restrict__ dx) {
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int xx = (int)(e % W);
+    const long long r = e / W;
+    const int y = (int)(r % H);
+    const long long c = r / H;
+    float v = 0.f;
+    if (y % S == 0 && xx % S == 0 && y / S < HO && xx / S < WO) v = dy[(c * HO + y / S) * WO + xx / S];
+    dx[e] = v;
+  }
+}
+
+static unsigned grid_for(long long n) { return (unsigned)std::min<long long>((n + 255) / 256, 16384); }
+
+static bool bad_geom(int c, int h, int w, int k, int s, int pad, int ho, int wo) {
+  return c < 1 || h < 1 || w < 1 || k < 1 || s < 1 || pad < 0 || ho < 1 || wo < 1 ||
+         (long long)c * h * w >= (1LL << 40) || (long long)h * w >= (1LL << 31);
+}
+
+}  // namespace msl
+
+using namespace msl;
+
+extern "C" {
+
+int msl_im2col(const float* x, int c, int h, int w, int kh, int kw, int stride, int pad, int dil, int ho, int wo,
+               float* col, msl_stream_t stream) {
+  if (!x || !col || bad_geom(c, h, w, std::max(kh, kw), stride, pad, ho, wo) || kh < 1 || kw < 1 || dil < 1 ||
+      (long long)c * kh * kw * ho * wo >= (1LL << 40))
+    return MSL_ERR_ARG;
+  const int K = c * kh * kw;
+  const long long n = (long long)K * ho * ((wo + 3) / 4);
+  hipLaunchKernelGGL(k_im2col, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, kh, kw, stride, pad, dil,
+                     ho, wo, K, col);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+int msl_col2im(const float* col, int c, int h, int w, int kh, int kw, int stride, int pad, int dil, int ho, int wo,
+               float* x, msl_stream_t stream) {
+  if (!x || !col || bad_geom(c, h, w, std::max(kh, kw), stride, pad, ho, wo) || kh < 1 || kw < 1 || dil < 1)
+    return MSL_ERR_ARG;
+  const long long n = (long long)c * h * w;
+  hipLaunchKernelGGL(k_col2im, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), col, c, h, w, kh, kw, stride, pad,
+                     dil, ho, wo, x);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+int msl_maxpool_fwd(const float* x, int c, int h, int w, int k, int stride, int pad, int ho, int wo, float* y,
+                    int32_t* idx, msl_stream_t stream) {
+  if (!x || !y || !idx || bad_geom(c, h, w, k, stride, pad, ho, wo) || 2 * pad > k) return MSL_ERR_ARG;
+  // every window must start inside the image (torch: the last window starts before h + pad)
+  if ((long long)(ho - 1) * stride - pad >= h || (long long)(wo - 1) * stride - pad >= w) return MSL_ERR_SHAPE;
+  const long long n = (long long)c * ho * wo;
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, k, stride, pad, ho,
+                     wo, n, y, idx);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+int msl_maxpool_bwd(const float* dy, const int32_t* idx, int c, int h, int w, int k, int stride, int pad, int ho,
+                    int wo, float* dx, msl_stream_t stream) {
+  if (!dy || !idx || !dx || bad_geom(c, h, w, k, stride, pad, ho, wo) || 2 * pad > k) return MSL_ERR_ARG;
+  const long long n = (long long)c * h * w;
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, idx, h, w, k, stride,
+                     pad, ho, wo, n, dx);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+int msl_subsample(const float* x, int c, int h, int w, int stride, int ho, int wo, float* y, msl_stream_t stream) {
+  if (!x || !y || bad_geom(c, h, w, 1, stride, 0, ho, wo) || (long long)(ho - 1) * stride >= h ||
+      (long long)(wo - 1) * stride >= w)
+    return MSL_ERR_ARG;
+  const long long n = (long long)c * ho * wo;
+  hipLaunchKernelGGL(k_subsample, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, stride, ho, wo, n, y);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+int msl_subsample_bwd(const float* dy, int c, int h, int w, int stride, int ho, int wo, float* dx,
+                      msl_stream_t stream) {
+  if (!dy || !dx || bad_geom(c, h, w, 1, stride, 0, ho, wo)) return MSL_ERR_ARG;
+  const long long n = (long long)c * h * w;
+  hipLaunchKernelGGL(k_subsample_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, h, w, stride, ho, wo,
+                     n, dx);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
+}  // extern "C"

@@ -7,10 +7,10 @@ Drop-in for graphs/models/deeplab_multi.py of the reference:
   - same `forward(x) -> (x2, x1)` (layer6 head, layer5 head) (:113-130),
   - same `optim_parameters(args)` groups, duplicates included (:132-171, Q2).
 
-What runs where:
+What runs where (no library kernel is left on the step, so it is bit-reproducible run to run):
   - every stride-1 3x3 Bottleneck.conv2 (dilation 2 in layer3, 4 in layer4, and
     1 in layers 1-2) -> `DilatedConv3x3`, HIP implicit-GEMM kernels (fwd, dgrad,
-    wgrad) on FP32 MFMA;
+    wgrad; fp32 in the f16x3 form by default);
   - the ASPP heads (live branches d=6 and d=12 only, quirk Q1) -> one fused
     two-branch HIP conv with both biases;
   - bilinear upsampling (align_corners=True) -> HIP kernel; the result keeps a
@@ -18,12 +18,12 @@ What runs where:
   - every BatchNorm (train mode, batch statistics of the one image, Q9) fused with the
     following ReLU and, for bn3, the residual add -> HIP kernels with fp64-accumulated
     statistics (MIOpen's single-pass variance is not accurate enough at bs=1);
-  - stride-1 1x1 convs -> `PointwiseConv`: three GEMMs, each on the fastest of the HIP bf16x6
-    pointwise kernels, MIOpen and hipBLASLt for its shape (ops.conv1x1_plan), weight gradients
-    accumulated in place into the flat gradient buffer, and conv1's data gradient summing in
-    the identity residual's gradient (ops.ResidualGrad);
-  - stem 7x7 conv, the two stride-2 1x1 convs of layer2 block 0, maxpool -> PyTorch-ROCm
-    (MIOpen), SURVEY.md §8f row 1.
+  - every 1x1 conv -> `PointwiseConv`: the HIP pointwise GEMMs, weight gradients accumulated in
+    place into the flat gradient buffer, conv1's data gradient summing in the identity
+    residual's gradient (ops.ResidualGrad); layer2.0's stride-2 conv1 and downsample read one
+    shared x[:, :, ::2, ::2] (ops.subsample);
+  - the stem 7x7/2 conv -> `StemConv` (im2col + the pointwise GEMM), the ceil-mode maxpool ->
+    `MaxPool` (csrc/stem.hip, gather-form backward).
 """
 import torch
 import torch.nn as nn
@@ -45,33 +45,47 @@ class DilatedConv3x3(nn.Conv2d):
         return ops.dconv3x3(x, self.weight, self.dilation[0], self._pack)
 
 
-# By default a stride-1 1x1 conv runs each of its three GEMMs on whichever of the HIP bf16x6
-# pointwise kernels, MIOpen and hipBLASLt is fastest for that shape on MI355X (ops.conv1x1_plan,
-# profiles/r02_conv1x1_dispatch.txt); USE_HIP_POINTWISE switches all three to the HIP kernels
-# (parity-tested), and so does the bf16 conv math (ops.set_conv_math), which has no library form.
-USE_HIP_POINTWISE = False
+# Bottleneck blocks with an identity residual let conv1's data-gradient GEMM sum in the residual's
+# gradient (ops.ResidualGrad) instead of autograd's separate add; False restores the add (tests).
+FUSE_RESIDUAL_GRAD = True
 
 
 class PointwiseConv(nn.Conv2d):
-    """nn.Conv2d(cin, cout, 1, stride=1, bias=False): ops.conv1x1, or the HIP pointwise kernels."""
+    """nn.Conv2d(cin, cout, 1, stride, bias=False) on the HIP pointwise GEMMs (ops.pconv).  A strided
+    one reads x[:, :, ::stride, ::stride]; `presampled` says the caller already passed that."""
 
-    def __init__(self, in_channels, out_channels):
-        super().__init__(in_channels, out_channels, kernel_size=1, stride=1, bias=False)
+    def __init__(self, in_channels, out_channels, stride=1):
+        super().__init__(in_channels, out_channels, kernel_size=1, stride=stride, bias=False)
         self._pack = ops.PackCache(pointwise=True)
 
-    def fuses_residual_grad(self):
-        return not (USE_HIP_POINTWISE or ops.CONV_MATH != "fp32")
+    def forward(self, x, residual_grad=None, presampled=False):
+        if self.stride[0] != 1 and not presampled:
+            x = ops.subsample(x, self.stride[0])
+        return ops.pconv(x, self.weight, self._pack, residual_grad)
 
-    def forward(self, x, residual_grad=None):
-        if USE_HIP_POINTWISE or ops.CONV_MATH != "fp32":
-            return ops.pconv(x, self.weight, self._pack)
-        return ops.conv1x1(x, self.weight, self._pack, residual_grad)
+
+class StemConv(nn.Conv2d):
+    """ResNetMulti.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False) (deeplab_multi.py:73):
+    im2col + the HIP pointwise GEMM (ops.stem_conv)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride, padding):
+        super().__init__(in_channels, out_channels, kernel_size=kernel_size, stride=stride, padding=padding,
+                         bias=False)
+        self._pack = ops.PackCache(pointwise=True)
+
+    def forward(self, x):
+        return ops.stem_conv(x, self.weight, self.stride[0], self.padding[0], self._pack)
+
+
+class MaxPool(nn.MaxPool2d):
+    """nn.MaxPool2d(3, 2, 1, ceil_mode=True) (deeplab_multi.py:77) on HIP (ops.maxpool2d)."""
+
+    def forward(self, x):
+        return ops.maxpool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode)
 
 
 def conv1x1(inplanes, planes, stride):
-    if stride == 1:
-        return PointwiseConv(inplanes, planes)
-    return nn.Conv2d(inplanes, planes, kernel_size=1, stride=stride, bias=False)
+    return PointwiseConv(inplanes, planes, stride)
 
 
 class Bottleneck(nn.Module):
@@ -94,14 +108,15 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         # identity residual: its gradient is summed into x's gradient by conv1's data-gradient
         # GEMM (ops.ResidualGrad) rather than by autograd's accumulation kernel
-        fuse = (self.downsample is None and torch.is_grad_enabled() and isinstance(self.conv1, PointwiseConv)
-                and self.conv1.fuses_residual_grad())
+        fuse = FUSE_RESIDUAL_GRAD and self.downsample is None and torch.is_grad_enabled()
         hold = ops.ResidualGrad() if fuse else None
-        out = ops.bn_act(self.bn1, self.conv1(x, hold) if fuse else self.conv1(x), relu=True)
+        # a strided block (layer2.0): conv1 and the downsample read one shared x[:, :, ::s, ::s]
+        xs = ops.subsample(x, self.stride) if self.stride != 1 else x
+        out = ops.bn_act(self.bn1, self.conv1(xs, hold, presampled=True), relu=True)
         out = ops.bn_act(self.bn2, self.conv2(out), relu=True)
         residual = x.detach() if fuse else x
         if self.downsample is not None:
-            residual = ops.bn_act(self.downsample[1], self.downsample[0](x))
+            residual = ops.bn_act(self.downsample[1], self.downsample[0](xs, presampled=True))
         # bn3 + residual add + ReLU in one kernel (deeplab_multi.py:38-46)
         return ops.bn_act(self.bn3, self.conv3(out), residual=residual, relu=True, residual_grad=hold)
 
@@ -136,12 +151,12 @@ class ResNetMulti(nn.Module):
     def __init__(self, block, layers, num_classes):
         self.inplanes = 64
         super().__init__()
-        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.conv1 = StemConv(3, 64, kernel_size=7, stride=2, padding=3)
         self.bn1 = nn.BatchNorm2d(64, affine=affine_par)
         for i in self.bn1.parameters():
             i.requires_grad = False
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1, ceil_mode=True)
+        self.maxpool = MaxPool(kernel_size=3, stride=2, padding=1, ceil_mode=True)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=1, dilation=2)

@@ -92,6 +92,12 @@ SIGNATURES = {
     "msl_bn_bwd_am": (c_int, [c_p] * 10 + [c_int] * 5 + [c_p, c_sz, c_p, c_p]),
     "msl_image_transform": (c_int, [c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p, c_p]),
     "msl_label_transform": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
+    "msl_im2col": (c_int, [c_p] + [c_int] * 10 + [c_p, c_p]),
+    "msl_col2im": (c_int, [c_p] + [c_int] * 10 + [c_p, c_p]),
+    "msl_maxpool_fwd": (c_int, [c_p] + [c_int] * 8 + [c_p, c_p, c_p]),
+    "msl_maxpool_bwd": (c_int, [c_p, c_p] + [c_int] * 8 + [c_p, c_p]),
+    "msl_subsample": (c_int, [c_p] + [c_int] * 6 + [c_p, c_p]),
+    "msl_subsample_bwd": (c_int, [c_p] + [c_int] * 6 + [c_p, c_p]),
     "msl_sgd_block_elems": (c_int, []),
     "msl_sgd_plan": (c_ll, [c_p, c_int, c_p, c_p, c_ll]),
     "msl_sgd_step": (c_int, [c_p, c_p, c_p, c_ll, c_f, c_f, c_f, c_f, c_f, c_p]),

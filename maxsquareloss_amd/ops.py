@@ -6,7 +6,6 @@ reference only runs bs=1: IW_MaxSquareloss broadcasts (N,H,W) weights against
 (N,C,H,W) probabilities, which only works for N=1 - SURVEY.md quirk Q3).
 """
 import torch
-import torch.nn.functional as F
 from torch.autograd import Function
 
 from . import hip
@@ -398,10 +397,16 @@ def aspp2(x, w0, b0, w1, b1, dil0, dil1, cache):
 
 # --------------------------------------------------------------------------- pointwise conv
 class _PConv(Function):
-    """y = W x for a 1x1, stride-1, bias-free conv (W: [cout][cin][1][1])."""
+    """y = W x for a 1x1, stride-1, bias-free conv (W: [cout][cin][1][1]) on the HIP pointwise GEMMs:
+      y  = W x        msl_pconv_fwd (the conv math's form)
+      dx = W^T dy     msl_pconv_dgrad; with a ResidualGrad `hold`, dx = (the identity residual's
+                      gradient) + W^T dy, summed by the GEMM's accumulate epilogue (fp32 / fp16)
+      dW += dy x^T    msl_pconv_wgrad, straight into the flat gradient buffer when the parameter
+                      has a sink
+    No library GEMM: every call is deterministic (fixed summation order)."""
 
     @staticmethod
-    def forward(ctx, x, weight, cache):
+    def forward(ctx, x, weight, cache, hold=None):
         x = _check_act(x, "pconv")
         cout, cin = weight.shape[0], weight.shape[1]
         if weight.shape[2:] != (1, 1) or x.size(1) != cin:
@@ -414,6 +419,7 @@ class _PConv(Function):
         wsb = lib.msl_pconv_fwd_workspace(cin, cout, p)
         ws = hip.workspace(wsb, x.device)
         math = CONV_MATH
+        # f16x3: x's absmax partials once for the forward and the weight gradient
         xpart = _parts(x, math, compute=_split_gemm(cout, cin))
         hip.check(_conv_call(lib, "msl_pconv_fwd", math,
                              (x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
@@ -422,6 +428,7 @@ class _PConv(Function):
         ctx.save_for_backward(x, weight)
         ctx.meta = (cin, cout, p, cache, math)
         ctx.xpart = xpart
+        ctx.hold = hold
         return y
 
     @staticmethod
@@ -432,26 +439,32 @@ class _PConv(Function):
         lib = hip.load()
         s = hip.stream_ptr()
         dx = None
+        hold = ctx.hold
+        # f16x3: dy's absmax partials once for the data and weight gradients
         gpart = _parts(gy, math, compute=_split_gemm(cin, cout))
         if ctx.needs_input_grad[0]:
+            acc = 0
+            if hold is not None and hold.g is not None:
+                dx, hold.g = hold.g, None
+                acc = 1
+            else:
+                dx = torch.empty_like(x)
             packed_d = cache.get([weight], cin, cout, 1)
-            dx = torch.empty_like(x)
             wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
             ws = hip.workspace(wsb, x.device)
+            cnt = hip.counters(x.device).data_ptr()
             if math == "bf16":
-                hip.check(lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
-                                                   hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s),
-                          "msl_pconv_dgrad")
-            elif math == "fp16":
-                hip.check(lib.msl_pconv_dgrad_f16(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
-                                                  0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s,
-                                                  *_pp(gpart)), "msl_pconv_dgrad")
+                tgt = torch.empty_like(x) if acc else dx
+                hip.check(lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), tgt.data_ptr(), cin, cout, p,
+                                                   cnt, ws.data_ptr(), wsb, s), "msl_pconv_dgrad")
+                if acc:  # the bf16 form has no accumulate epilogue
+                    dx.add_(tgt)
             else:
-                hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
-                                                     0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s,
-                                                     *_pp(gpart)), "msl_pconv_dgrad")
+                fn = lib.msl_pconv_dgrad_f16 if math == "fp16" else lib.msl_pconv_dgrad_acc_sc
+                hip.check(fn(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, acc, cnt,
+                             ws.data_ptr(), wsb, s, *_pp(gpart)), "msl_pconv_dgrad")
         if not ctx.needs_input_grad[1]:
-            return dx, None, None
+            return dx, None, None, None
         sink = grad_sink(weight)
         dst = sink[0] if sink is not None else torch.empty_like(weight)
         wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
@@ -460,22 +473,27 @@ class _PConv(Function):
                              (x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p, int(sink is not None),
                               ws.data_ptr(), wsb, s), (ctx.xpart, gpart)), "msl_pconv_wgrad")
         if sink is None:
-            return dx, dst, None
+            return dx, dst, None, None
         sink[1].notify(sink[2])
-        return dx, None, None
+        return dx, None, None, None
 
 
-def pconv(x, weight, cache):
-    """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99)."""
-    return _PConv.apply(x, weight, cache)
+def pconv(x, weight, cache, residual_grad=None):
+    """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99).
+    `residual_grad` (a ResidualGrad also given to the block's bn_act): its gradient is added into
+    this conv's input gradient by the data-gradient GEMM."""
+    return _PConv.apply(x, weight, cache, residual_grad)
+
+
+conv1x1 = pconv
 
 
 # --------------------------------------------------------------------------- fused residual gradient
 class ResidualGrad:
     """Carries the gradient of a bottleneck's identity residual from bn3's backward (which runs
     first) to conv1's backward, which adds it into the block input's gradient inside its data-
-    gradient GEMM (msl_pconv_dgrad_acc / hipBLASLt addmm with beta = 1) instead of autograd's
-    separate accumulation kernel (deeplab_multi.py:31-48: x feeds conv1 and the residual)."""
+    gradient GEMM (msl_pconv_dgrad_acc) instead of autograd's separate accumulation kernel
+    (deeplab_multi.py:31-48: x feeds conv1 and the residual)."""
 
     __slots__ = ("g",)
 
@@ -483,165 +501,152 @@ class ResidualGrad:
         self.g = None
 
 
-# --------------------------------------------------------------------------- 1x1 conv, per-GEMM dispatch
-def conv1x1_plan(cin, cout, p, form="bf16x6", residual=False):
-    """Implementation of each of the three GEMMs of a stride-1 1x1 conv: (fwd, dgrad, wgrad), each
-    "hip" (the bf16x6 pointwise kernels, fp32 form bf16x6 only), "miopen" or "hipblaslt".
-    `residual`: the data gradient also sums in an identity residual's gradient (ops.ResidualGrad),
-    which the HIP kernel and hipBLASLt do in the GEMM while MIOpen needs a separate add.
-
-    Per-GEMM winners of every 1x1 shape the UDA step runs, timed on MI355X in isolation
-    (scripts/bench_conv1x1_dispatch.py, profiles/r02_conv1x1_dispatch.txt), as rules:
-      fwd    HIP on the 33k-px layer1 maps, and at <= 16k px when cin >= 512 and one side is >= 1024
-             channels (layer3/4 conv1/conv3/downsample); MIOpen elsewhere (256 -> 1024: HIP wins in
-             isolation on some boxes, MIOpen in the full step - scripts/bench_plan_ab.py);
-      dgrad  HIP on the narrowing 33k-px GEMM (256 -> 64), and at <= 16k px when one side is >= 1024
-             and both >= 256, except the narrowing 1024 -> 256 without a residual (MIOpen wins
-             there); else hipBLASLt when cout > cin or at 33k px, else MIOpen;
-      wgrad  HIP at 33k px and at <= 16k px when one side is >= 1024 channels and both >= 256
-             (k_wgrad_x6 with one tap; with cout > cin on swapped operands, so the narrower
-             operand is the pre-split one), hipBLASLt addmm elsewhere.
-    With the residual, the narrowing 1024 -> 256 data gradient goes to the HIP kernel too (its
-    accumulating form beats MIOpen + add by 3-4 us on every box measured).  The HIP forward-form
-    GEMMs run the hybrid schedule (SkArgs: data-parallel rounds + a stream-K remainder), which
-    is what makes them win on the >= 512-tile shapes (256 -> 1024: 53 vs 61 us pure stream-K).
-    In the f16x3 form (profiles/r02_conv1x1_dispatch_f16x3.txt) the HIP kernels win every GEMM of
-    the wide shapes outright (256 -> 1024 fwd 35 vs 50 us MIOpen, 1024 -> 256 dgrad 35 vs 45), so
-    there the wide forward and data gradient are HIP whatever the direction or residual.
-    """
-    x6 = form in SPLIT_FORMS
-    h3 = form == "f16x3"
-    big = p > 16384
-    wide = max(cin, cout) >= 1024 and min(cin, cout) >= 256
-    fwd = "hip" if x6 and (big or (wide and (cin >= 512 or h3))) else "miopen"
-    if x6 and ((big and cin > cout) or (not big and wide and (h3 or residual or not (cin > cout and cout < 512)))):
-        dgrad = "hip"
-    elif cout > cin or big:
-        dgrad = "hipblaslt"
-    else:
-        dgrad = "miopen"
-    wgrad = "hip" if big or (x6 and wide) else "hipblaslt"
-    return fwd, dgrad, wgrad
+# --------------------------------------------------------------------------- stem, maxpool, stride-2 glue
+def pool_out(n, k, s, p, ceil):
+    """torch's pooling_output_shape (dilation 1)."""
+    num = n + 2 * p - (k - 1) - 1 + ((s - 1) if ceil else 0)
+    o = num // s + 1
+    if ceil and (o - 1) * s >= n + p:
+        o -= 1
+    return o
 
 
-_PLANS = {}
-
-
-class _Conv1x1(Function):
-    """1x1, stride-1, bias-free conv as three GEMMs, each on the implementation conv1x1_plan picks:
-      y  = W x        HIP x6 pointwise fwd or MIOpen
-      dx = W^T dy     HIP x6 pointwise dgrad, hipBLASLt (torch.mm) or MIOpen
-      dW += dy x^T    HIP pointwise wgrad or hipBLASLt addmm, straight into the flat gradient
-                      buffer (beta = 1) when the parameter has a sink
-    """
+class _StemConv(Function):
+    """conv2d(x, W, stride, padding) for a bias-free k x k conv as im2col + the pointwise GEMM
+    (csrc/stem.hip): the [cout][cin][k][k] weight is a [cout][cin*k*k] pointwise weight as laid out."""
 
     @staticmethod
-    def forward(ctx, x, weight, cache, hold=None):
-        cout, cin = weight.shape[0], weight.shape[1]
+    def forward(ctx, x, weight, stride, pad, cache):
+        x = _check_act(x, "stem_conv")
+        cout, cin, kh, kw = weight.shape
+        if x.size(1) != cin:
+            raise hip.MSLError(f"stem_conv: weight {tuple(weight.shape)} does not match input {tuple(x.shape)}")
         h, w = x.shape[2], x.shape[3]
-        p = h * w
-        form = f32_form()
-        ctx.hold = hold
-        ctx.form = form
-        key = (cin, cout, p, form, hold is not None)
-        plan = _PLANS.get(key)
-        if plan is None:
-            plan = _PLANS[key] = conv1x1_plan(cin, cout, p, form, hold is not None)
-        # f16x3: x's absmax partials once for the HIP forward and the HIP weight gradient
-        ctx.xpart = _parts(x, compute=plan[0] == "hip" and plan[2] == "hip")
-        if plan[0] == "hip":
-            lib = hip.load()
-            packed = cache.get([weight], cin, cout, 0)
-            y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
-            wsb = lib.msl_pconv_fwd_workspace(cin, cout, p)
-            ws = hip.workspace(wsb, x.device)
-            hip.check(lib.msl_pconv_fwd_sc(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
-                                           hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr(),
-                                           *_pp(ctx.xpart)), "msl_pconv_fwd")
-        else:
-            y = F.conv2d(x, weight)
-        ctx.save_for_backward(x, weight)
-        ctx.cache = cache
-        ctx.plan = plan
+        ho, wo = (h + 2 * pad - kh) // stride + 1, (w + 2 * pad - kw) // stride + 1
+        kk, p = cin * kh * kw, ho * wo
+        lib = hip.load()
+        s = hip.stream_ptr()
+        col = torch.empty((1, kk, ho, wo), dtype=_f32, device=x.device)
+        hip.check(lib.msl_im2col(x.data_ptr(), cin, h, w, kh, kw, stride, pad, 1, ho, wo, col.data_ptr(), s),
+                  "msl_im2col")
+        wmat = weight.detach().contiguous()
+        packed = cache.get([wmat], kk, cout, 0)
+        y = torch.empty((1, cout, ho, wo), dtype=_f32, device=x.device)
+        wsb = lib.msl_pconv_fwd_workspace(kk, cout, p)
+        ws = hip.workspace(wsb, x.device)
+        math = CONV_MATH
+        cpart = _parts(col, math, compute=_split_gemm(cout, kk))
+        hip.check(_conv_call(lib, "msl_pconv_fwd", math,
+                             (col.data_ptr(), packed.data_ptr(), y.data_ptr(), kk, cout, p,
+                              hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (cpart,)), "msl_pconv_fwd")
+        ctx.save_for_backward(col, weight)
+        ctx.meta = (cin, h, w, kh, kw, stride, pad, ho, wo, cache, math)
+        ctx.cpart = cpart
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
-        _, dplan, wplan = ctx.plan
-        cout, cin = weight.shape[0], weight.shape[1]
-        h, w = x.shape[2], x.shape[3]
-        p = h * w
+        col, weight = ctx.saved_tensors
+        cin, h, w, kh, kw, stride, pad, ho, wo, cache, math = ctx.meta
+        cout, kk, p = weight.shape[0], col.size(1), ho * wo
         gy = gy.contiguous()
-        g2 = gy.view(cout, p)
-        x2 = x.view(cin, p)
-        w2 = weight.view(cout, cin)
+        lib = hip.load()
+        s = hip.stream_ptr()
         dx = None
-        hold = ctx.hold
-        # f16x3: dy's absmax partials once for the HIP data and weight gradients
-        gpart = _parts(gy, compute=dplan == "hip" and wplan == "hip" and ctx.needs_input_grad[0]
-                       and ctx.needs_input_grad[1])
-        if ctx.needs_input_grad[0] and hold is not None and hold.g is not None:
-            # dx = (the residual's gradient) + W^T dy, accumulated by the GEMM itself
-            dx, hold.g = hold.g, None
-            if dplan == "hip":
-                lib = hip.load()
-                packed_d = ctx.cache.get([weight], cin, cout, 1)
-                wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
-                ws = hip.workspace(wsb, x.device)
-                hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
-                                                     1, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
-                                                     hip.stream_ptr(), *_pp(gpart)), "msl_pconv_dgrad_acc")
-            elif dplan == "hipblaslt":
-                dx.view(cin, p).addmm_(w2.t(), g2)
-            else:  # MIOpen's data gradient has no accumulate form: the add stays a kernel of its own
-                dx.add_(torch.ops.aten.convolution_backward(gy, x, weight, None, (1, 1), (0, 0), (1, 1), False,
-                                                            (0, 0), 1, (True, False, False))[0])
-        elif ctx.needs_input_grad[0]:
-            if dplan == "hip":
-                lib = hip.load()
-                packed_d = ctx.cache.get([weight], cin, cout, 1)
-                dx = torch.empty_like(x)
-                wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
-                ws = hip.workspace(wsb, x.device)
-                hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p,
-                                                     0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
-                                                     hip.stream_ptr(), *_pp(gpart)), "msl_pconv_dgrad")
-            elif dplan == "hipblaslt":
-                dx = torch.mm(w2.t(), g2).view(1, cin, h, w)
+        gpart = _parts(gy, math, compute=_split_gemm(kk, cout))
+        if ctx.needs_input_grad[0]:
+            packed_d = cache.get([weight.detach().contiguous()], kk, cout, 1)
+            dcol = torch.empty_like(col)
+            wsb = lib.msl_pconv_dgrad_workspace(kk, cout, p)
+            ws = hip.workspace(wsb, gy.device)
+            cnt = hip.counters(gy.device).data_ptr()
+            if math == "bf16":
+                st = lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), dcol.data_ptr(), kk, cout, p, cnt,
+                                              ws.data_ptr(), wsb, s)
             else:
-                dx = torch.ops.aten.convolution_backward(gy, x, weight, None, (1, 1), (0, 0), (1, 1), False,
-                                                         (0, 0), 1, (True, False, False))[0]
+                fn = lib.msl_pconv_dgrad_f16 if math == "fp16" else lib.msl_pconv_dgrad_acc_sc
+                st = fn(gy.data_ptr(), packed_d.data_ptr(), dcol.data_ptr(), kk, cout, p, 0, cnt, ws.data_ptr(), wsb,
+                        s, *_pp(gpart))
+            hip.check(st, "msl_pconv_dgrad")
+            dx = torch.empty((1, cin, h, w), dtype=_f32, device=gy.device)
+            hip.check(lib.msl_col2im(dcol.data_ptr(), cin, h, w, kh, kw, stride, pad, 1, ho, wo, dx.data_ptr(), s),
+                      "msl_col2im")
         if not ctx.needs_input_grad[1]:
-            return dx, None, None, None
+            return dx, None, None, None, None
         sink = grad_sink(weight)
-        if wplan == "hip":
-            # HIP pointwise wgrad (accumulating into the flat buffer when it can)
-            lib = hip.load()
-            dst = sink[0] if sink is not None else torch.empty_like(weight)
-            wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
-            ws = hip.workspace(wsb, x.device)
-            hip.check(lib.msl_pconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p,
-                                             int(sink is not None), ws.data_ptr(), wsb, hip.stream_ptr(),
-                                             *_pp(ctx.xpart), *_pp(gpart)), "msl_pconv_wgrad")
-            if sink is None:
-                return dx, dst, None, None
-        elif sink is not None:
-            sink[0].view(cout, cin).addmm_(g2, x2.t())
-        else:
-            return dx, torch.mm(g2, x2.t()).view_as(weight), None, None
+        dst = sink[0] if sink is not None else torch.empty_like(weight)
+        wsb = lib.msl_pconv_wgrad_workspace(kk, cout, p)
+        ws = hip.workspace(wsb, gy.device)
+        hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
+                             (col.data_ptr(), gy.data_ptr(), dst.data_ptr(), kk, cout, p, int(sink is not None),
+                              ws.data_ptr(), wsb, s), (ctx.cpart, gpart)), "msl_pconv_wgrad")
+        if sink is None:
+            return dx, dst, None, None, None
         sink[1].notify(sink[2])
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
-def conv1x1(x, weight, cache, residual_grad=None):
-    """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99).
-    `residual_grad` (a ResidualGrad also given to the block's bn_act): its gradient is added into
-    this conv's input gradient by the data-gradient GEMM."""
-    x = _check_act(x, "conv1x1")
-    if weight.shape[2:] != (1, 1) or x.size(1) != weight.shape[1]:
-        raise hip.MSLError(f"conv1x1: weight {tuple(weight.shape)} does not match input {tuple(x.shape)}")
-    return _Conv1x1.apply(x, weight, cache, residual_grad)
+def stem_conv(x, weight, stride, pad, cache):
+    """nn.Conv2d(cin, cout, k, stride, pad, bias=False) (ResNetMulti.conv1, deeplab_multi.py:73-74)."""
+    return _StemConv.apply(x, weight, int(stride), int(pad), cache)
+
+
+class _MaxPool(Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, ceil):
+        x = _check_act(x, "maxpool")
+        c, h, w = x.shape[1:]
+        ho, wo = pool_out(h, k, s, p, ceil), pool_out(w, k, s, p, ceil)
+        y = torch.empty((1, c, ho, wo), dtype=_f32, device=x.device)
+        idx = torch.empty((1, c, ho, wo), dtype=torch.int32, device=x.device)
+        hip.check(hip.load().msl_maxpool_fwd(x.data_ptr(), c, h, w, k, s, p, ho, wo, y.data_ptr(), idx.data_ptr(),
+                                             hip.stream_ptr()), "msl_maxpool_fwd")
+        ctx.save_for_backward(idx)
+        ctx.meta = (c, h, w, k, s, p, ho, wo)
+        ctx.mark_non_differentiable(idx)
+        return y, idx
+
+    @staticmethod
+    def backward(ctx, gy, _gi):
+        (idx,) = ctx.saved_tensors
+        c, h, w, k, s, p, ho, wo = ctx.meta
+        gy = gy.contiguous()
+        dx = torch.empty((1, c, h, w), dtype=_f32, device=gy.device)
+        hip.check(hip.load().msl_maxpool_bwd(gy.data_ptr(), idx.data_ptr(), c, h, w, k, s, p, ho, wo, dx.data_ptr(),
+                                             hip.stream_ptr()), "msl_maxpool_bwd")
+        return dx, None, None, None, None
+
+
+def maxpool2d(x, kernel_size, stride, padding, ceil_mode):
+    """nn.MaxPool2d(k, s, p, ceil_mode) (deeplab_multi.py:77); returns the pooled tensor."""
+    return _MaxPool.apply(x, int(kernel_size), int(stride), int(padding), bool(ceil_mode))[0]
+
+
+class _Subsample(Function):
+    @staticmethod
+    def forward(ctx, x, s):
+        x = _check_act(x, "subsample")
+        c, h, w = x.shape[1:]
+        ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+        y = torch.empty((1, c, ho, wo), dtype=_f32, device=x.device)
+        hip.check(hip.load().msl_subsample(x.data_ptr(), c, h, w, s, ho, wo, y.data_ptr(), hip.stream_ptr()),
+                  "msl_subsample")
+        ctx.meta = (c, h, w, s, ho, wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        c, h, w, s, ho, wo = ctx.meta
+        gy = gy.contiguous()
+        dx = torch.empty((1, c, h, w), dtype=_f32, device=gy.device)
+        hip.check(hip.load().msl_subsample_bwd(gy.data_ptr(), c, h, w, s, ho, wo, dx.data_ptr(), hip.stream_ptr()),
+                  "msl_subsample_bwd")
+        return dx, None
+
+
+def subsample(x, stride):
+    """x[:, :, ::stride, ::stride] (the input a stride-s 1x1 conv reads)."""
+    return _Subsample.apply(x, int(stride))
 
 
 # --------------------------------------------------------------------------- upsample

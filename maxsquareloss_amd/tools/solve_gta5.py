@@ -98,26 +98,38 @@ class UDATrainer(Trainer):
 
     def uda_step(self, x_s, y_s, x_t):
         """One iteration of the hot loop (solve_gta5.py:336-383), inputs already on the device.
-        With use_graph (single process), iterations after the first replay a captured hipGraph."""
+        With use_graph, iterations after the first replay captured hipGraphs (utils/graph.py): one
+        graph for the whole iteration on a single process; with a data-parallel reducer, a graph of
+        the two forward/backward passes, the gradient all-reduce, then a graph of the SGD step."""
         self.poly_lr_scheduler(optimizer=self.optimizer, init_lr=self.args.lr)
-        if self.use_graph and self.reducer is None:
+        if self.use_graph:
             if self._graphed is None:
-                self._graphed = GraphedStep(self, self._uda_body)
+                if self.reducer is None:
+                    self._graphed = GraphedStep(self, self._uda_body)
+                else:
+                    self._graphed = GraphedStep(self, self._uda_grads, exchange=self.reducer.reduce_all,
+                                                update=self._uda_update)
             self._graphed(x_s, y_s, x_t)
         else:
             self._uda_body(x_s, y_s, x_t)
         self.current_iter += 1
 
-    def _uda_body(self, x_s, y_s, x_t):
+    def _uda_grads(self, x_s, y_s, x_t):
         pred = self.model(x_s)
         self.train_source(pred, y_s)
         pred = self.model(x_t)
         self.train_target(pred)
-        if self.reducer:
-            self.reducer.finish()
+
+    def _uda_update(self):
         self.optimizer.step()
         self.optimizer.zero_grad()
         self.packer.run()  # the next iteration's weight packs, batched (ops.PackBatch)
+
+    def _uda_body(self, x_s, y_s, x_t):
+        self._uda_grads(x_s, y_s, x_t)
+        if self.reducer:
+            self.reducer.finish()
+        self._uda_update()
 
     # ---------------------------------------------------------------- loop
     def main(self):

@@ -238,8 +238,10 @@ def add_train_args(arg_parser):
            "fp16 MFMA path (scaled fp16 operands, fp32 sums), bf16 = bf16 products, fp32 sums; BN, "
            "losses, SGD stay fp32")
     a("--f32_form", default=None, choices=["mfma_f32", "bf16x6", "f16x3"],
-      help="matrix-core form of the fp32 convs (default: the library's): mfma_f32 = "
-           "v_mfma_f32_32x32x2_f32; bf16x6 = three-way bf16 split, six products, fp32-accurate")
+      help="matrix-core form of the fp32 convs; default f16x3 (the library's default): each operand "
+           "scaled by a power of two and split into two fp16 terms, three v_mfma_f32_32x32x16_f16 "
+           "products with fp32 sums (fp32-accurate); mfma_f32 = v_mfma_f32_32x32x2_f32 (exact fp32 "
+           "FMA chains); bf16x6 = three-way bf16 split, six products, fp32-accurate")
     return arg_parser
 
 

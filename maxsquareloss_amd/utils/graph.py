@@ -13,18 +13,27 @@ iteration:
     ring before each replay;
   - every weight pack (ops.PackCache) and the SGD step are inside the graph, so each replay
     repacks from the weights the previous replay updated; after a replay the parameters'
-    version counters are bumped so eager code outside the graph repacks too;
+    version counters are bumped so eager code outside the graph repacks too, and recorded: a
+    parameter changed eagerly between replays (load_checkpoint, an in-place edit) shows as a new
+    version, and the packs are then rebuilt eagerly before the next replay reads them;
   - loss scalars / meters are the captured tensors, rewritten in place by every replay.
-Data-parallel runs (a GradReducer with host-driven bucket countdown) stay eager.
+Data-parallel runs (a GradReducer, whose bucket countdown is host-driven) capture two graphs: the
+forward/backward passes (`body`, the reducer deferred) and the update (`update`: SGD, zero_grad,
+packs); each iteration replays the first, runs `exchange` (the reducer's all-reduce of every live
+bucket, eager, on RCCL's stream), then replays the second.  Those captures use the thread-local
+capture mode, so RCCL's / gloo's own threads may keep calling the HIP runtime meanwhile.
 """
 import torch
 
 
 class GraphedStep:
-    def __init__(self, trainer, body, ring=4):
+    def __init__(self, trainer, body, ring=4, exchange=None, update=None):
         self.tr = trainer
         self.body = body
+        self.exchange = exchange
+        self.update = update
         self.graph = None
+        self.graph_update = None
         self.static = None
         self.device = trainer.device
         self.stream = torch.cuda.Stream(device=self.device)
@@ -33,6 +42,8 @@ class GraphedStep:
         self.ring_ev = [None] * ring
         self.k = 0
         self.replays = 0
+        self.versions = None   # the parameters' versions right after the last replay's bump
+        self.eager_repacks = 0
 
     def _set_lr(self):
         slot = self.k % len(self.ring)
@@ -55,31 +66,57 @@ class GraphedStep:
         for s, x in zip(self.static, inputs):
             if s.data_ptr() != x.data_ptr():
                 s.copy_(x, non_blocking=True)
+        opt = self.tr.optimizer
+        if self.versions is not None and any(p._version != v for p, v in zip(opt._uniq, self.versions)):
+            # weights edited outside the graph since the last replay: its captured forward reads the
+            # packs the last replay wrote, so rebuild them from the current weights first
+            self.tr.packer.run()
+            self.eager_repacks += 1
         self._set_lr()
         self.graph.replay()
+        if self.exchange is not None:
+            self.exchange()
+            self.graph_update.replay()
         self.replays += 1
-        opt = self.tr.optimizer
         for p in opt._uniq:
             torch.autograd.graph.increment_version(p)
+        self.versions = [p._version for p in opt._uniq]
 
     def _first(self, *inputs):
         opt = self.tr.optimizer
         self.static = [x.detach().clone() for x in inputs]
         s = self.stream
         s.wait_stream(torch.cuda.current_stream(self.device))
+        dp = self.exchange is not None
+        red = self.tr.reducer if dp else None
         with torch.cuda.stream(s):
-            self.body(*self.static)  # iteration 0, eager (host learning rates)
+            if dp:  # iteration 0, eager, with the overlapped exchange (learns the live set)
+                self.body(*self.static)
+                red.finish()
+                self.update()
+            else:
+                self.body(*self.static)  # iteration 0, eager (host learning rates)
         torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
         opt.prepare()  # the table of every later step (buffers exist: has_buf = 1)
         opt.lr_dev = self.lr_dev
         owners = [self.tr] + [m for m in vars(self.tr).values() if isinstance(m, torch.nn.Module)]
         before = [{k: v for k, v in vars(o).items() if isinstance(v, torch.Tensor)} for o in owners]
+        mode = "thread_local" if dp else "global"
         try:
+            if dp:
+                red.deferred = True
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph, stream=s):
+            with torch.cuda.graph(self.graph, stream=s, capture_error_mode=mode):
                 self.body(*self.static)
+            if dp:
+                self.graph_update = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph_update, stream=s, capture_error_mode=mode):
+                    self.update()
         finally:
             opt.lr_dev = None  # eager steps outside the graph keep passing the rates by value
+            if dp:
+                red.deferred = False
         # the capture rebound the step's outputs (loss scalars, IW histogram, ...) to tensors the
         # graph writes but has not written yet: give them iteration 0's values
         with torch.cuda.stream(s):

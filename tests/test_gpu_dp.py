@@ -178,3 +178,74 @@ def test_grad_reducer_real_model_two_ranks(tmp_path):
                                       bool(np.array_equal(got_b[sl], other[sl])), "n differing", int((d != 0).sum()),
                                       "of", d.size, "at argmax: got", got_b[sl][k], "s0", s0[k], "s1", s1[k],
                                       "other rank", other[sl][k]))
+
+
+def _graph_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK="0")
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from maxsquareloss_amd.tools.solve_gta5 import UDATrainer, build_parser
+        from maxsquareloss_amd.tools.train_source import init_args
+        from maxsquareloss_amd.utils.synthetic import synthetic_image, synthetic_labels
+        out = {}
+        for graph in (False, True):
+            argv = ["--crop_size", f"{W},{H}", "--target_crop_size", f"{W},{H}", "--imagenet_pretrained", "False",
+                    "--save_dir", "", "--target_mode", "IW_maxsquare", "--multi", "True", "--lambda_target", "0.09",
+                    "--iter_max", "1000", "--graph", str(graph)]
+            args, _, _ = init_args(build_parser().parse_args(argv))
+            tr = UDATrainer(args, cuda=True)
+            tr.optimizer.zero_grad()
+            losses = []
+            for it in range(4):
+                seed = 1000 * rank + it
+                tr.uda_step(synthetic_image(H, W, seed).cuda(), synthetic_labels(H, W, 19, seed).cuda(),
+                            synthetic_image(H, W, 500 + seed).cuda())
+                torch.cuda.synchronize()
+                losses.append((tr.loss_val.item(), tr.loss_target.item(), tr.loss_target_2.item()))
+            if graph:
+                assert tr._graphed is not None and tr._graphed.replays == 3 and tr._graphed.graph_update is not None
+            out[graph] = (losses, torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).cpu().numpy())
+            del tr
+        q.put((rank, "ok", out))
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure to the parent instead of hanging it
+        import traceback
+        q.put((rank, "error", traceback.format_exc() + repr(e)))
+        raise
+
+
+def test_graphed_dp_step_matches_eager_dp():
+    """The captured data-parallel step (utils/graph.py: graph of the two forward/backward passes,
+    the reducer's all-reduce of every live bucket, graph of the SGD step) against the eager DP
+    step with the overlapped bucket countdown, 2 ranks (gloo) x 4 UDA iterations: every loss and
+    every parameter bit-identical (the step has no library kernel and the 2-rank sum is exact in
+    either order), and the two replicas' parameters identical after every run (one exchange per
+    iteration keeps data-parallel replicas in lock step)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            item = q.get(timeout=300)
+            assert item[1] == "ok", item[2]
+            got[item[0]] = item[2]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    for r in range(world):
+        (le, pe), (lg, pg) = got[r][False], got[r][True]
+        assert le == lg, (r, le, lg)
+        assert np.array_equal(pe, pg), (r, int((pe != pg).sum()))
+    for graph in (False, True):
+        assert np.array_equal(got[0][graph][1], got[1][graph][1]), graph

@@ -88,9 +88,9 @@ def test_pconv_fwd_bwd(cin, cout, h, w, f32_form):
 @pytest.mark.parametrize("cin,cout,h,w", [(64, 256, 129, 257), (256, 64, 129, 257), (64, 64, 129, 257),
                                            (1024, 256, 65, 129), (256, 1024, 65, 129), (1024, 512, 65, 129),
                                            (512, 128, 65, 129), (128, 512, 65, 129), (512, 2048, 17, 33)])
-def test_conv1x1_dispatch(cin, cout, h, w, f32_form):
-    """ops.conv1x1: every GEMM on the implementation conv1x1_plan picks (HIP x6 / MIOpen /
-    hipBLASLt), every gradient against fp64, in both fp32 forms."""
+def test_conv1x1_step_shapes(cin, cout, h, w, f32_form):
+    """ops.conv1x1 on every 1x1 shape of the UDA step: all three GEMMs on the HIP pointwise kernels,
+    every gradient against fp64, in every fp32 form."""
     g = torch.Generator().manual_seed(cin + 5 * cout)
     x = torch.randn(1, cin, h, w, generator=g)
     wt = torch.randn(cout, cin, 1, 1, generator=g) * 0.05
@@ -608,7 +608,7 @@ def test_bottleneck_fused_residual_grad(f32_form, monkeypatch):
     gy = torch.randn(1, 1024, 17, 33).to(DEV)
     out = {}
     for fused in (True, False):
-        monkeypatch.setattr(dm.PointwiseConv, "fuses_residual_grad", lambda self, f=fused: f)
+        monkeypatch.setattr(dm, "FUSE_RESIDUAL_GRAD", fused)
         xg = x.clone().requires_grad_()
         for prm in blk.parameters():
             prm.grad = None
@@ -793,3 +793,71 @@ def test_bn_absmax_outputs(c, h, w, res, relu, fused):
         assert torch.equal(ba, dx.abs().amax(dim=1))
     finally:
         ops.set_bn_fused(prev)
+
+
+# ---------------------------------------------------------------------------- stem / maxpool / stride 2
+@pytest.mark.parametrize("h,w", [(64, 128), (33, 47), (512, 1024)])
+def test_stem_conv_fwd_bwd(h, w, f32_form):
+    """ResNetMulti.conv1 (7x7, stride 2, pad 3) as im2col + the pointwise GEMM: output, data and weight
+    gradients against fp64 (deeplab_multi.py:73-74)."""
+    g = torch.Generator().manual_seed(h + w)
+    x = torch.randn(1, 3, h, w, generator=g) * 50
+    wt = torch.randn(64, 3, 7, 7, generator=g) * 0.01
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    gy = torch.randn(1, 64, ho, wo, generator=g)
+    xr, wr = x.double().requires_grad_(), wt.double().requires_grad_()
+    yr = F.conv2d(xr, wr, stride=2, padding=3)
+    yr.backward(gy.double())
+    xg, wg = x.to(DEV).requires_grad_(), wt.to(DEV).requires_grad_()
+    y = ops.stem_conv(xg, wg, 2, 3, ops.PackCache(pointwise=True))
+    assert y.shape == yr.shape
+    y.backward(gy.to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 1e-5
+    assert _rel(xg.grad, xr.grad) < 1e-5
+    assert _rel(wg.grad, wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("c,h,w,ceil", [(64, 256, 512, True), (5, 17, 33, True), (3, 16, 16, True),
+                                        (4, 15, 20, False), (2, 7, 9, True)])
+def test_maxpool_bit_exact(c, h, w, ceil):
+    """MaxPool2d(3, 2, 1, ceil_mode) (deeplab_multi.py:77): output, argmax and gradient bit-exact
+    against torch-CPU, with ties (quantised values), NaNs and -inf in the input."""
+    g = torch.Generator().manual_seed(c * h + w)
+    x = torch.relu(torch.randint(-3, 5, (1, c, h, w), generator=g).float())  # many exact ties
+    x.view(-1)[::97] = float("nan")
+    x.view(-1)[5::89] = float("-inf")
+    gy = None
+    xr = x.clone().requires_grad_()
+    yr = F.max_pool2d(xr, 3, 2, 1, ceil_mode=ceil)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy)
+    xg = x.to(DEV).requires_grad_()
+    y = ops.maxpool2d(xg, 3, 2, 1, ceil)
+    y.backward(gy.to(DEV))
+    torch.cuda.synchronize()
+    assert y.shape == yr.shape
+    assert torch.equal(y.cpu().nan_to_num(7.0), yr.detach().nan_to_num(7.0))
+    assert torch.equal(xg.grad.cpu(), xr.grad)
+
+
+def test_subsample_and_strided_pointwise(f32_form):
+    """x[:, :, ::2, ::2] and the stride-2 1x1 convs of layer2.0 (deeplab_multi.py:12-13, 96-99):
+    forward and gradients against fp64 F.conv2d(stride=2)."""
+    from maxsquareloss_amd.graphs.models import deeplab_multi as dm
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(1, 256, 33, 65, generator=g)
+    conv = dm.PointwiseConv(256, 512, stride=2).to(DEV)
+    wt = conv.weight.detach().cpu()
+    xr, wr = x.double().requires_grad_(), wt.double().requires_grad_()
+    yr = F.conv2d(xr, wr, stride=2)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy.double())
+    xg = x.to(DEV).requires_grad_()
+    y = conv(xg)
+    y.backward(gy.to(DEV))
+    torch.cuda.synchronize()
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-5 and _rel(xg.grad, xr.grad) < 1e-5 and _rel(conv.weight.grad, wr.grad) < 1e-5
+    s = ops.subsample(x.to(DEV), 2)
+    assert torch.equal(s.cpu(), x[:, :, ::2, ::2])
