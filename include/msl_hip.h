@@ -187,19 +187,22 @@ int msl_subsample_bwd(const float* dy, int c, int h, int w, int stride, int ho, 
                       msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
- * Operand scales of the f16x3 form (msl_conv_set_f32_form(5)).  Each GEMM operand tensor is
- * scaled by a power of two derived from its absolute maximum, which msl_absmax_partials reduces
- * into msl_absmax_parts() floats.  The plain fp32 entry points compute the partials of their
- * image / gradient operands themselves, once per call; the _sc variants below take them from the
- * caller instead as (pointer, count) - msl_absmax_partials' msl_absmax_parts() floats, or the c
- * per-channel maxima msl_bn_fwd_am / msl_bn_bwd_am wrote for the tensor (NULL = compute) - so a
- * tensor read by two GEMMs (x by the forward and the weight gradient, dy by the data and the
- * weight gradient) is reduced once, or not at all when a BN kernel produced it.  Partials must
- * describe exactly the tensor passed (same contents); a non-NULL pointer needs count >= 1.  The
- * other forms ignore them.
+ * Operand scales of the f16x3 form (msl_conv_set_f32_form(5)).  Each GEMM operand is scaled by a
+ * power of two derived from absolute maxima and split into two fp16 terms.  The maxima come as
+ * PER-ROW partials: msl_absmax_partials writes part[r] = max |x[r][.]| for each of the `rows` rows
+ * (channels) of a [rows][row_len] tensor, and msl_bn_fwd_am / msl_bn_bwd_am write the same per-
+ * channel maxima for the tensor a BN kernel produced.  The plain fp32 entry points reduce them
+ * themselves; the _sc variants below take them from the caller as (pointer, count), count = the
+ * operand's rows (its channels; NULL = compute), so a tensor read by two GEMMs (x by the forward
+ * and the weight gradient, dy by the data and the weight gradient) is reduced once, or not at all
+ * when a BN kernel produced it.  The forward / data gradient scale the image operand by one
+ * tensor-wide power of two (the maximum of the partials: its rows are the GEMM's K index); the
+ * weight gradient scales every row of dY and of x by its own power of two (both are output
+ * indices there), so each dW element keeps the form's full precision even for channels far
+ * below the tensor's maximum.  Partials must describe exactly the tensor passed (same contents).
+ * The other forms ignore them.
  * ---------------------------------------------------------------------- */
-int msl_absmax_parts(void);
-int msl_absmax_partials(const float* x, long long n, float* part, msl_stream_t stream);
+int msl_absmax_partials(const float* x, int rows, int row_len, float* part, msl_stream_t stream);
 int msl_dconv_fwd_sc(const float* x, const float* packed, const float* bias, float* y, int nbranch,
                      int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
                      size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart);

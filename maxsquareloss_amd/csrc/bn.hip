@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(256) k_absmax_rows(const float* __restrict__ t
               __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
-static int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
+int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
   const hipError_t e = hipMemsetAsync(absmax, 0, (size_t)c * sizeof(float), st);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_absmax_rows, dim3(c, cdiv(p, kAbsChunk)), dim3(256), 0, st, t, p, absmax);

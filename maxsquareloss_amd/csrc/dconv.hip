@@ -618,7 +618,7 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
 // the dW^T tiles transposed.
 static bool wgrad_swaps(int nbranch, int taps, int cin, int cout) { return nbranch == 1 && taps == 1 && cout > cin; }
 
-static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P, int w) {
+static size_t wgrad_core_bytes(int nbranch, int taps, int cin, int cout, int P, int w) {
   // large enough for either fp32 form and orientation: pieces, then (k_wgrad_x6) the split planes
   size_t b = 0;
   for (int x6 = 0; x6 < 2; ++x6)
@@ -627,7 +627,12 @@ static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P, in
                         : plan_wgrad(nbranch, taps, cin, cout, P, x6 != 0, w);
       b = std::max(b, wgrad_piece_bytes(pl) + wgrad_planes_bytes(pl));
     }
-  return b + 2 * kPartBytes + 16;  // + (f16x3) both operands' absmax partials
+  return align_up(b, 16);
+}
+
+static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P, int w) {
+  // + (f16x3) both operands' per-row absmax partials when the caller passes none
+  return wgrad_core_bytes(nbranch, taps, cin, cout, P, w) + align_up((size_t)(cin + cout) * 4, 16) + 16;
 }
 
 template <int MT>
@@ -694,30 +699,33 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   if (pl.rx6) {
     bf16x8* planes = reinterpret_cast<bf16x8*>((char*)ws + wgrad_piece_bytes(pl));
     a.dyx6 = planes;
-    if constexpr (F16) {  // both operands' absmax partials, then the scaled split
+    if constexpr (F16) {  // both operands' per-row absmax partials, then the per-row scaled split
       const float* ap = dy_part;
       const float* bp = x_part;
       int an = dy_npart, bn = x_npart;
+      // the caller's partials are one maximum per row (msl_absmax_partials, the BN kernels' per-
+      // channel outputs); none given: reduce them here (after a swap the operands traded places)
+      float* rp = reinterpret_cast<float*>((char*)ws + wgrad_core_bytes(nbranch, taps, cin, cout, P, w));
       if (!ap) {
-        float* w2 = ws_partials(ws, ws_bytes, 2);
-        hipLaunchKernelGGL(k_absmax, dim3(kNPart), block, 0, st, dy, (long long)cout * P, 0LL, 1, w2);
-        MSL_CHECK_LAUNCH();
-        ap = w2;
-        an = kNPart;
+        const int e = absmax_rows(dy, cout, P, rp, st);
+        if (e != MSL_OK) return e;
+        ap = rp;
+        an = cout;
       }
       if (!bp) {
-        float* w1 = ws_partials(ws, ws_bytes, 1);
-        hipLaunchKernelGGL(k_absmax, dim3(kNPart), block, 0, st, x, (long long)cin * P, 0LL, 1, w1);
-        MSL_CHECK_LAUNCH();
-        bp = w1;
-        bn = kNPart;
+        float* r2 = rp + align_up((size_t)cout, 4);
+        const int e = absmax_rows(x, cin, P, r2, st);
+        if (e != MSL_OK) return e;
+        bp = r2;
+        bn = cin;
       }
       a.apart = ap;
       a.bpart = bp;
       a.anpart = an;
       a.bnpart = bn;
+      a.rowscale = (an == cout && bn == cin) ? 1 : 0;
       hipLaunchKernelGGL(k_split_rows<MT>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
-                         pl.KS, pl.lda, planes, ap, an);
+                         pl.KS, pl.lda, planes, ap, an, a.rowscale);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL(k_wgrad_x6<MT>, grid, block, 0, st, a);
     } else {
@@ -944,15 +952,11 @@ int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, i
                  as_stream(stream), 1);
 }
 
-int msl_absmax_parts(void) { return kNPart; }
-
 static bool bad_parts(const float* p, int n) { return p && n < 1; }
 
-int msl_absmax_partials(const float* x, long long n, float* part, msl_stream_t stream) {
-  if (!x || !part || n < 0) return MSL_ERR_ARG;
-  hipLaunchKernelGGL(k_absmax, dim3(kNPart), dim3(256), 0, as_stream(stream), x, n, 0LL, 1, part);
-  MSL_CHECK_LAUNCH();
-  return MSL_OK;
+int msl_absmax_partials(const float* x, int rows, int row_len, float* part, msl_stream_t stream) {
+  if (!x || !part || rows < 1 || row_len < 1) return MSL_ERR_ARG;
+  return absmax_rows(x, rows, row_len, part, as_stream(stream));
 }
 
 int msl_dconv_fwd_sc(const float* x, const float* packed, const float* bias, float* y, int nbranch,

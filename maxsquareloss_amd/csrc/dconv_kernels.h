@@ -1614,6 +1614,12 @@ struct WskArgs {
   const float* apart;
   const float* bpart;
   int anpart, bnpart;  // partials in apart / bpart
+  // rowscale = 1: apart / bpart hold one maximum per row of their operand (anpart = M, bnpart = N),
+  // and every row gets its own power-of-two scale: k_split_rows scales dY row m by s_m,
+  // k_wgrad_x6 scales X row n by t_n, and k_wsk_reduce unscales dW[m][n] by 1/(s_m t_n) (exact).
+  // Each dW element then keeps the full f16x3 precision of its own rows however far they sit below
+  // the tensor's absolute maximum.  rowscale = 0: one scale per tensor (max over the partials).
+  int rowscale;
 };
 
 constexpr int kWskBK = 64;
@@ -1808,10 +1814,20 @@ __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
         if (a.nchunk > 0) return part[(long long)(wc * a.ntiles + t) * a.slots * P4 + g4];
         return part[(long long)(wc * a.slots + t - sk_start(wc, a.T, a.NW) / a.KS) * P4 + g4];
       });
-      tt[r][c4] = v.x;
-      tt[r][c4 + 1] = v.y;
-      tt[r][c4 + 2] = v.z;
-      tt[r][c4 + 3] = v.w;
+      float sv[4] = {v.x, v.y, v.z, v.w};
+      if (a.rowscale) {  // tile element (m, n): 1 / (s_m t_n), exact
+        float ia, ib;
+        pow2_scale(a.apart[min(a.M - 1, tm * BM + sr * 32 + r)], ia);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pow2_scale(a.bpart[min(a.N - 1, tn * BN + sc * 32 + c4 + q)], ib);
+          sv[q] = sv[q] * ia * ib;
+        }
+      }
+      tt[r][c4] = sv[0];
+      tt[r][c4 + 1] = sv[1];
+      tt[r][c4 + 2] = sv[2];
+      tt[r][c4 + 3] = sv[3];
       __syncthreads();
       // thread -> dW row n = n0 + sc*32 + (tid >> 3) (a cout), columns m = m0 + sr*32 + rr .. + 3
       const int n = tn * BN + sc * 32 + (threadIdx.x >> 3), rr = (threadIdx.x & 7) * 4;
@@ -1853,6 +1869,15 @@ __global__ void __launch_bounds__(256) k_wsk_reduce(WskArgs a) {
   float* dst = a.dw + br * a.cbranch + ((long long)m * a.N + n) * a.taps + tap;
   float vals[4] = {v.x, v.y, v.z, v.w};
   const int nn = min(4, a.N - n);
+  if (a.rowscale) {  // per-row f16x3 scales (k_wgrad_x6): dW[m][n] / (s_m t_n), exact
+    float ia, ib;
+    pow2_scale(a.apart[m], ia);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      pow2_scale(a.bpart[min(a.N - 1, n + c)], ib);
+      vals[c] = vals[c] * ia * ib;
+    }
+  }
   if (a.accumulate) {  // all old values loaded before the first store
     float old[4];
 #pragma unroll
@@ -1959,7 +1984,7 @@ constexpr int kWx6BK = 16;
 template <int MT = kMathX6>
 __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ src, int M, int P, int KS, int lda,
                                                      bf16x8* __restrict__ planes, const float* __restrict__ part,
-                                                     int npart) {
+                                                     int npart, int rowscale = 0) {
   constexpr int R = 64, LDP = 72;  // rows per block, LDS row stride in 16-bit terms (64 pixels + 8)
   constexpr bool F16 = MT == kMathH3P || MT == kMathH1P;
   constexpr int NP = MT == kMathH1P ? 1 : F16 ? 2 : 3;
@@ -1969,20 +1994,26 @@ __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ sr
   const int p = ks0 * kWx6BK + lane;
   const bool pin = p < P;
   float sc = 1.f, inv;
-  if constexpr (F16) sc = pow2_scale(partials_max(part, npart, lane), inv);
+  if constexpr (F16) {
+    if (!rowscale) sc = pow2_scale(partials_max(part, npart, lane), inv);
+  }
   float v[R / 4];
 #pragma unroll
   for (int i = 0; i < R / 4; ++i) {
     const int m = m0 + wv + 4 * i;
     v[i] = (pin && m < M) ? src[(long long)m * P + p] : 0.f;
+    if constexpr (F16) {  // the row's own scale (its maximum: one partial per row)
+      if (rowscale) v[i] *= m < M ? pow2_scale(part[m], inv) : 1.f;
+      else v[i] *= sc;
+    }
   }
 #pragma unroll
   for (int i = 0; i < R / 4; ++i) {
     const int r = wv + 4 * i;
     if constexpr (MT == kMathH1P) {
-      tile[r * LDP + lane] = __builtin_bit_cast(unsigned short, (_Float16)(v[i] * sc));
+      tile[r * LDP + lane] = __builtin_bit_cast(unsigned short, (_Float16)v[i]);
     } else if constexpr (MT == kMathH3P) {
-      const float x = v[i] * sc;
+      const float x = v[i];
       const _Float16 h = (_Float16)x;
       const _Float16 l = (_Float16)(x - (float)h);
       tile[(0 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, h);
@@ -2046,9 +2077,12 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       (void*)a.dyx6, (short)0, (int)min(0x7fffffffLL, (long long)a.KS * 2 * NP * a.lda * 16), 0x00020000);
   float sX = 1.f, iA = 1.f, iB = 1.f;
   if constexpr (H3) {
-    sX = pow2_scale(partials_max(a.bpart, a.bnpart, lane), iB);
-    pow2_scale(partials_max(a.apart, a.anpart, lane), iA);
+    if (!a.rowscale) {
+      sX = pow2_scale(partials_max(a.bpart, a.bnpart, lane), iB);
+      pow2_scale(partials_max(a.apart, a.anpart, lane), iA);
+    }
   }
+  float sXr[4] = {sX, sX, sX, sX};  // the scales of this thread's four B rows (per tile with rowscale)
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.x, (short)0, (int)min(0x7fffffffLL, (long long)a.N * a.P * 4), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
@@ -2095,6 +2129,16 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       if (cx >= a.W) { cx -= a.W; ++cy; }
       return m16;
     };
+    if constexpr (H3) {
+      if (a.rowscale) {
+        float iv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = n0 + (tid >> 3) + 32 * i;
+          sXr[i] = n < a.N ? pow2_scale(a.bpart[n], iv) : 1.f;
+        }
+      }
+    }
     float rbv[16];
     auto loadB = [&]() {  // the stage's two K-steps (a missing second one is all-masked)
       const int ks0 = ld_ks;
@@ -2125,7 +2169,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
         for (int i = 0; i < 4; ++i) {
           f16x4 hi;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) hi[j] = (_Float16)(rbv[4 * i + j] * sX);
+          for (int j = 0; j < 4; ++j) hi[j] = (_Float16)(rbv[4 * i + j] * sXr[i]);
           *reinterpret_cast<f16x4*>(base + i * 32 * 16) = hi;
         }
         return;
@@ -2135,7 +2179,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
           f16x4 hi, lo;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float v = rbv[4 * i + j] * sX;
+            const float v = rbv[4 * i + j] * sXr[i];
             const _Float16 h = (_Float16)v;
             hi[j] = h;
             lo[j] = (_Float16)(v - (float)h);
@@ -2255,7 +2299,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       if (more) storeB((s + 1) & 1);
       __syncthreads();
     }
-    if constexpr (H3) {  // exact: both factors are powers of two
+    if (H3 && !a.rowscale) {  // exact: both factors are powers of two (rowscale: in k_wsk_reduce)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll

@@ -34,4 +34,8 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// absmax[r] = max |t[r][0..p)| for r < c (bn.hip; stream-ordered memset + one launch, integer
+// atomicMax on the float bits: exact and order-independent).  The f16x3 convs' per-row partials.
+int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st);
+
 }  // namespace msl

@@ -43,8 +43,7 @@ SIGNATURES = {
     "msl_pconv_dgrad_acc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_wgrad_workspace": (c_sz, [c_int] * 3),
     "msl_pconv_wgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
-    "msl_absmax_parts": (c_int, []),
-    "msl_absmax_partials": (c_int, [c_p, c_ll, c_p, c_p]),
+    "msl_absmax_partials": (c_int, [c_p, c_int, c_int, c_p, c_p]),
     "msl_dconv_fwd_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_dconv_dgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_dconv_wgrad_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),

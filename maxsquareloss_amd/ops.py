@@ -84,10 +84,10 @@ def _tag_absmax(t, part):
 
 
 def _parts(t, math="fp32", compute=True):
-    """The absmax partials of an operand tensor for the f16x3 form, as (tensor, count): the ones the
-    BN kernel that produced `t` wrote (msl_bn_fwd_am / msl_bn_bwd_am: one per channel, no pass of
-    their own), else - when `compute` - msl_absmax_partials, so that a tensor two GEMMs read (x:
-    forward and weight gradient; dy: data and weight gradient) is reduced once.  None in the other
+    """The per-channel absmax partials of an operand tensor for the f16x3 form, as (tensor, count =
+    channels): the ones the BN kernel that produced `t` wrote (msl_bn_fwd_am / msl_bn_bwd_am, no
+    pass of their own), else - when `compute` - msl_absmax_partials, so that a tensor two GEMMs read
+    (x: forward and weight gradient; dy: data and weight gradient) is reduced once.  None in the other
     forms (the kernels ignore them), or when not worth a launch (the entry point then reduces the
     operand itself if its kernel needs it)."""
     if not _h3(math):
@@ -98,10 +98,11 @@ def _parts(t, math="fp32", compute=True):
     if not compute:
         return None
     lib = hip.load()
-    part = torch.empty(lib.msl_absmax_parts(), dtype=_f32, device=t.device)
-    hip.check(lib.msl_absmax_partials(t.data_ptr(), t.numel(), part.data_ptr(), hip.stream_ptr()),
+    rows = t.size(1)
+    part = torch.empty(rows, dtype=_f32, device=t.device)
+    hip.check(lib.msl_absmax_partials(t.data_ptr(), rows, t.numel() // rows, part.data_ptr(), hip.stream_ptr()),
               "msl_absmax_partials")
-    return part, part.numel()
+    return part, rows
 
 
 def _pp(q):

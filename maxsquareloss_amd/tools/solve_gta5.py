@@ -51,6 +51,8 @@ class UDATrainer(Trainer):
         self._reset_meters()
         self.use_graph = bool(getattr(self.args, "graph", False))
         self._graphed = None
+        self.overlap = bool(getattr(self.args, "overlap", True))
+        self._side = None
 
     def _reset_meters(self):
         # zeroed in place once they exist: a captured step (utils/graph.py) adds into these tensors
@@ -115,10 +117,32 @@ class UDATrainer(Trainer):
         self.current_iter += 1
 
     def _uda_grads(self, x_s, y_s, x_t):
+        if not self.overlap:
+            pred = self.model(x_s)
+            self.train_source(pred, y_s)
+            pred = self.model(x_t)
+            self.train_target(pred)
+            return
+        # The target forward depends on neither the source backward nor its gradients (the weights
+        # change only at the optimizer step; BN running statistics are updated by the forwards, in
+        # the reference's order: source, then target), so it runs on a side stream concurrently with
+        # the source backward.  The target backward (autograd runs it on the stream of its forward)
+        # accumulates into the same gradient buffer: it waits for the source backward first, and the
+        # main stream waits for it before the optimizer step.  Same kernels, same operands, same
+        # order per buffer: the results are bit-identical to the sequential order.
+        main = torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        side = self._side
         pred = self.model(x_s)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            pred_t = self.model(x_t)
         self.train_source(pred, y_s)
-        pred = self.model(x_t)
-        self.train_target(pred)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.train_target(pred_t)
+        main.wait_stream(side)
 
     def _uda_update(self):
         self.optimizer.step()
@@ -189,6 +213,9 @@ def add_UDA_train_args(arg_parser):
     a("--IW_ratio", type=float, default=0.2)
     a("--threshold", type=float, default=0.95)
     a("--target_solo_epoch", type=int, default=0)
+    a("--overlap", type=str2bool, default=True,
+      help="run the target forward on a side stream concurrently with the source backward (same "
+           "results; not in the reference, whose loop is sequential)")
     a("--graph", type=str2bool, default=False,
       help="replay each iteration after the first as one captured hipGraph (single process; not in the "
            "reference, whose loop is eager)")

@@ -664,7 +664,7 @@ def test_sk_hybrid_schedule(cin, cout, h, w, f32_form):
 def test_pconv_wgrad_accumulate_both_orientations(cin, cout, h, w, form):
     """msl_pconv_wgrad, accumulate = 1, in both split forms: with cout > cin the kernel runs on the
     swapped operands (the image pre-split, dW^T tiles transposed by the reduce); either way
-    dW += dy x^T.  f16x3: msl_pconv_wgrad_sc given the operands' absmax partials
+    dW += dy x^T.  f16x3: msl_pconv_wgrad_sc given the operands' per-row absmax partials
     (msl_absmax_partials) writes exactly the bytes of the plain call, which reduces them itself."""
     from maxsquareloss_amd import hip
     lib = hip.load()
@@ -684,14 +684,13 @@ def test_pconv_wgrad_accumulate_both_orientations(cin, cout, h, w, form):
         torch.cuda.synchronize()
         assert _rel(dw, ref) < 1e-5
         if form == "f16x3":
-            np_ = lib.msl_absmax_parts()
-            xp, gp = torch.empty(np_, device=DEV), torch.empty(np_, device=DEV)
-            for t, q in ((xd, xp), (gd, gp)):
-                assert lib.msl_absmax_partials(t.data_ptr(), t.numel(), q.data_ptr(), hip.stream_ptr()) == 0
-            assert xp.max().item() == x.abs().max().item() and gp.max().item() == gy.abs().max().item()
+            xp, gp = torch.empty(cin, device=DEV), torch.empty(cout, device=DEV)
+            for t, q, rows in ((xd, xp, cin), (gd, gp, cout)):
+                assert lib.msl_absmax_partials(t.data_ptr(), rows, p, q.data_ptr(), hip.stream_ptr()) == 0
+            assert torch.equal(xp.cpu(), x.abs().amax(1)) and torch.equal(gp.cpu(), gy.abs().amax(1))  # per row
             dw2 = dw0.to(DEV)
             assert lib.msl_pconv_wgrad_sc(xd.data_ptr(), gd.data_ptr(), dw2.data_ptr(), cin, cout, p, 1, ws.data_ptr(),
-                                          wsb, hip.stream_ptr(), xp.data_ptr(), np_, gp.data_ptr(), np_) == 0
+                                          wsb, hip.stream_ptr(), xp.data_ptr(), cin, gp.data_ptr(), cout) == 0
             torch.cuda.synchronize()
             assert torch.equal(dw2, dw)
     finally:
@@ -732,6 +731,52 @@ def test_f16x3_is_fp32_accurate(cin, cout, h, w, d, xs, gs):
             xg = x.to(DEV).requires_grad_()
             wg = wt.to(DEV).requires_grad_()
             y = ops.dconv3x3(xg, wg, d, ops.PackCache())
+            y.backward(gy.to(DEV))
+            torch.cuda.synchronize()
+            errs[form] = (_elem_err(y, yr, ya), _elem_err(xg.grad, xr.grad, xa.grad),
+                          _elem_err(wg.grad, wr.grad, wa.grad))
+        finally:
+            ops.set_f32_form(prev)
+    for i, what in enumerate(("fwd", "dgrad", "wgrad")):
+        e, ref = errs["f16x3"][i], errs["mfma_f32"][i]
+        assert e < 2e-7 and e <= 2.0 * max(ref, 1e-8), (what, errs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,cin,cout,h,w", [("3x3", 256, 256, 33, 65), ("1x1", 256, 1024, 33, 65),
+                                               ("1x1", 1024, 256, 33, 65), ("3x3", 512, 512, 17, 33)])
+def test_f16x3_channel_spread_accuracy(kind, cin, cout, h, w):
+    """with one power-of-two scale per tensor, a channel far below the tensor's absolute
+    maximum loses its lo term to fp16 subnormals.  Here every channel of x and of dy gets its own
+    scale, log-uniform over 1e-8 .. 1 (per-channel spread within one tensor), and each output
+    element's error against fp64, relative to its own sum of |terms|, must stay within 2x the exact
+    fp32 MFMA's and below 2e-7 - forward, data and weight gradients (the 1x1 shapes include the
+    swapped-operand weight gradient, cout > cin).  The weight gradient's output rows / columns ARE
+    the channels, so it scales every row of dY and of x by its own power of two (rowscale); the
+    forward and data gradient sum over channels, where a tiny channel's terms are tiny in the
+    element's sum too."""
+    g = torch.Generator().manual_seed(cin * 5 + cout + h)
+    k = 3 if kind == "3x3" else 1
+    d = 2 if k == 3 else 0
+    cs = 10.0 ** (-8.0 * torch.rand(cin, generator=g))
+    gsc = 10.0 ** (-8.0 * torch.rand(cout, generator=g))
+    x = torch.relu(torch.randn(1, cin, h, w, generator=g)) * cs.view(1, cin, 1, 1)
+    wt = torch.randn(cout, cin, k, k, generator=g) * 0.01
+    gy = torch.randn(1, cout, h, w, generator=g) * gsc.view(1, cout, 1, 1)
+    conv = (lambda a, b: F.conv2d(a, b, padding=d, dilation=d)) if k == 3 else (lambda a, b: F.conv2d(a, b))
+    xr, wr = x.double().requires_grad_(), wt.double().requires_grad_()
+    conv(xr, wr).backward(gy.double())
+    xa, wa = x.double().abs().requires_grad_(), wt.double().abs().requires_grad_()
+    ya = conv(xa, wa)
+    ya.backward(gy.double().abs())
+    yr = conv(x.double(), wt.double())
+    errs = {}
+    for form in ("mfma_f32", "f16x3"):
+        prev = ops.set_f32_form(form)
+        try:
+            xg, wg = x.to(DEV).requires_grad_(), wt.to(DEV).requires_grad_()
+            y = (ops.dconv3x3(xg, wg, d, ops.PackCache()) if k == 3 else
+                 ops.pconv(xg, wg, ops.PackCache(pointwise=True)))
             y.backward(gy.to(DEV))
             torch.cuda.synchronize()
             errs[form] = (_elem_err(y, yr, ya), _elem_err(xg.grad, xr.grad, xa.grad),
