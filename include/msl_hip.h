@@ -72,6 +72,11 @@ int msl_conv_set_pack_form(int form);
  * workgroups, whole rounds of tiles run data-parallel and only the remainder is split stream-K
  * (default); 0 = pure stream-K (every tile range-split over 512 workgroups). */
 int msl_conv_set_sk_hybrid(int on);
+/* Kernel-variant switch for same-box A/B measurements of alternative kernel forms (process-wide,
+ * read at launch; identical results up to fp32 summation order): 0 = the default forms; bit 0 =
+ * the weight gradient's dY fragments prefetched three K-steps ahead (k_wgrad_x6 PIPE 1).
+ * MSL_ERR_ARG for a negative value. */
+int msl_conv_set_variant(int variant);
 
 /* ------------------------------------------------------------------------
  * Dilated 3x3 convolution, stride 1, padding = dilation, as an FP32-MFMA

@@ -244,6 +244,9 @@ static int g_sk_hybrid = 1;
 // 4e-8 vs 6e-8 relative to sum|terms|), kMathH3P the scaled two-way fp16 split (three fp16
 // MFMAs per slice; dconv_kernels.h Split2h).  Process-wide; packs are form-specific.
 static int g_f32_form = kMathH3P;
+// Kernel-variant switch for same-box A/B of alternative kernel forms (msl_conv_set_variant; bit 0:
+// k_wgrad_x6 with the 3-ahead dY fragment ring).  Process-wide, read at launch.
+static int g_variant = 0;
 constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
 
 struct FwdPlan {
@@ -727,7 +730,10 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
       hipLaunchKernelGGL(k_split_rows<MT>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, ap, an, a.rowscale);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_wgrad_x6<MT>, grid, block, 0, st, a);
+      if (g_variant & 1)
+        hipLaunchKernelGGL((k_wgrad_x6<MT, 1>), grid, block, 0, st, a);
+      else
+        hipLaunchKernelGGL((k_wgrad_x6<MT, 0>), grid, block, 0, st, a);
     } else {
       hipLaunchKernelGGL(k_split_rows<kMathX6>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, (const float*)nullptr, 0);
@@ -794,6 +800,12 @@ int msl_conv_set_f32_form(int form) {
 }
 
 int msl_conv_f32_form(void) { return g_f32_form; }
+
+int msl_conv_set_variant(int v) {
+  if (v < 0) return MSL_ERR_ARG;
+  g_variant = v;
+  return MSL_OK;
+}
 
 int msl_conv_set_sk_hybrid(int on) {
   if (on != 0 && on != 1) return MSL_ERR_ARG;

@@ -2043,7 +2043,10 @@ __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ sr
 // MT = kMathH3P (f16x3): dY (the pre-split operand) as two fp16 planes scaled by k_split_rows<H3>,
 // X scaled by its own pow2_scale (absmax partials bpart) and split into two fp16 planes; the
 // pieces are unscaled by both before they are stored.
-template <int MT = kMathX6>
+// PIPE = 1 (r03): the dY fragments come from a ring of four register sets, loaded three K-steps
+// ahead of their MFMAs instead of one (one K-step is only 12 MFMAs = ~0.17 us per wave, less than an
+// L2 round trip), the stage loop unrolled by two so every ring slot is a static register set.
+template <int MT = kMathX6, int PIPE = 0>
 __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
   constexpr bool H1 = MT == kMathH1P;  // fp16 math: the hi planes only
   constexpr bool H3 = MT == kMathH3P || H1;
@@ -2278,6 +2281,36 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __syncthreads();  // the previous segment's LDS reads are complete in every wave
+    if constexpr (PIPE == 1) {
+      u32x4 A2[TM][NP], A3[TM][NP];
+      loadB();
+      loadA(A0, k_a);
+      if (k_a + 1 < k_b) loadA(A1, k_a + 1);
+      if (k_a + 2 < k_b) loadA(A2, k_a + 2);
+      storeB(0);
+      __syncthreads();
+      // stage s: K-steps k_a + 2s (ring slot 2s % 4) and k_a + 2s + 1; each K-step i first issues the
+      // load of K-step i + 3 into the slot K-step i - 1 freed
+      auto stage = [&](int s, u32x4 (&Ra)[TM][NP], u32x4 (&Rb)[TM][NP], u32x4 (&Rl)[TM][NP]) {
+        const int left = nst - 2 * s;
+        const bool more = left > 2;
+        const int i = k_a + 2 * s;
+        if (more) loadB();
+        const char* Bs = smem + (s & 1) * STAGEB;
+        if (i + 3 < k_b) loadA(Rl, i + 3);
+        compute(Bs, Ra);
+        if (left > 1) {
+          if (i + 4 < k_b) loadA(Ra, i + 4);
+          compute(Bs + KVB, Rb);
+        }
+        if (more) storeB((s + 1) & 1);
+        __syncthreads();
+      };
+      for (int s = 0; 2 * s < nst; s += 2) {
+        stage(s, A0, A1, A3);
+        if (2 * (s + 1) < nst) stage(s + 1, A2, A3, A1);
+      }
+    } else {
     loadB();
     loadA(A0, k_a);
     storeB(0);
@@ -2298,6 +2331,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       }
       if (more) storeB((s + 1) & 1);
       __syncthreads();
+    }
     }
     if (H3 && !a.rowscale) {  // exact: both factors are powers of two (rowscale: in k_wsk_reduce)
 #pragma unroll

@@ -28,6 +28,7 @@ SIGNATURES = {
     "msl_conv_set_f32_form": (c_int, [c_int]),
     "msl_conv_f32_form": (c_int, []),
     "msl_conv_set_sk_hybrid": (c_int, [c_int]),
+    "msl_conv_set_variant": (c_int, [c_int]),
     "msl_conv_set_pack_form": (c_int, [c_int]),
     "msl_dconv_fwd": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_dgrad_workspace": (c_sz, [c_int] * 5),

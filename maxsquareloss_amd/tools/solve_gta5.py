@@ -133,6 +133,9 @@ class UDATrainer(Trainer):
         main = torch.cuda.current_stream(self.device)
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device)
+            # the ASPP parameters' AccumulateGrad nodes were made on the main stream: their
+            # accumulation after the side-stream target backward syncs to it, as intended
+            torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
         side = self._side
         pred = self.model(x_s)
         side.wait_stream(main)

@@ -1,0 +1,127 @@
+"""Per-op timing of the conv GEMMs at the step's 1024x512 shapes (GPU), for same-box A/B of kernel forms.
+
+    python scripts/bench_ops.py [--variant K ...] [--reps N] [--check]
+
+Each op call (the C-ABI entry point as ops.py issues it, incl. its reduce and split launches) is timed
+with HIP events over `reps` back-to-back calls after warm-up, on f16x3 (the default fp32 form).  With
+--variant, the library's experiment switch (msl_conv_set_variant) is set to each value in turn and
+every op is re-timed, so variants compare on one box within one process.  --check also compares each
+variant's outputs against fp64 (per-element error relative to the sum of |terms|).
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from maxsquareloss_amd import hip, ops  # noqa: E402
+
+DEV = "cuda"
+H, W = 65, 129
+
+
+def timed(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3  # us
+
+
+def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W):
+    """(label, fwd, dgrad, wgrad callables, flops, reference checker) for one conv shape."""
+    g = torch.Generator().manual_seed(cin + cout)
+    x = torch.relu(torch.randn(1, cin, h, w, generator=g)).to(DEV)
+    wt = (torch.randn(cout, cin, k, k, generator=g) * 0.02).to(DEV)
+    gy = torch.randn(1, cout, h, w, generator=g).to(DEV)
+    lib = hip.load()
+    s = hip.stream_ptr()
+    p = h * w
+    cnt = hip.counters(x.device).data_ptr()
+    cache = ops.PackCache(pointwise=(k == 1))
+    xpart = ops._parts(x)
+    gpart = ops._parts(gy)
+    y = torch.empty(1, cout, h, w, device=DEV)
+    dx = torch.empty(1, cin, h, w, device=DEV)
+    dw = torch.empty_like(wt)
+    if k == 1:
+        pf, pd = cache.get([wt], cin, cout, 0), cache.get([wt], cin, cout, 1)
+        wsf = hip.workspace(lib.msl_pconv_fwd_workspace(cin, cout, p), DEV)
+        wsd = hip.workspace(lib.msl_pconv_dgrad_workspace(cin, cout, p), DEV)
+        wsw = hip.workspace(lib.msl_pconv_wgrad_workspace(cin, cout, p), DEV)
+        fwd = lambda: hip.check(lib.msl_pconv_fwd_sc(x.data_ptr(), pf.data_ptr(), y.data_ptr(), cin, cout, p, cnt,  # noqa: E731
+                                                     wsf.data_ptr(), wsf.numel(), s, *ops._pp(xpart)), "fwd")
+        dgr = lambda: hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), pd.data_ptr(), dx.data_ptr(), cin, cout, p,  # noqa: E731
+                                                           0, cnt, wsd.data_ptr(), wsd.numel(), s, *ops._pp(gpart)), "dgrad")
+        wgr = lambda: hip.check(lib.msl_pconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), cin, cout, p, 0,  # noqa: E731
+                                                       wsw.data_ptr(), wsw.numel(), s, *ops._pp(xpart),
+                                                       *ops._pp(gpart)), "wgrad")
+        ref = lambda xx, ww: F.conv2d(xx, ww)  # noqa: E731
+    else:
+        pf, pd = cache.get([wt], cin, cout, 0), cache.get([wt], cin, cout, 1)
+        wsf = hip.workspace(lib.msl_dconv_fwd_workspace(1, cin, cout, h, w), DEV)
+        wsd = hip.workspace(lib.msl_dconv_dgrad_workspace(1, cin, cout, h, w), DEV)
+        wsw = hip.workspace(lib.msl_dconv_wgrad_workspace(1, cin, cout, h, w), DEV)
+        fwd = lambda: hip.check(lib.msl_dconv_fwd_sc(x.data_ptr(), pf.data_ptr(), None, y.data_ptr(), 1, cin, cout,  # noqa: E731
+                                                     h, w, d, 0, cnt, wsf.data_ptr(), wsf.numel(), s,
+                                                     *ops._pp(xpart)), "fwd")
+        dgr = lambda: hip.check(lib.msl_dconv_dgrad_sc(gy.data_ptr(), pd.data_ptr(), dx.data_ptr(), 1, cin, cout, h,  # noqa: E731
+                                                       w, d, 0, cnt, wsd.data_ptr(), wsd.numel(), s,
+                                                       *ops._pp(gpart)), "dgrad")
+        wgr = lambda: hip.check(lib.msl_dconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), None, 1, cin,  # noqa: E731
+                                                       cout, h, w, d, 0, 0, wsw.data_ptr(), wsw.numel(), s,
+                                                       *ops._pp(xpart), *ops._pp(gpart)), "wgrad")
+        ref = lambda xx, ww: F.conv2d(xx, ww, padding=d, dilation=d)  # noqa: E731
+    flops = 2.0 * cin * cout * k * k * p
+
+    def check():
+        xr, wr = x.double().cpu().requires_grad_(), wt.double().cpu().requires_grad_()
+        yr = ref(xr, wr)
+        yr.backward(gy.double().cpu())
+        xa, wa = x.double().cpu().abs().requires_grad_(), wt.double().cpu().abs().requires_grad_()
+        ya = ref(xa, wa)
+        ya.backward(gy.double().cpu().abs())
+        fwd(); dgr(); wgr()  # noqa: E702
+        torch.cuda.synchronize()
+        e = lambda o, r, b: ((o.double().cpu() - r).abs() / b.clamp_min(1e-300)).max().item()  # noqa: E731
+        return e(y, yr.detach(), ya.detach()), e(dx, xr.grad, xa.grad), e(dw, wr.grad, wa.grad)
+    return name, fwd, dgr, wgr, flops, check
+
+
+SHAPES = [("layer3 3x3 d2", 256, 256, 3, 2), ("layer4 3x3 d4", 512, 512, 3, 4), ("layer2 3x3", 128, 128, 3, 1),
+          ("1x1 256->1024", 256, 1024, 1, 0), ("1x1 1024->256", 1024, 256, 1, 0), ("1x1 2048->512", 2048, 512, 1, 0),
+          ("1x1 512->2048", 512, 2048, 1, 0)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", type=int, nargs="*", default=[0])
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--only", default=None, help="substring of the shape names to run")
+    a = ap.parse_args()
+    lib = hip.load()
+    ops_list = [conv_ops(*s) for s in SHAPES if a.only is None or a.only in s[0]]
+    for v in a.variant:
+        if hasattr(lib, "msl_conv_set_variant"):
+            hip.check(lib.msl_conv_set_variant(v), "msl_conv_set_variant")
+        for name, fwd, dgr, wgr, flops, check in ops_list:
+            t = [timed(f, a.reps) for f in (fwd, dgr, wgr)]
+            rec = {"variant": v, "op": name, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
+                   "wgrad_us": round(t[2], 1), "fwd_tf": round(flops / t[0] / 1e6, 1),
+                   "wgrad_tf": round(flops / t[2] / 1e6, 1)}
+            if a.check:
+                rec["err_fwd_dgrad_wgrad"] = [float(f"{e:.2e}") for e in check()]
+            print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

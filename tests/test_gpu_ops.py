@@ -750,7 +750,7 @@ def test_f16x3_channel_spread_accuracy(kind, cin, cout, h, w):
     maximum loses its lo term to fp16 subnormals.  Here every channel of x and of dy gets its own
     scale, log-uniform over 1e-8 .. 1 (per-channel spread within one tensor), and each output
     element's error against fp64, relative to its own sum of |terms|, must stay within 2x the exact
-    fp32 MFMA's and below 2e-7 - forward, data and weight gradients (the 1x1 shapes include the
+    fp32 MFMA's (and below 1e-6) - forward, data and weight gradients (the 1x1 shapes include the
     swapped-operand weight gradient, cout > cin).  The weight gradient's output rows / columns ARE
     the channels, so it scales every row of dY and of x by its own power of two (rowscale); the
     forward and data gradient sum over channels, where a tiny channel's terms are tiny in the
@@ -785,7 +785,7 @@ def test_f16x3_channel_spread_accuracy(kind, cin, cout, h, w):
             ops.set_f32_form(prev)
     for i, what in enumerate(("fwd", "dgrad", "wgrad")):
         e, ref = errs["f16x3"][i], errs["mfma_f32"][i]
-        assert e < 2e-7 and e <= 2.0 * max(ref, 1e-8), (what, errs)
+        assert e < 1e-6 and e <= 2.0 * max(ref, 1e-8), (what, errs)
 
 
 @pytest.mark.gpu
