@@ -74,7 +74,9 @@ int msl_conv_set_pack_form(int form);
 int msl_conv_set_sk_hybrid(int on);
 /* Kernel-variant switch for same-box A/B measurements of alternative kernel forms (process-wide,
  * read at launch; identical results up to fp32 summation order): 0 = the default forms; bit 0 =
- * the weight gradient's dY fragments prefetched three K-steps ahead (k_wgrad_x6 PIPE 1).
+ * the weight gradient's dY fragments prefetched three K-steps ahead (k_wgrad_x6 PIPE 1); bit 1 =
+ * the 3x3 / ASPP forward-form GEMMs on <= 64-row tiles run their K-steps channel-block-major
+ * (the taps of one channel block back to back: L2 reuse of the shifted image reads).
  * MSL_ERR_ARG for a negative value. */
 int msl_conv_set_variant(int variant);
 

@@ -245,7 +245,8 @@ static int g_sk_hybrid = 1;
 // MFMAs per slice; dconv_kernels.h Split2h).  Process-wide; packs are form-specific.
 static int g_f32_form = kMathH3P;
 // Kernel-variant switch for same-box A/B of alternative kernel forms (msl_conv_set_variant; bit 0:
-// k_wgrad_x6 with the 3-ahead dY fragment ring).  Process-wide, read at launch.
+// k_wgrad_x6 with the 3-ahead dY fragment ring; bit 1: the tap-inner K order of the <= 64-row
+// exact-f32 forward tiles).  Process-wide, read at launch.
 static int g_variant = 0;
 constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
 
@@ -396,6 +397,16 @@ static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials 
 template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
+    if constexpr (BM == 128 && G == 1 && ST == 4 && WM == 1 && WN == 4) {
+      if (g_variant & 4) {  // the image operand straight to registers (BD form)
+        if (accum)
+          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a, sk);
+        else
+          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true>), grid, block, 0, st, a,
+                             sk);
+        return;
+      }
+    }
     if (accum)
       hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true>), grid, block, 0, st, a, sk);
     else
@@ -453,6 +464,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   a.kps = pl.kps;
   a.taps = taps;
   a.slab = (long long)M * P;
+  // the exact-f32 (<= 64-row) stream-K tiles of the 3x3 / ASPP convs: channel-block-major K order
+  // (FwdArgs::tapinner; variant bit 1 while it is measured)
+  a.tapinner = (pl.sk && taps == 9 && pl.bm <= 64 && (g_variant & 2)) ? 1 : 0;
   if (pl.sk) {
     if (!counters) return MSL_ERR_ARG;
     if ((long long)pl.tiles_m * pl.tiles_n > kMaxCounters) return MSL_ERR_SHAPE;

@@ -29,6 +29,11 @@ struct FwdArgs {
   const float* ascale;
   const float* bpart;
   int bnpart;  // partials in bpart
+  // tapinner = 1 (exact-f32 stream-K forms, r03): the K-steps run channel-block-major with the
+  // (branch, tap) index fastest, (cb, z) -> packed K-step z*ncb + cb, so the 9 (or 18) shifted reads
+  // of one 16-channel block follow each other and hit L2, instead of re-streaming the whole image
+  // once per tap (the 19-class ASPP forward moved 1.16 GB per launch for a 69 MB input, r02).
+  int tapinner;
 };
 
 struct WgradArgs {
@@ -505,6 +510,43 @@ __device__ __forceinline__ void mfma_stage_h1p(const float* __restrict__ As, con
   }
 }
 
+// f16x3 / fp16 stage with the B operand in registers (fwd_sk_body's BD form, r03): braw = this lane's
+// 8 image values B[k = 8h .. 8h+7][n = its pixel] of the K-step, loaded from global memory a few
+// K-steps ahead; A fragments from the LDS ring as in mfma_stage_h3p.  One K-step, one 32-pixel column
+// per wave (1 x 4 waves).
+template <int TM, int BM, bool HI_ONLY, typename F>
+__device__ __forceinline__ void mfma_stage_hd(const float* __restrict__ As, int wm, int lane, f32x16 (&acc)[TM][1],
+                                              F&& mid, float sB, const float (&braw)[8]) {
+  const int l32 = lane & 31, h = lane >> 5;
+  const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
+  if constexpr (HI_ONLY) {
+    f16x8 av[TM], bv;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bv[j] = (_Float16)(braw[j] * sB);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bv, acc[i][0], 0, 0, 0);
+  } else {
+    Split2h av[TM], bv;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i].lo = Ab[(2 + h) * BM + wm + i * 32 + l32];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split2h_set(bv, j, braw[j] * sB);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bv.hi, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv.lo, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv.hi, acc[i][0], 0, 0, 0);
+  }
+  mid();
+}
+
 // Forward form: C[m][p] = sum_k A[k][m] * B[k][p], BK = G * 16 (G tap-groups per K-step).
 template <int BM, int BN, int BK, int WM, int WN>
 __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
@@ -904,7 +946,14 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
   return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
 }
 
-template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false>
+// BD (r03, f16x3 / fp16, 1 x 4 waves, G = 1, STAGES = 4): the image operand skips LDS - each lane
+// loads its own 8 values per K-step (B[8h .. 8h+7][its pixel], the shifted pixel zero-filled through an
+// out-of-range offset) with plain buffer loads three K-steps ahead into a register ring, so the only
+// LDS-DMA left per K-step is the two A-plane pieces (the 8 dword DMA pieces of B cost ~60 issue cycles
+// each, more than the K-step's 12 MFMAs).  Every wave of the 1 x 4 layout reads its own 32 columns,
+// so nothing is lost by not sharing B through LDS.
+template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
+          bool BD = false>
 __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -921,8 +970,9 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr int NQL = H1 ? 2 : NQ;  // of them staged (fp16 math: plane 0's two halves)
   static_assert(!APRE || BM % 64 == 0, "pre-split A: 64-row DMA pieces");
   static_assert(!BPRE || (!PW && BN % 64 == 0), "pre-split B: 64-pixel DMA pieces");
+  static_assert(!BD || (H3 && G == 1 && WM == 1 && WN == 4 && TN == 1 && STAGES == 4 && !BPRE), "BD form");
   constexpr int A_STAGE = APRE ? G * 4 * NQL * BM : BK * BM;
-  constexpr int STAGE = A_STAGE + (BPRE ? G * 24 * BN : BK * BN);
+  constexpr int STAGE = A_STAGE + (BD ? 0 : BPRE ? G * 24 * BN : BK * BN);
   constexpr int A_ROWS_PER_INST = 256 / BM;
   constexpr int A_INST = APRE ? G * NQL * (BM / 64) : BK / A_ROWS_PER_INST;
   constexpr int A_INST_W = A_INST / 4;
@@ -933,7 +983,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr int BG_INST_W = BPRE ? 6 * NH / 4 : PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B DMAs per wave per K-step
 #endif
   static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
-  constexpr int INST_W = A_INST_W + G * BG_INST_W;
+  constexpr int INST_W = A_INST_W + G * (BD ? 8 : BG_INST_W);
   static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
   static_assert((STAGES - 2) * INST_W < 64, "vmcnt range");
   // ONE __shared__ object: a second one (even a 4-byte flag) makes hipcc emit vmcnt(0) before the
@@ -1015,11 +1065,20 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     // offsets (OOB outside the image) are recomputed only when the tap changes.
     int c_cb, c_tap = -1;
     unsigned vrow[NH];
+    unsigned vbd = OOB;  // BD: this lane's shifted pixel byte offset (OOB outside the image)
+    const int pbd = n0 + wn + (lane & 31);
+    const int pyd = pbd / a.W, pxd = pbd - pyd * a.W;
     {
       const int ks0 = k_a * G;
-      const int tq = ks0 / a.ncb;  // branch*taps + tap
-      c_cb = ks0 - tq * a.ncb;
-      c_tap = tq;
+      if (a.tapinner) {  // logical K-step = cb * nz + z
+        const int nz = a.ksteps / a.ncb;
+        c_cb = ks0 / nz;
+        c_tap = ks0 - c_cb * nz;
+      } else {
+        const int tq = ks0 / a.ncb;  // branch*taps + tap
+        c_cb = ks0 - tq * a.ncb;
+        c_tap = tq;
+      }
     }
     auto set_tap = [&](int tq) {
       const int br = tq / a.taps;
@@ -1027,14 +1086,20 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       const int d = br ? a.dil1 : a.dil0;
       const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
       const int shift = dh * a.W + dw;
+      if constexpr (BD) {
+        const bool v = pbd < a.P && (unsigned)(pyd + dh) < (unsigned)a.H && (unsigned)(pxd + dw) < (unsigned)a.W;
+        vbd = v ? (unsigned)((pbd + shift) * 4) : OOB;
+      } else {
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        const bool v = pin[h] && (unsigned)(py[h] + dh) < (unsigned)a.H && (unsigned)(px[h] + dw) < (unsigned)a.W;
-        vrow[h] = v ? (unsigned)((n0 + h * 64 + lane + shift) * (BPRE ? 16 : 4)) : OOB;
+        for (int h = 0; h < NH; ++h) {
+          const bool v = pin[h] && (unsigned)(py[h] + dh) < (unsigned)a.H && (unsigned)(px[h] + dw) < (unsigned)a.W;
+          vrow[h] = v ? (unsigned)((n0 + h * 64 + lane + shift) * (BPRE ? 16 : 4)) : OOB;
+        }
       }
     };
     set_tap(c_tap);
-    auto issue = [&](int s, int slot) {
+    float bdq[4][8];  // BD: the register ring of B values (K-step i in slot i % 4)
+    auto issue = [&](int s, int slot, float (&bq)[8]) {
 #ifdef MSL_SK_NODMA  // tuning-harness experiment only: no operand traffic
       return;
 #endif
@@ -1050,6 +1115,19 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
           const int ks = s * G + g;
           dma_b128(rx, As + inst * 256, (unsigned)(((ks * NQ + qh) * a.lda + m0 + mb + lane) * 16));
         }
+      } else if (a.tapinner) {
+        // logical K-step s*G + g = (cb, z), z fastest; instruction inst covers rows of K-step
+        // g = inst / (A_INST / G) of the stage, at packed K-step z*ncb + cb
+        const int nz = a.ksteps / a.ncb;
+#pragma unroll
+        for (int i = 0; i < A_INST_W; ++i) {
+          const int inst = wid * A_INST_W + i;
+          const int g = inst / (A_INST / G);
+          const int lk = s * G + g;
+          const int cbk = lk / nz, zk = lk - cbk * nz;
+          const unsigned a_base = (unsigned)((zk * a.ncb + cbk) * kCB * a.lda * 4) - (unsigned)(g * kCB * a.lda * 4);
+          dma_b128(ra, As + inst * 256, a_off[i] + a_base);
+        }
       } else {
         const unsigned a_base = (unsigned)s * a_stage_bytes;
 #pragma unroll
@@ -1061,7 +1139,16 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int cb16 = c_cb * kCB;
-        if constexpr (BPRE) {
+        if constexpr (BD) {
+          // channels cb16 + 8h + j of this lane's pixel; a channel past cimg reads 0 (OOB offset;
+          // OOB + c * P * 4 stays >= 2^31 since cimg * P * 4 < 2^31)
+          const int ci0 = cb16 + 8 * (lane >> 5);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const unsigned off = ci0 + j < a.cimg ? vbd + (unsigned)(ci0 + j) * chan_bytes : OOB;
+            bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0));
+          }
+        } else if constexpr (BPRE) {
           // piece (plane*2 + k half, 64-pixel half): lane = pixel, 16 B = 8 channels of a plane
 #pragma unroll
           for (int j = 0; j < BG_INST_W; ++j) {
@@ -1098,7 +1185,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
             dma_b32(rb, Bs + (g * kCB + r) * BN + h * 64, vrow[h] + cofs);
           }
         }
-        if (++c_cb == a.ncb) {
+        if (a.tapinner) {
+          if (++c_tap * a.ncb == a.ksteps) {
+            c_tap = 0;
+            ++c_cb;
+          }
+          set_tap(c_tap);
+        } else if (++c_cb == a.ncb) {
           c_cb = 0;
           if (++c_tap * a.ncb < a.ksteps) set_tap(c_tap);  // (past the last K-step: nothing to set)
         }
@@ -1111,9 +1204,37 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __builtin_amdgcn_s_barrier();  // the previous segment's LDS reads are complete in every wave
+    if constexpr (BD) {
+      if (0 < nst) issue(k_a, 0, bdq[0]);
+      if (1 < nst) issue(k_a + 1, 1, bdq[1]);
+      if (2 < nst) issue(k_a + 2, 2, bdq[2]);
+      // K-step i: wait until its A piece and B values landed (the younger stages may stay in flight),
+      // barrier (the A slot refilled next was read by every wave at i - 1), issue K-step i + 3 into
+      // the ring slot K-step i - 1 freed, compute
+      auto step = [&](int i, float (&cur)[8], float (&nxt)[8]) {
+        const int younger = min(STAGES - 2, nst - 1 - i);
+        if (younger >= 2) wait_vmcnt<2 * INST_W>();
+        else if (younger == 1) wait_vmcnt<INST_W>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        const float* As = smem + (i % STAGES) * STAGE;
+        const bool more = i + STAGES - 1 < nst;
+        auto mid = [&] {
+          if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt);
+        };
+        mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      };
+      for (int i = 0; i < nst; i += 4) {
+        step(i, bdq[0], bdq[3]);
+        if (i + 1 < nst) step(i + 1, bdq[1], bdq[0]);
+        if (i + 2 < nst) step(i + 2, bdq[2], bdq[1]);
+        if (i + 3 < nst) step(i + 3, bdq[3], bdq[2]);
+      }
+    } else {
 #pragma unroll
     for (int k = 0; k < STAGES - 1; ++k)
-      if (k < nst) issue(k_a + k, k);
+      if (k < nst) issue(k_a + k, k, bdq[0]);
     for (int i = 0; i < nst; ++i) {
       const int younger = min(STAGES - 2, nst - 1 - i);
       if constexpr (STAGES >= 6) {
@@ -1141,7 +1262,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       const float* As = smem + (i % STAGES) * STAGE;
       const bool more = i + STAGES - 1 < nst;
       auto mid = [&] {
-        if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
+        if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, bdq[0]);
       };
       if constexpr (MT == kMathBf16)
         mfma_stage_bf16<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
@@ -1158,6 +1279,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       else
         mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     }
 
     if constexpr (H3) {  // exact: both factors are powers of two
@@ -1247,9 +1369,10 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 
 // The same kernel held to two waves per SIMD (<= 256 VGPRs + AGPRs): the f16x3 form, left to the
 // compiler's default budget, takes 199 VGPRs + 64 AGPRs and one wave per SIMD.
-template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false>
+template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
+          bool BD = false>
 __global__ void __launch_bounds__(256, 2) k_igemm_fwd_sk2(FwdArgs a, SkArgs sk) {
-  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC>(a, sk);
+  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD>(a, sk);
 }
 
 // sum of pieces w_lo..w_hi in that order (deterministic), eight loads in flight per step: a tile
