@@ -156,8 +156,9 @@ def test_bf16_conv_math_loss_curve(C, h, w, mode, multi):
     """BASELINE config 5 (SYNTHIA 16 classes, fp16/bf16 MFMA with fp32 accumulation; 1280x760 in
     the bench, 320x190 here so the CPU oracle stays quick): two UDA iterations with every conv
     in bf16 against the fp32 CPU oracle.  bf16 operand rounding (2^-9 relative) is amplified by
-    the ~100 bs=1 BN layers: the bar is the loss curve within 3e-2 relative ("parity
-    is loss curve vs fp32 CPU within tolerance").  The IW class histogram is not compared: it
+    the ~100 bs=1 BN layers: the bar is the loss curve within 3e-2 relative on the CE and 5e-2 / 8e-2
+    on the small target loss ("parity is loss curve vs fp32 CPU within tolerance"; the
+    fp16 path BASELINE config 5 names is held tighter, at full size, in tests/test_gpu_configs.py).  The IW class histogram is not compared: it
     counts argmax classes, and random-init logits have such small class margins that bf16 moves
     3-7 % of the argmaxes (fp32: < 0.1 %, test_uda_steps_match_goldens_and_oracle); the IW loss
     it weights is compared."""
@@ -179,10 +180,10 @@ def test_bf16_conv_math_loss_curve(C, h, w, mode, multi):
             out = orc.uda_step(model, opt, xs, ys, xt, cfg, it)
             for k, v in (("loss_seg", tr.loss_val.item()), ("loss_target", tr.loss_target.item())):
                 assert np.isfinite(v)
-                # 3e-2 on the CE; 6e-2 on the (small, -2e-3) IW-MaxSquare target loss after one bf16
-                # update, whose value also moves with MIOpen's split-K weight-gradient atomics of the
-                # stem conv (run-to-run: measured 2.9 % and 3.6 % on two boxes)
-                tol = 3e-2 if k == "loss_seg" or it == 0 else 6e-2
+                # 3e-2 on the CE; 5e-2 / 8e-2 on the small (-3e-3) IW-MaxSquare target loss: since r03
+                # every conv but the stem runs bf16 products (layer2.0's stride-2 1x1 convs were MIOpen
+                # fp32 before), measured 3.5 % at iteration 0 (bit-reproducible run to run now)
+                tol = 3e-2 if k == "loss_seg" else (5e-2 if it == 0 else 8e-2)
                 assert v == pytest.approx(out[k], rel=tol), f"{k} it{it}: bf16 {v} vs fp32 oracle {out[k]}"
     finally:
         from maxsquareloss_amd import ops
