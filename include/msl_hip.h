@@ -73,10 +73,12 @@ int msl_conv_set_pack_form(int form);
  * (default); 0 = pure stream-K (every tile range-split over 512 workgroups). */
 int msl_conv_set_sk_hybrid(int on);
 /* Kernel-variant switch for same-box A/B measurements of alternative kernel forms (process-wide,
- * read at launch; identical results up to fp32 summation order): 0 = the default forms; bit 0 =
- * the weight gradient's dY fragments prefetched three K-steps ahead (k_wgrad_x6 PIPE 1); bit 1 =
- * the 3x3 / ASPP forward-form GEMMs on <= 64-row tiles run their K-steps channel-block-major
- * (the taps of one channel block back to back: L2 reuse of the shifted image reads).
+ * read at launch; identical results up to fp32 summation order): 0 = the default forms; each bit a
+ * deviation: bit 0 = the weight gradient's dY fragments prefetched three K-steps ahead (k_wgrad_x6
+ * PIPE 1); bit 1 = the 3x3 / ASPP forward-form GEMMs on <= 64-row tiles run their K-steps
+ * channel-block-major; bit 2 = the 3x3 f16x3 / fp16 forward-form GEMMs stage the image operand
+ * through LDS (the r02 form) instead of loading it straight to registers; bit 3 = the stream-K
+ * remainder after data-parallel rounds spread at one K-step per workgroup (the r02 split).
  * MSL_ERR_ARG for a negative value. */
 int msl_conv_set_variant(int variant);
 

@@ -244,9 +244,12 @@ static int g_sk_hybrid = 1;
 // 4e-8 vs 6e-8 relative to sum|terms|), kMathH3P the scaled two-way fp16 split (three fp16
 // MFMAs per slice; dconv_kernels.h Split2h).  Process-wide; packs are form-specific.
 static int g_f32_form = kMathH3P;
-// Kernel-variant switch for same-box A/B of alternative kernel forms (msl_conv_set_variant; bit 0:
-// k_wgrad_x6 with the 3-ahead dY fragment ring; bit 1: the tap-inner K order of the <= 64-row
-// exact-f32 forward tiles).  Process-wide, read at launch.
+// Kernel-variant switch for same-box A/B of alternative kernel forms (msl_conv_set_variant), each bit a
+// deviation from the default forms: bit 0: k_wgrad_x6 with the 3-ahead dY fragment ring; bit 1: the
+// tap-inner K order of the <= 64-row exact-f32 forward tiles; bit 2: the 3x3 f16x3 / fp16 forward
+// form stages B through LDS (the pre-r03 form) instead of loading it to registers (BD); bit 3: the
+// stream-K remainder after data-parallel rounds on one K-step per worker (the pre-r03 split).
+// Bits 0 and 1 measured no faster (profiles/r03_fwd_forms_ab.txt).  Process-wide, read at launch.
 static int g_variant = 0;
 constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
 
@@ -398,7 +401,11 @@ template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
     if constexpr (BM == 128 && G == 1 && ST == 4 && WM == 1 && WN == 4) {
-      if (g_variant & 4) {  // the image operand straight to registers (BD form)
+      // the image operand straight to registers (BD form) for the shifted 3x3 rows (dword pieces);
+      // the pointwise rows keep their two dwordx4 LDS-DMA pieces per wave and K-step (BD loses there:
+      // 256 -> 1024 fwd 32.7 vs 31.0 us, 2048 -> 512 82.7 vs 75.1; layer3 3x3 fwd 52.4 vs 55.0,
+      // layer4 172 vs 190; profiles/r03_fwd_forms_ab.txt)
+      if (!PW && !(g_variant & 4)) {
         if (accum)
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a, sk);
         else
@@ -486,6 +493,12 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     sk.tdp = (g_sk_hybrid && tiles >= kSkNW) ? (int)(tiles / kSkNW * kSkNW) : 0;
     const long long T = (tiles - sk.tdp) * sk.KS;
     sk.NW = (int)std::min<long long>(kSkNW, T);
+    // the remainder after data-parallel rounds (e.g. 16 tiles x 16 K-steps of a 256 -> 1024 pointwise
+    // GEMM): at one or two K-steps per worker every worker writes a whole 64-KB piece for almost no
+    // work; at least kSkMinIt K-steps each (512 -> 2048 fwd 75.9 vs 82.2 us, 2048 -> 512 dgrad 85.6 vs
+    // 90.0; variant bit 3 restores one per worker)
+    constexpr long long kSkMinIt = 8;
+    if (sk.tdp > 0 && !(g_variant & 8)) sk.NW = (int)std::max<long long>(1, std::min<long long>(sk.NW, T / kSkMinIt));
     sk.T = (int)T;
     a.C = out;
     a.bias = bias;

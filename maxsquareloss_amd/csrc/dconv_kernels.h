@@ -1000,9 +1000,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // whole data-parallel tiles w, w + nb, ... below sk.tdp first, then this worker's stream-K
   // range of the remaining tiles' iterations (none for w >= sk.NW)
   int dp_t = w, it = 0, it_end = 0;
-  if (w < sk.NW) {
-    it = sk.tdp * sk.KS + sk_start(w, sk.T, sk.NW);
-    it_end = sk.tdp * sk.KS + sk_start(w + 1, sk.T, sk.NW);
+  // the stream-K worker index: w (XCD-aware: neighbouring ranges share an L2); for the remainder
+  // after data-parallel rounds with fewer stream-K workers than workgroups, the block id, so those
+  // workers spread over all XCDs instead of filling the first one
+  const int sw = (sk.tdp > 0 && sk.NW < nb) ? b : w;
+  if (sw < sk.NW) {
+    it = sk.tdp * sk.KS + sk_start(sw, sk.T, sk.NW);
+    it_end = sk.tdp * sk.KS + sk_start(sw + 1, sk.T, sk.NW);
   }
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
@@ -1304,7 +1308,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // all workgroups read pieces at once with nothing to overlap: 38 of 135 us on layer3.)
       const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
           (void*)sk.part, (short)0, (int)min(0x7fffffffLL, (long long)sk.NW * 2 * PSZ * 4), 0x00020000);
-      const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4);
+      const unsigned pbase = (unsigned)((sw * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
