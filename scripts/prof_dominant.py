@@ -1,6 +1,8 @@
 """The bench's dominant kernel alone: the layer3 dilated conv forward (256->256, d=2) at the
 1024x512 feature size (65x129), launched through the same op as the training step.  Profiled
-with rocprofv3 (--kernel-trace --stats, then separate --pmc passes) by scripts/gpu_bench_prof.sh."""
+with rocprofv3 (--kernel-trace --stats, then separate --pmc passes) by scripts/gpu_counters.sh.
+
+    prof_dominant.py [N] [H W MATH]     e.g. 20 96 161 fp16 (BASELINE configs[4]: 1280x760, fp16 MFMA)"""
 import os
 import sys
 
@@ -10,8 +12,11 @@ import torch  # noqa: E402
 from maxsquareloss_amd import ops  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+H, W = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (65, 129)
+if len(sys.argv) > 4:
+    ops.set_conv_math(sys.argv[4])
 g = torch.Generator(device="cuda").manual_seed(0)
-x = torch.randn(1, 256, 65, 129, device="cuda", generator=g)
+x = torch.randn(1, 256, H, W, device="cuda", generator=g)
 w = torch.randn(256, 256, 3, 3, device="cuda", generator=g) * 0.02
 cache = ops.PackCache()
 # f16x3: in the step the input's absmax partials come from the BN kernel that produced it, so the
