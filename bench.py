@@ -68,6 +68,8 @@ def parse():
                     help="1: iterations after the first replay one captured hipGraph (single process); 0: eager")
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: the target forward runs on a side stream concurrently with the source backward")
+    ap.add_argument("--async-wgrad", type=int, default=1,
+                    help="1: in-place weight gradients on a side stream beside the data-gradient chain (ops.ASYNC_WGRAD)")
     ap.add_argument("--variant", type=int, default=0, help="msl_conv_set_variant (kernel-form A/B experiments)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=2, help="0 disables the CPU baseline")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -89,6 +91,7 @@ def main():
         argv += ["--f32_form", a.f32_form]
     args, _, _ = init_args(build_parser().parse_args(argv))
     ops.set_bn_fused(a.bn_form == "fused")
+    ops.ASYNC_WGRAD = bool(a.async_wgrad)
     if a.variant:
         from maxsquareloss_amd import hip
         hip.check(hip.load().msl_conv_set_variant(a.variant), "msl_conv_set_variant")
@@ -214,7 +217,7 @@ def main():
         "data": "synthetic (counter-generated uint8 images -> BGR-mean, uniform labels; random-init weights)",
         "config": {"workload": f"{'SYNTHIA' if C == 16 else 'GTA5'}->Cityscapes {args.target_mode} UDA step "
                                f"(solve_gta5.py), {W}x{H}, bs=1/GPU",
-                   "conv_math": a.conv_math, "bn_form": a.bn_form, "hipgraph": graphed, "overlap": bool(a.overlap), "variant": a.variant, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
+                   "conv_math": a.conv_math, "bn_form": a.bn_form, "hipgraph": graphed, "overlap": bool(a.overlap), "async_wgrad": bool(a.async_wgrad), "variant": a.variant, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
                    "target_mode": args.target_mode, "multi": args.multi, "lambda_target": args.lambda_target,
                    "num_classes": C, "global_batch": 2 * world, "parallelism": f"dp{world}"},
         "roofline": roofline, "cpu_baseline": cpu,

@@ -5,6 +5,8 @@ calls on torch's current HIP stream.  Tensors are bs=1 NCHW fp32 (the
 reference only runs bs=1: IW_MaxSquareloss broadcasts (N,H,W) weights against
 (N,C,H,W) probabilities, which only works for N=1 - SURVEY.md quirk Q3).
 """
+from contextlib import nullcontext as _nullctx
+
 import torch
 from torch.autograd import Function
 
@@ -151,6 +153,44 @@ def grad_sink(p):
     if g.data_ptr() != fg.flat.data_ptr() + 4 * int(fg.offsets[i]):
         return None
     return g, fg, i
+
+
+# --------------------------------------------------------------------------- asynchronous weight gradients
+# With ASYNC_WGRAD the weight gradients that accumulate in place into the flat gradient buffer (the
+# training path: ops.grad_sink) run on a side stream per device, concurrently with the data-gradient
+# chain of the backward (dgrad -> BN backward -> dgrad ...), which is latency-bound between its GEMMs.
+# Everything that reads the flat buffer joins that stream first (wgrad_join: the SGD step, the data-
+# parallel bucket launches, zero_grad).  Kernels, operands and per-buffer order are unchanged
+# (results bit-identical).  Not in the reference, whose backward is one stream.
+ASYNC_WGRAD = True
+_WG_STREAMS = {}
+
+
+def _wgrad_stream(t):
+    idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    ws = _WG_STREAMS.get(idx)
+    if ws is None:
+        ws = _WG_STREAMS[idx] = torch.cuda.Stream(device=t.device)
+    ws.wait_stream(torch.cuda.current_stream(t.device))
+    return ws
+
+
+def _keep(ws, *tensors):
+    """The side stream reads these: the caching allocator must not hand their memory to another
+    stream's allocations before the side stream's work on them is done."""
+    for t in tensors:
+        if t is not None:
+            t.record_stream(ws)
+
+
+def wgrad_join(device=None):
+    """Make the current stream wait for every weight gradient enqueued on the side stream."""
+    if not _WG_STREAMS:
+        return
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    ws = _WG_STREAMS.get(dev.index if dev.index is not None else torch.cuda.current_device())
+    if ws is not None:
+        torch.cuda.current_stream(dev).wait_stream(ws)
 
 
 # --------------------------------------------------------------------------- packing cache
@@ -366,14 +406,19 @@ class _DConv3x3(Function):
                       "msl_dconv_dgrad")
         sink = grad_sink(weights[0]) if (nb == 1 and not has_bias and ctx.needs_input_grad[1]) else None
         wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w)
-        ws = hip.workspace(wsb, x.device)
         if sink is not None:
             g, fg, i = sink
-            hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
-                                 (x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w, dil0, 0, 1,
-                                  ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
+            side = _wgrad_stream(x) if ASYNC_WGRAD else None
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                ws = hip.workspace(wsb, x.device)
+                hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
+                                     (x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w, dil0, 0, 1,
+                                      ws.data_ptr(), wsb, hip.stream_ptr()), (xpart, gpart)), "msl_dconv_wgrad")
+            if side is not None:
+                _keep(side, x, gy, *(q[0] for q in (xpart, gpart) if q is not None))
             fg.notify(i)
             return dx, None, None, None, None, None, None, None
+        ws = hip.workspace(wsb, x.device)
         dw_all = torch.empty((nb, cout, cin, 3, 3), dtype=_f32, device=x.device)
         db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
         hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
@@ -469,10 +514,14 @@ class _PConv(Function):
         sink = grad_sink(weight)
         dst = sink[0] if sink is not None else torch.empty_like(weight)
         wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
-        ws = hip.workspace(wsb, x.device)
-        hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
-                             (x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p, int(sink is not None),
-                              ws.data_ptr(), wsb, s), (ctx.xpart, gpart)), "msl_pconv_wgrad")
+        side = _wgrad_stream(x) if (ASYNC_WGRAD and sink is not None) else None
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            ws = hip.workspace(wsb, x.device)
+            hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
+                                 (x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p, int(sink is not None),
+                                  ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.xpart, gpart)), "msl_pconv_wgrad")
+        if side is not None:
+            _keep(side, x, gy, *(q[0] for q in (ctx.xpart, gpart) if q is not None))
         if sink is None:
             return dx, dst, None, None
         sink[1].notify(sink[2])
@@ -580,10 +629,14 @@ class _StemConv(Function):
         sink = grad_sink(weight)
         dst = sink[0] if sink is not None else torch.empty_like(weight)
         wsb = lib.msl_pconv_wgrad_workspace(kk, cout, p)
-        ws = hip.workspace(wsb, gy.device)
-        hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
-                             (col.data_ptr(), gy.data_ptr(), dst.data_ptr(), kk, cout, p, int(sink is not None),
-                              ws.data_ptr(), wsb, s), (ctx.cpart, gpart)), "msl_pconv_wgrad")
+        side = _wgrad_stream(gy) if (ASYNC_WGRAD and sink is not None) else None
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            ws = hip.workspace(wsb, gy.device)
+            hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
+                                 (col.data_ptr(), gy.data_ptr(), dst.data_ptr(), kk, cout, p, int(sink is not None),
+                                  ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.cpart, gpart)), "msl_pconv_wgrad")
+        if side is not None:
+            _keep(side, col, gy, *(q[0] for q in (ctx.cpart, gpart) if q is not None))
         if sink is None:
             return dx, dst, None, None, None
         sink[1].notify(sink[2])

@@ -19,6 +19,7 @@ import os
 
 import torch
 
+from .. import ops
 from ..utils.loss import IW_MaxSquareloss, MaxSquareloss, multi_level_guidance_ce
 from ..utils.graph import GraphedStep
 from ..utils.synthetic import SyntheticDomain
@@ -122,6 +123,7 @@ class UDATrainer(Trainer):
             self.train_source(pred, y_s)
             pred = self.model(x_t)
             self.train_target(pred)
+            ops.wgrad_join(self.device)  # the side-stream weight gradients (ops.ASYNC_WGRAD) rejoin
             return
         # The target forward depends on neither the source backward nor its gradients (the weights
         # change only at the optimizer step; BN running statistics are updated by the forwards, in
@@ -146,6 +148,7 @@ class UDATrainer(Trainer):
         with torch.cuda.stream(side):
             self.train_target(pred_t)
         main.wait_stream(side)
+        ops.wgrad_join(self.device)  # the side-stream weight gradients (ops.ASYNC_WGRAD) rejoin
 
     def _uda_update(self):
         self.optimizer.step()

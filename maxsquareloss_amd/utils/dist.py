@@ -66,6 +66,8 @@ class GradReducer:
     def _launch(self, b):
         a, e = self._elem_range(b)
         if self.world > 1:
+            from .. import ops
+            ops.wgrad_join(self.flat.flat.device)  # the bucket's weight gradients may be on the side stream
             self.works.append(dist.all_reduce(self.flat.flat[a:e], group=self.pg, async_op=True))
 
     def _advance(self):

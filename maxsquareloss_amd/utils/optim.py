@@ -89,6 +89,8 @@ class FlatGrads:
         return self.flat[self.offsets[i]:self.offsets[i + 1]]
 
     def zero_(self):
+        from .. import ops
+        ops.wgrad_join(self.flat.device)  # weight gradients still being accumulated on the side stream
         self.flat.zero_()
         self.used[:] = False
         self.new_backward()
@@ -211,6 +213,8 @@ class SGD:
         if self.device.type != "cuda":
             raise hip.MSLError("SGD.step runs on the HIP path only (no CPU fallback)")
         lib = hip.load()
+        from .. import ops
+        ops.wgrad_join(self.device)  # the weight gradients accumulated on the side stream (ops.ASYNC_WGRAD)
         self._ensure_table()
         self._last_used = self.grads.used.copy()
         _dev, p_ent, p_be, p_bo, nblocks = self._table
