@@ -19,8 +19,10 @@ for r in seg:
     n = re.sub(r"\(.*", "", n)
     n = re.sub(r"^void ", "", n)
     if "k_igemm_fwd_sk2" in n:
-        pw = ", true, 5" in n or ", true, 8" in n
-        n = "fwd-form GEMM f16x3 " + ("pointwise" if pw else "3x3") + (" acc" if n.endswith("true>") else "")
+        t = [x.strip() for x in n.split("<", 1)[1].rstrip(">").split(",")]  # BM BN G ST WM WN PW MT ACC [BD]
+        pw, acc, bd = t[6] == "true", t[8] == "true", len(t) > 9 and t[9] == "true"
+        n = ("fwd-form GEMM " + ("fp16 " if t[7] == "8" else "f16x3 ") + ("pointwise" if pw else "3x3") +
+             (" acc" if acc else "") + (" (B in registers)" if bd else ""))
     elif "k_igemm_fwd_sk<" in n:
         n = "fwd-form GEMM exact-f32 " + n.split("<")[1].split(",")[0] + "-row"
     elif "elementwise" in n:
