@@ -68,7 +68,7 @@ def parse():
                     help="1: iterations after the first replay one captured hipGraph (single process); 0: eager")
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: the target forward runs on a side stream concurrently with the source backward")
-    ap.add_argument("--async-wgrad", type=int, default=1,
+    ap.add_argument("--async-wgrad", type=int, default=0,
                     help="1: in-place weight gradients on a side stream beside the data-gradient chain (ops.ASYNC_WGRAD)")
     ap.add_argument("--variant", type=int, default=0, help="msl_conv_set_variant (kernel-form A/B experiments)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=2, help="0 disables the CPU baseline")

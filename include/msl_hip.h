@@ -78,7 +78,8 @@ int msl_conv_set_sk_hybrid(int on);
  * PIPE 1); bit 1 = the 3x3 / ASPP forward-form GEMMs on <= 64-row tiles run their K-steps
  * channel-block-major; bit 2 = the 3x3 f16x3 / fp16 forward-form GEMMs stage the image operand
  * through LDS (the r02 form) instead of loading it straight to registers; bit 3 = the stream-K
- * remainder after data-parallel rounds spread at one K-step per workgroup (the r02 split).
+ * remainder after data-parallel rounds spread at one K-step per workgroup (the r02 split); bit 4 =
+ * the f16x3 / fp16 3x3 GEMMs with M <= 64 (ASPP forward, layer1) on exact-f32 32 / 64-row tiles.
  * MSL_ERR_ARG for a negative value. */
 int msl_conv_set_variant(int variant);
 

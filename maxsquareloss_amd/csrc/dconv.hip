@@ -194,7 +194,6 @@ __global__ void __launch_bounds__(256) k_absmax_jobs(const msl_pack_job* __restr
   const msl_pack_job jb = jobs[blockIdx.y];
   const int cimg = jb.for_dgrad ? jb.cout : jb.cin;
   const int m = jb.for_dgrad ? jb.cin : jb.cout;
-  if (m <= 64) return;  // no planes to split (as msl_*_pack: the tail stays untouched)
   const long long f32 = (long long)jb.nbranch * ((cimg + kCB - 1) / kCB) * TAPS * kCB * ((m + kPackPad - 1) / kPackPad * kPackPad);
   absmax_block(jb.w, (long long)jb.cout * jb.cin * TAPS, jb.branch_stride, jb.nbranch, blockIdx.x,
                jb.packed + pack_tail_offset(f32) + blockIdx.x);
@@ -224,7 +223,7 @@ __global__ void __launch_bounds__(256) k_pack_split_many(const msl_pack_job* __r
   const long long rest = local / nmx;
   const int cb = (int)(rest % ncb), br = (int)(rest / ncb);
   const long long f32 = (long long)jb.nbranch * ncb * TAPS * kCB * lda;
-  pack_split_block<TAPS>(jb.w, jb.branch_stride, jb.cin, jb.cout, jb.for_dgrad, ncb, lda, m > 64, jb.packed,
+  pack_split_block<TAPS>(jb.w, jb.branch_stride, jb.cin, jb.cout, jb.for_dgrad, ncb, lda, m > 64 || h3, jb.packed,
                          reinterpret_cast<__bf16*>(jb.packed + f32), mx, cb, br, s,
                          h3 ? jb.packed + pack_tail_offset(f32) : nullptr);
 }
@@ -389,7 +388,8 @@ static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)
 // + (f16x3) the image's kNPart absmax partials at the end of the caller's workspace.
 constexpr size_t kPartBytes = kNPart * sizeof(float);
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
-  if (pl.sk) return (size_t)kSkNW * 2 * pl.bm * pl.bn * sizeof(float) + kPartBytes;
+  // (the <= 64-row f16x3 / fp16 3x3 tiles run 64 rows: room for those pieces whatever the form)
+  if (pl.sk) return (size_t)kSkNW * 2 * std::max(pl.bm, 64) * pl.bn * sizeof(float) + kPartBytes;
   return (pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0) + kPartBytes;
 }
 static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials block from the end
@@ -400,7 +400,7 @@ static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials 
 template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
-    if constexpr (BM == 128 && G == 1 && ST == 4 && WM == 1 && WN == 4) {
+    if constexpr ((BM == 128 || (BM == 64 && MT == kMathH3P)) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
       // the image operand straight to registers (BD form) for the shifted 3x3 rows (dword pieces);
       // the pointwise rows keep their two dwordx4 LDS-DMA pieces per wave and K-step (BD loses there:
       // 256 -> 1024 fwd 32.7 vs 31.0 us, 2048 -> 512 82.7 vs 75.1; layer3 3x3 fwd 52.4 vs 55.0,
@@ -444,6 +444,19 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   if (X6L && pl.sk && pl.bm == 128) {
     pl.G = 1;
     pl.bk = kCB;
+    pl.kps = pl.ksteps;
+  }
+  // f16x3 / fp16 (r03): the 3x3 / ASPP GEMMs with M <= 64 (the 19-class ASPP forward, layer1's
+  // 64-channel convs) on 64-row tiles of the same kernel (weights from the fp16 planes, the image
+  // operand straight to registers) instead of exact-f32 32 / 64-row tiles: 3 fp16 MFMAs per 16-deep
+  // slice at 64 rows cost 2.7x less matrix time than 8 f32 MFMAs at 32 rows.  Variant bit 4 keeps
+  // the exact-f32 tiles.
+  const bool small_f16 = MT == kMathH3P && pl.sk && pl.bm <= 64 && taps == 9 && !(g_variant & 16);
+  if (small_f16) {
+    pl.G = 1;
+    pl.bm = 64;
+    pl.bk = kCB;
+    pl.tiles_m = cdiv(M, 64);
     pl.kps = pl.ksteps;
   }
   if (ws_bytes < fwd_ws_bytes(pl, M, P)) return MSL_ERR_WORKSPACE;
@@ -505,9 +518,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
     const dim3 rgrid(pl.bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp));
     const bool reduce = T > 0;
-    if (X6L && pl.bm == 128) {
+    if (X6L && (pl.bm == 128 || small_f16)) {
       // the x6 kernel stages its weights from the bf16 planes that pack() split once, behind
-      // the fp32 part of the same buffer (M > 64 <=> 128-row tiles)
+      // the fp32 part of the same buffer (M > 64 <=> 128-row tiles; f16x3: every M)
       const long long f32 = (long long)pl.ksteps * kCB * a.lda;
       a.Ax6 = reinterpret_cast<const __bf16*>(packed + f32);
       if constexpr (F16) {
@@ -529,7 +542,11 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // waves 1 x 4 (each 128 rows x 32 pixels): every wave splits only its own B columns
         // (2 x 2 waves split each column twice); step 40.5 vs 40.9 ms on one box
         // (profiles/r02_f16x3_waves.txt)
-        if (taps == 1 && dil0 == 0)
+        if constexpr (MT == kMathH3P) {
+          if (small_f16) launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk);
+        }
+        if (small_f16) {
+        } else if (taps == 1 && dil0 == 0)
           launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk);
         else
           launch_sk<128, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk);
@@ -537,7 +554,12 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
       }
       MSL_CHECK_LAUNCH();
-      if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
+      if (reduce) {
+        if (small_f16)
+          hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
+        else
+          hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
+      }
     } else if (pl.bm == 128) {
       if (pl.G == 2)
         launch_sk<128, 2, 2, 2, 2, MB>(accum, grid, block, st, a, sk);
@@ -605,11 +627,12 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
   const int lda = pad_to(m, kPackPad);
   const int ncb = cdiv(cimg, kCB);
   __bf16* planes = reinterpret_cast<__bf16*>(packed + total);
-  const bool h3 = g_f32_form == kMathH3P && m > 64;
+  // f16x3: fp16 planes for every M (the <= 64-row 3x3 / ASPP tiles run f16x3 too since r03)
+  const bool h3 = g_f32_form == kMathH3P;
   float* tail = h3 ? packed + pack_tail_offset(total) : nullptr;
   // M <= 64 has no planes to split, and its 128-row padding is mostly zeros, which k_pack's
   // fully coalesced rows write faster (ASPP fwd 2048 -> 19: 5.2 vs 9.5 us)
-  if ((g_pack_form == 0 && !h3) || m <= 64) {  // element-wise gather, then a separate split
+  if (!h3 && (g_pack_form == 0 || m <= 64)) {  // element-wise gather, then a separate split
     const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
     hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
                        ncb, lda, taps, total, packed);
@@ -625,7 +648,7 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
   // lda is a multiple of kPackPad (128): the m chunks tile it exactly, zero rows included
   static_assert(kPackPad % kPackTileM == 0, "pack tiles must cover lda");
   const dim3 grid(lda / kPackTileM, ncb, nbranch);
-  const int split = m > 64;
+  const int split = m > 64 || h3;
   if (taps != 9 && taps != 1) return MSL_ERR_ARG;
   if (h3) {
     hipLaunchKernelGGL(k_absmax, dim3(kNPart), dim3(256), 0, st, w, (long long)cout * cin * taps, branch_stride,

@@ -161,8 +161,10 @@ def grad_sink(p):
 # chain of the backward (dgrad -> BN backward -> dgrad ...), which is latency-bound between its GEMMs.
 # Everything that reads the flat buffer joins that stream first (wgrad_join: the SGD step, the data-
 # parallel bucket launches, zero_grad).  Kernels, operands and per-buffer order are unchanged
-# (results bit-identical).  Not in the reference, whose backward is one stream.
-ASYNC_WGRAD = True
+# (results bit-identical).  Not in the reference, whose backward is one stream.  Off by default: the
+# step measured slower with it (40.2 vs 39.5 ms same box: the concurrent GEMMs share the CUs and the
+# caches; profiles/r03_async_wgrad_ab.txt).
+ASYNC_WGRAD = False
 _WG_STREAMS = {}
 
 

@@ -75,6 +75,8 @@ def _worker(rank, world, port, q, outdir):
             events.append(("notify", i))
 
         def launch(b):
+            from maxsquareloss_amd import ops
+            ops.wgrad_join()  # the bucket's weight gradients may still be on the side stream
             a, e = red._elem_range(b)
             events.append(("launch", b, flat.flat[a:e].clone(), in_finish[0]))  # stream-ordered copy
             if os.environ.get("MSL_DP_SYNC_LAUNCH"):
