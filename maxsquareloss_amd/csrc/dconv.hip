@@ -513,9 +513,31 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     constexpr long long kSkMinIt = 8;
     if (sk.tdp > 0 && !(g_variant & 8)) sk.NW = (int)std::max<long long>(1, std::min<long long>(sk.NW, T / kSkMinIt));
     sk.T = (int)T;
+    sk.nchunk = sk.kchunk = 0;
+    // the small-M f16x3 3x3 GEMMs (ASPP forward, layer1): chunked split-K, channel-block-major K
+    // (a chunk's weights in each XCD's L2, the taps of one channel block back to back: L2 reuse of
+    // the shifted image rows), chunks sized to fill one round of the 512 resident workgroups
+    if (small_f16 && !(g_variant & 32)) {
+      int nch = 0, kch = 0;
+      double best = 0.0;
+      for (int C = 1; C <= 64 && tiles * C <= 512; ++C) {
+        const int L = cdiv(sk.KS, C);
+        if (L < 16) break;
+        const int Ce = cdiv(sk.KS, L);
+        const double eff = (double)(tiles * Ce) / 512.0;
+        if (eff > best) { best = eff; nch = Ce; kch = L; }
+      }
+      if (nch > 1) {
+        sk.nchunk = nch;
+        sk.kchunk = kch;
+        sk.tdp = 0;
+        sk.NW = (int)(tiles * nch);
+        a.tapinner = 1;
+      }
+    }
     a.C = out;
     a.bias = bias;
-    const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
+    const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);  // (chunked: NW = items <= 512)
     const dim3 rgrid(pl.bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp));
     const bool reduce = T > 0;
     if (X6L && (pl.bm == 128 || small_f16)) {

@@ -925,6 +925,12 @@ struct SkArgs {
   int tiles_m, tiles_n, KS, NW;
   int T;           // stream-K iterations: (tiles - tdp) * KS  (T * NW < 2^31, checked by the planner)
   int tdp;         // leading tiles that run data-parallel (a multiple of the grid size)
+  // chunked split-K (r03, nchunk > 0; tdp = 0): worker w = one (chunk c = w / tiles, tile t = w % tiles)
+  // item, K-steps [c*kchunk, (c+1)*kchunk) of tile t; NW = nchunk * tiles.  Chunk-major items give the
+  // workgroups of one XCD the same K chunk of every tile, so the weights of that chunk stay in its L2
+  // (the 19-class ASPP forward re-read its whole weight pack once per pixel tile).  Every item leaves a
+  // piece (slot 1 for chunk 0, slot 0 otherwise) that k_sk_reduce sums in chunk order.
+  int nchunk, kchunk;
 };
 
 __device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
@@ -1004,7 +1010,14 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // after data-parallel rounds with fewer stream-K workers than workgroups, the block id, so those
   // workers spread over all XCDs instead of filling the first one
   const int sw = (sk.tdp > 0 && sk.NW < nb) ? b : w;
-  if (sw < sk.NW) {
+  if (sk.nchunk > 0) {
+    if (w < sk.NW) {
+      const int ntl = sk.tiles_m * sk.tiles_n;
+      const int c = w / ntl, t = w - c * ntl;
+      it = t * sk.KS + c * sk.kchunk;
+      it_end = t * sk.KS + min(sk.KS, (c + 1) * sk.kchunk);
+    }
+  } else if (sw < sk.NW) {
     it = sk.tdp * sk.KS + sk_start(sw, sk.T, sk.NW);
     it_end = sk.tdp * sk.KS + sk_start(sw + 1, sk.T, sk.NW);
   }
@@ -1116,7 +1129,12 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
           const int inst = wid * A_INST_W + i;
           const int g = inst / (NQL * (BM / 64)), r = inst % (NQL * (BM / 64));
           const int qh = r / (BM / 64), mb = (r % (BM / 64)) * 64;
-          const int ks = s * G + g;
+          int ks = s * G + g;
+          if (a.tapinner) {  // logical (cb, z), z fastest -> packed K-step z * ncb + cb
+            const int nz = a.ksteps / a.ncb;
+            const int cbk = ks / nz;
+            ks = (ks - cbk * nz) * a.ncb + cbk;
+          }
           dma_b128(rx, As + inst * 256, (unsigned)(((ks * NQ + qh) * a.lda + m0 + mb + lane) * 16));
         }
       } else if (a.tapinner) {
@@ -1409,8 +1427,10 @@ template <int BM, int BN>
 __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   constexpr int PSZ = BM * BN;
   const int tl = blockIdx.y, t = sk.tdp + tl;  // tile, and its index in the stream-K space
-  const int w_lo = sk_worker_of(tl * sk.KS, sk.T, sk.NW);
-  const int w_hi = sk_worker_of((tl + 1) * sk.KS - 1, sk.T, sk.NW);
+  const bool chunked = sk.nchunk > 0;
+  const int ntl = sk.tiles_m * sk.tiles_n;
+  const int w_lo = chunked ? 0 : sk_worker_of(tl * sk.KS, sk.T, sk.NW);
+  const int w_hi = chunked ? sk.nchunk - 1 : sk_worker_of((tl + 1) * sk.KS - 1, sk.T, sk.NW);
   if (w_lo == w_hi) return;
   int tm, tn;
     sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
@@ -1418,6 +1438,7 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   const float4* __restrict__ part = reinterpret_cast<const float4*>(sk.part);
   for (int g = blockIdx.x * 256 + threadIdx.x; g < PSZ / 4; g += gridDim.x * 256) {
     auto piece = [&](int wc) {
+      if (chunked) return part[(long long)((wc * ntl + tl) * 2 + (wc > 0 ? 0 : 1)) * (PSZ / 4) + g];
       const int slot = sk_start(wc, sk.T, sk.NW) > tl * sk.KS ? 0 : 1;
       return part[(long long)(wc * 2 + slot) * (PSZ / 4) + g];
     };
