@@ -79,7 +79,8 @@ int msl_conv_set_sk_hybrid(int on);
  * channel-block-major; bit 2 = the 3x3 f16x3 / fp16 forward-form GEMMs stage the image operand
  * through LDS (the r02 form) instead of loading it straight to registers; bit 3 = the stream-K
  * remainder after data-parallel rounds spread at one K-step per workgroup (the r02 split); bit 4 =
- * the f16x3 / fp16 3x3 GEMMs with M <= 64 (ASPP forward, layer1) on exact-f32 32 / 64-row tiles.
+ * the f16x3 3x3 GEMMs with M <= 64 (ASPP forward, layer1) on exact-f32 32 / 64-row tiles; bit 5 =
+ * those 64-row f16x3 GEMMs as chunked split-K in channel-block-major K order.
  * MSL_ERR_ARG for a negative value. */
 int msl_conv_set_variant(int variant);
 

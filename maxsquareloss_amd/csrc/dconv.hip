@@ -514,10 +514,11 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     if (sk.tdp > 0 && !(g_variant & 8)) sk.NW = (int)std::max<long long>(1, std::min<long long>(sk.NW, T / kSkMinIt));
     sk.T = (int)T;
     sk.nchunk = sk.kchunk = 0;
-    // the small-M f16x3 3x3 GEMMs (ASPP forward, layer1): chunked split-K, channel-block-major K
-    // (a chunk's weights in each XCD's L2, the taps of one channel block back to back: L2 reuse of
-    // the shifted image rows), chunks sized to fill one round of the 512 resident workgroups
-    if (small_f16 && !(g_variant & 32)) {
+    // the small-M f16x3 3x3 GEMMs (ASPP forward, layer1), variant bit 5: chunked split-K,
+    // channel-block-major K (a chunk's weights in each XCD's L2, the taps of one channel block back to
+    // back), chunks sized to fill one round of the 512 resident workgroups.  Measured, not adopted:
+    // ASPP d=6 forward 140.6 vs 131.8 us stream-K, layer1 20.3 vs 21.4 (profiles/r03_fwd_forms_ab.txt)
+    if (small_f16 && (g_variant & 32)) {
       int nch = 0, kch = 0;
       double best = 0.0;
       for (int C = 1; C <= 64 && tiles * C <= 512; ++C) {
