@@ -803,7 +803,9 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
       hipLaunchKernelGGL(k_split_rows<MT>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, ap, an, a.rowscale);
       MSL_CHECK_LAUNCH();
-      if (g_variant & 1)
+      if (g_variant & 64)
+        hipLaunchKernelGGL((k_wgrad_x6<MT, 2>), grid, block, 0, st, a);
+      else if (g_variant & 1)
         hipLaunchKernelGGL((k_wgrad_x6<MT, 1>), grid, block, 0, st, a);
       else
         hipLaunchKernelGGL((k_wgrad_x6<MT, 0>), grid, block, 0, st, a);

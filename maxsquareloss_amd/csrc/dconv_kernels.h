@@ -2291,10 +2291,14 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       }
     }
     float rbv[16];
-    auto loadB = [&]() {  // the stage's two K-steps (a missing second one is all-masked)
+    unsigned rmb = 0;
+    // loads the stage's two K-steps (a missing second one is all-masked) into rv; the border mask is
+    // kept in mbo and applied when the values are split (storeB), so nothing waits for the loads here
+    auto loadB = [&](float (&rv)[16], unsigned& mbo) {
       const int ks0 = ld_ks;
       const unsigned m32 = kmask() | (kmask() << 16);
       const unsigned mb = (m32 >> (4 * cc)) & 0xfu;
+      mbo = mb;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int nr = (tid >> 3) + 32 * i;
@@ -2310,11 +2314,14 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
           }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) rbv[4 * i + j] = (mb >> j) & 1u ? c.f[j] : 0.f;
+        for (int j = 0; j < 4; ++j) rv[4 * i + j] = c.f[j];
       }
     };
-    auto storeB = [&](int buf) {  // split once, NP 8-B plane quarters per chunk
+    auto storeB = [&](int buf, const float (&rv0)[16], unsigned mbv) {  // split once, NP 8-B plane quarters
       char* base = smem + buf * STAGEB + wofs;
+      float rbv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rbv[q] = (mbv >> (q & 3)) & 1u ? rv0[q] : 0.f;
       if constexpr (H1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -2429,21 +2436,24 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __syncthreads();  // the previous segment's LDS reads are complete in every wave
-    if constexpr (PIPE == 1) {
+    if constexpr (PIPE == 2) {
+      // PIPE 2: the PIPE 1 dY ring, and the X values of stage s + 2 loaded at the start of stage s into
+      // the register set stage s's values left (two sets), so each load has two stages to land
       u32x4 A2[TM][NP], A3[TM][NP];
-      loadB();
+      float rb2[16];
+      unsigned rmb2 = 0;
+      loadB(rbv, rmb);
       loadA(A0, k_a);
       if (k_a + 1 < k_b) loadA(A1, k_a + 1);
       if (k_a + 2 < k_b) loadA(A2, k_a + 2);
-      storeB(0);
+      storeB(0, rbv, rmb);
+      if (nst > 2) loadB(rb2, rmb2);
       __syncthreads();
-      // stage s: K-steps k_a + 2s (ring slot 2s % 4) and k_a + 2s + 1; each K-step i first issues the
-      // load of K-step i + 3 into the slot K-step i - 1 freed
-      auto stage = [&](int s, u32x4 (&Ra)[TM][NP], u32x4 (&Rb)[TM][NP], u32x4 (&Rl)[TM][NP]) {
+      auto stage = [&](int s, u32x4 (&Ra)[TM][NP], u32x4 (&Rb)[TM][NP], u32x4 (&Rl)[TM][NP], float (&rl)[16],
+                       unsigned& ml, const float (&rs)[16], unsigned ms) {
         const int left = nst - 2 * s;
-        const bool more = left > 2;
         const int i = k_a + 2 * s;
-        if (more) loadB();
+        if (left > 4) loadB(rl, ml);  // stage s + 2
         const char* Bs = smem + (s & 1) * STAGEB;
         if (i + 3 < k_b) loadA(Rl, i + 3);
         compute(Bs, Ra);
@@ -2451,7 +2461,36 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
           if (i + 4 < k_b) loadA(Ra, i + 4);
           compute(Bs + KVB, Rb);
         }
-        if (more) storeB((s + 1) & 1);
+        if (left > 2) storeB((s + 1) & 1, rs, ms);  // stage s + 1
+        __syncthreads();
+      };
+      for (int s = 0; 2 * s < nst; s += 2) {
+        stage(s, A0, A1, A3, rbv, rmb, rb2, rmb2);
+        if (2 * (s + 1) < nst) stage(s + 1, A2, A3, A1, rb2, rmb2, rbv, rmb);
+      }
+    } else if constexpr (PIPE == 1) {
+      u32x4 A2[TM][NP], A3[TM][NP];
+      loadB(rbv, rmb);
+      loadA(A0, k_a);
+      if (k_a + 1 < k_b) loadA(A1, k_a + 1);
+      if (k_a + 2 < k_b) loadA(A2, k_a + 2);
+      storeB(0, rbv, rmb);
+      __syncthreads();
+      // stage s: K-steps k_a + 2s (ring slot 2s % 4) and k_a + 2s + 1; each K-step i first issues the
+      // load of K-step i + 3 into the slot K-step i - 1 freed
+      auto stage = [&](int s, u32x4 (&Ra)[TM][NP], u32x4 (&Rb)[TM][NP], u32x4 (&Rl)[TM][NP]) {
+        const int left = nst - 2 * s;
+        const bool more = left > 2;
+        const int i = k_a + 2 * s;
+        if (more) loadB(rbv, rmb);
+        const char* Bs = smem + (s & 1) * STAGEB;
+        if (i + 3 < k_b) loadA(Rl, i + 3);
+        compute(Bs, Ra);
+        if (left > 1) {
+          if (i + 4 < k_b) loadA(Ra, i + 4);
+          compute(Bs + KVB, Rb);
+        }
+        if (more) storeB((s + 1) & 1, rbv, rmb);
         __syncthreads();
       };
       for (int s = 0; 2 * s < nst; s += 2) {
@@ -2459,15 +2498,15 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
         if (2 * (s + 1) < nst) stage(s + 1, A2, A3, A1);
       }
     } else {
-    loadB();
+    loadB(rbv, rmb);
     loadA(A0, k_a);
-    storeB(0);
+    storeB(0, rbv, rmb);
     __syncthreads();
     int ks = k_a;  // the K-step computed next
     for (int s = 0; 2 * s < nst; ++s) {
       const int left = nst - 2 * s;
       const bool more = left > 2;  // a next stage
-      if (more) loadB();           // in flight during this stage's MFMAs
+      if (more) loadB(rbv, rmb);   // in flight during this stage's MFMAs
       const char* Bs = smem + (s & 1) * STAGEB;
       if (ks + 1 < k_b) loadA(A1, ks + 1);
       compute(Bs, A0);
@@ -2477,7 +2516,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
         compute(Bs + KVB, A1);
         ++ks;
       }
-      if (more) storeB((s + 1) & 1);
+      if (more) storeB((s + 1) & 1, rbv, rmb);
       __syncthreads();
     }
     }
