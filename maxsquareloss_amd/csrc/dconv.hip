@@ -387,9 +387,14 @@ static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)
 // counters, flags or other state survive a call).
 // + (f16x3) the image's kNPart absmax partials at the end of the caller's workspace.
 constexpr size_t kPartBytes = kNPart * sizeof(float);
-static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P) {
+// stream-K pieces, then (variant bit 7) the image operand's fp16 planes, then the partials at the end
+static size_t fwd_piece_bytes(const FwdPlan& pl) {
   // (the <= 64-row f16x3 / fp16 3x3 tiles run 64 rows: room for those pieces whatever the form)
-  if (pl.sk) return (size_t)kSkNW * 2 * std::max(pl.bm, 64) * pl.bn * sizeof(float) + kPartBytes;
+  return align_up((size_t)kSkNW * 2 * std::max(pl.bm, 64) * pl.bn * sizeof(float), 256);
+}
+static size_t img_planes_bytes(int cimg, int P) { return align_up((size_t)cdiv(cimg, kCB) * kCB * P * 4, 256); }
+static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P, int cimg) {
+  if (pl.sk) return fwd_piece_bytes(pl) + img_planes_bytes(cimg, P) + kPartBytes;
   return (pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0) + kPartBytes;
 }
 static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials block from the end
@@ -398,9 +403,19 @@ static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials 
 
 // The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
 template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
-static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
+static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk,
+                      bool bp = false) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
     if constexpr ((BM == 128 || (BM == 64 && MT == kMathH3P)) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
+      if (bp) {  // the image operand pre-split by k_split_img (variant bit 7)
+        if (accum)
+          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0, st,
+                             a, sk);
+        else
+          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true, true>), grid, block, 0,
+                             st, a, sk);
+        return;
+      }
       // the image operand straight to registers (BD form) for the shifted 3x3 rows (dword pieces);
       // the pointwise rows keep their two dwordx4 LDS-DMA pieces per wave and K-step (BD loses there:
       // 256 -> 1024 fwd 32.7 vs 31.0 us, 2048 -> 512 82.7 vs 75.1; layer3 3x3 fwd 52.4 vs 55.0,
@@ -459,7 +474,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     pl.tiles_m = cdiv(M, 64);
     pl.kps = pl.ksteps;
   }
-  if (ws_bytes < fwd_ws_bytes(pl, M, P)) return MSL_ERR_WORKSPACE;
+  if (ws_bytes < fwd_ws_bytes(pl, M, P, cimg)) return MSL_ERR_WORKSPACE;
   FwdArgs a{};
   a.Ax6 = nullptr;
   a.ascale = nullptr;
@@ -559,6 +574,18 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
           a.bnpart = kNPart;
         }
         a.ascale = packed + pack_tail_offset(f32) + kNPart;
+        const bool bp = (g_variant & 128) != 0;
+        if (bp) {  // pre-split the image operand once for the whole GEMM (behind the pieces)
+          f16x8* planes = reinterpret_cast<f16x8*>((char*)ws + fwd_piece_bytes(pl));
+          const long long n = (long long)a.ncb * 2 * P;
+          const dim3 sgrid((unsigned)std::min<long long>(cdiv(n, 256), 8192));
+          if constexpr (MT == kMathH1P)
+            hipLaunchKernelGGL(k_split_img<1>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
+          else
+            hipLaunchKernelGGL(k_split_img<2>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
+          MSL_CHECK_LAUNCH();
+          a.Bx6 = planes;
+        }
         // pointwise: B rows are unshifted, so they move as dwordx4 (4 pixels per lane: 2 DMAs per
         // wave and K-step instead of 8 dword ones): 1-4 us per call on the wide 1x1 GEMMs
         // (profiles/r02_f16x3_pw_dma.txt)
@@ -566,13 +593,13 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // (2 x 2 waves split each column twice); step 40.5 vs 40.9 ms on one box
         // (profiles/r02_f16x3_waves.txt)
         if constexpr (MT == kMathH3P) {
-          if (small_f16) launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk);
+          if (small_f16) launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp);
         }
         if (small_f16) {
         } else if (taps == 1 && dil0 == 0)
-          launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk);
+          launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
         else
-          launch_sk<128, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk);
+          launch_sk<128, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp);
       } else {
         launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
       }
@@ -949,8 +976,8 @@ int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, i
 size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w) {
   if (bad_dims(nbranch, cin, cout, h, w)) return 0;
   // large enough with or without a bias (the plan depends on it)
-  return std::max(fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, h * w, false), cout, h * w),
-                  fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, h * w, true), cout, h * w));
+  return std::max(fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, h * w, false), cout, h * w, cin),
+                  fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, h * w, true), cout, h * w, cin));
 }
 
 int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
@@ -965,7 +992,7 @@ int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float*
 
 size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
   if (bad_dims(nbranch, cin, cout, h, w)) return 0;
-  return fwd_ws_bytes(plan_fwd(nbranch, 9, cout, cin, h * w, false), cin, h * w);
+  return fwd_ws_bytes(plan_fwd(nbranch, 9, cout, cin, h * w, false), cin, h * w, cout);
 }
 
 int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
@@ -1007,7 +1034,7 @@ int msl_pconv_pack(const float* w, int cin, int cout, int for_dgrad, float* pack
 
 size_t msl_pconv_fwd_workspace(int cin, int cout, int p) {
   if (bad_dims(1, cin, cout, 1, p)) return 0;
-  return fwd_ws_bytes(plan_fwd(1, 1, cin, cout, p, false), cout, p);
+  return fwd_ws_bytes(plan_fwd(1, 1, cin, cout, p, false), cout, p, cin);
 }
 
 int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
@@ -1019,7 +1046,7 @@ int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int co
 
 size_t msl_pconv_dgrad_workspace(int cin, int cout, int p) {
   if (bad_dims(1, cin, cout, 1, p)) return 0;
-  return fwd_ws_bytes(plan_fwd(1, 1, cout, cin, p, false), cin, p);
+  return fwd_ws_bytes(plan_fwd(1, 1, cout, cin, p, false), cin, p, cout);
 }
 
 int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,

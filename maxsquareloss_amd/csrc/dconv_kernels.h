@@ -547,6 +547,41 @@ __device__ __forceinline__ void mfma_stage_hd(const float* __restrict__ As, int 
   mid();
 }
 
+// The BD stage with the image operand pre-split (k_split_img): braw holds the lane's hi plane (floats
+// 0..3 as 16 B) and lo plane (4..7), already scaled; no split work in the loop.
+template <int TM, int BM, bool HI_ONLY, typename F>
+__device__ __forceinline__ void mfma_stage_hdp(const float* __restrict__ As, int wm, int lane, f32x16 (&acc)[TM][1],
+                                               F&& mid, const float (&braw)[8]) {
+  const int l32 = lane & 31, h = lane >> 5;
+  const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
+  union { float f[4]; f16x8 h; } bh, bl;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bh.f[j] = braw[j];
+    bl.f[j] = braw[4 + j];
+  }
+  if constexpr (HI_ONLY) {
+    f16x8 av[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bh.h, acc[i][0], 0, 0, 0);
+  } else {
+    Split2h av[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i].lo = Ab[(2 + h) * BM + wm + i * 32 + l32];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bh.h, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bl.h, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bh.h, acc[i][0], 0, 0, 0);
+  }
+  mid();
+}
+
 // Forward form: C[m][p] = sum_k A[k][m] * B[k][p], BK = G * 16 (G tap-groups per K-step).
 template <int BM, int BN, int BK, int WM, int WN>
 __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
@@ -906,6 +941,38 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
 }
 
 
+// The forward-form image operand pre-split (variant bit 7, r03): planes[((cb*NP + q)*2 + h)*P + p] =
+// 16 B = plane q of the 8 channels cb*16 + 8h .. +7 of pixel p, scaled by the tensor's power of two
+// (0 past cimg).  NP = 2 (f16x3: hi, lo) or 1 (fp16: hi).  One thread per (cb, h, p): eight loads
+// coalesced over p, one or two 16-B stores.
+template <int NP>
+__global__ void __launch_bounds__(256) k_split_img(const float* __restrict__ x, int cimg, int ncb, int P,
+                                                   const float* __restrict__ part, int npart,
+                                                   f16x8* __restrict__ planes) {
+  float inv;
+  const float sc = pow2_scale(partials_max(part, npart, threadIdx.x & 63), inv);
+  const long long n = (long long)ncb * 2 * P;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const int p = (int)(e % P);
+    const int r = (int)(e / P);
+    const int h = r & 1, cb = r >> 1;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cb * kCB + 8 * h + j;
+      v[j] = c < cimg ? x[(long long)c * P + p] * sc : 0.f;
+    }
+    Split2h sp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (NP == 1) sp.hi[j] = (_Float16)v[j];
+      else split2h_set(sp, j, v[j]);
+    }
+    planes[((long long)(cb * NP) * 2 + h) * P + p] = sp.hi;
+    if constexpr (NP == 2) planes[((long long)(cb * NP + 1) * 2 + h) * P + p] = sp.lo;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Stream-K forward form.  The (tile, stage) iteration space of all output tiles is cut into NW
 // equal ranges, one per persistent workgroup (NW = CUs x resident workgroups per CU), so every
@@ -959,7 +1026,7 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
 // each, more than the K-step's 12 MFMAs).  Every wave of the 1 x 4 layout reads its own 32 columns,
 // so nothing is lost by not sharing B through LDS.
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false>
+          bool BD = false, bool BP = false>
 __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -989,7 +1056,8 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr int BG_INST_W = BPRE ? 6 * NH / 4 : PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B DMAs per wave per K-step
 #endif
   static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
-  constexpr int INST_W = A_INST_W + G * (BD ? 8 : BG_INST_W);
+  static_assert(!BP || BD, "BP: the BD form with a pre-split image");
+  constexpr int INST_W = A_INST_W + G * (BP ? (H1 ? 1 : 2) : BD ? 8 : BG_INST_W);
   static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
   static_assert((STAGES - 2) * INST_W < 64, "vmcnt range");
   // ONE __shared__ object: a second one (even a 4-byte flag) makes hipcc emit vmcnt(0) before the
@@ -1029,7 +1097,8 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * NQ * a.lda * 16), 0x00020000);
   const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.Bx6, (short)0, (int)min(0x7fffffffLL, (long long)a.ncb * 6 * a.P * 16), 0x00020000);
+      (void*)a.Bx6, (short)0,
+      (int)min(0x7fffffffLL, (long long)a.ncb * (BP ? (H1 ? 2 : 4) : 6) * a.P * 16), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
   const unsigned chan_bytes = (unsigned)a.P * 4u;
   // f16x3: B's scale from its absmax partials, A's from the pack; the result is unscaled by both
@@ -1105,7 +1174,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       const int shift = dh * a.W + dw;
       if constexpr (BD) {
         const bool v = pbd < a.P && (unsigned)(pyd + dh) < (unsigned)a.H && (unsigned)(pxd + dw) < (unsigned)a.W;
-        vbd = v ? (unsigned)((pbd + shift) * 4) : OOB;
+        vbd = v ? (unsigned)((pbd + shift) * (BP ? 16 : 4)) : OOB;
       } else {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
@@ -1161,7 +1230,19 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int cb16 = c_cb * kCB;
-        if constexpr (BD) {
+        if constexpr (BP) {
+          // the pre-split planes: 16 B per plane of this lane's pixel (hi, then lo)
+          constexpr int NPB = H1 ? 1 : 2;
+          const unsigned pl_bytes = (unsigned)a.P * 16u;
+#pragma unroll
+          for (int q = 0; q < NPB; ++q) {
+            const unsigned row = (unsigned)((c_cb * NPB + q) * 2 + (lane >> 5)) * pl_bytes;
+            union { u32x4 u; float f[4]; } c;
+            c.u = __builtin_amdgcn_raw_buffer_load_b128(rbx, vbd + row, 0, 0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bq[4 * q + j] = c.f[j];
+          }
+        } else if constexpr (BD) {
           // channels cb16 + 8h + j of this lane's pixel; a channel past cimg reads 0 (OOB offset;
           // OOB + c * P * 4 stays >= 2^31 since cimg * P * 4 < 2^31)
           const int ci0 = cb16 + 8 * (lane >> 5);
@@ -1244,7 +1325,10 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         auto mid = [&] {
           if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt);
         };
-        mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
+        if constexpr (BP)
+          mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
+        else
+          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       };
       for (int i = 0; i < nst; i += 4) {
@@ -1392,9 +1476,9 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 // The same kernel held to two waves per SIMD (<= 256 VGPRs + AGPRs): the f16x3 form, left to the
 // compiler's default budget, takes 199 VGPRs + 64 AGPRs and one wave per SIMD.
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false>
+          bool BD = false, bool BP = false>
 __global__ void __launch_bounds__(256, 2) k_igemm_fwd_sk2(FwdArgs a, SkArgs sk) {
-  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD>(a, sk);
+  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD, BP>(a, sk);
 }
 
 // sum of pieces w_lo..w_hi in that order (deterministic), eight loads in flight per step: a tile

@@ -135,6 +135,8 @@ def load(require_gpu=True):
     if lib.msl_abi_version() != ABI_VERSION:
         raise MSLError("libmsl_hip.so ABI version mismatch; rebuild it")
     _lib = lib
+    if os.environ.get("MSL_CONV_VARIANT"):  # kernel-form experiments (msl_conv_set_variant) for a whole run
+        check(lib.msl_conv_set_variant(int(os.environ["MSL_CONV_VARIANT"])), "msl_conv_set_variant")
     return lib
 
 
