@@ -81,8 +81,9 @@ int msl_conv_set_sk_hybrid(int on);
  * remainder after data-parallel rounds spread at one K-step per workgroup (the r02 split); bit 4 =
  * the f16x3 3x3 GEMMs with M <= 64 (ASPP forward, layer1) on exact-f32 32 / 64-row tiles; bit 5 =
  * those 64-row f16x3 GEMMs as chunked split-K in channel-block-major K order; bit 6 = the
- * fp16 weight-gradient GEMMs with the image values two stages ahead (PIPE 2); bit 7 = the f16x3 /
- * fp16 forward-form GEMMs read an image pre-split into fp16 planes by one pass ahead of the GEMM.
+ * fp16 weight-gradient GEMMs with the image values two stages ahead (PIPE 2); bit 7 flips which f16x3 /
+ * fp16 forward-form GEMMs read an image pre-split into fp16 planes by one pass ahead of the GEMM
+ * (default: the 3x3 GEMMs with M >= 512).
  * MSL_CONV_VARIANT in the environment sets it when the Python host loads the library.
  * MSL_ERR_ARG for a negative value. */
 int msl_conv_set_variant(int variant);

@@ -574,8 +574,12 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
           a.bnpart = kNPart;
         }
         a.ascale = packed + pack_tail_offset(f32) + kNPart;
-        const bool bp = (g_variant & 128) != 0;
-        if (bp) {  // pre-split the image operand once for the whole GEMM (behind the pieces)
+        // the image operand pre-split once for the whole GEMM (BP form, behind the pieces): pays on
+        // the layer4 3x3 GEMMs (M = 512: the split pass is shared by 4 row blocks and 9 taps), fwd
+        // 162 vs 174 us, dgrad 172 vs 185; loses where the pass is a large share (pointwise 39 vs
+        // 31 us, layer2 34 vs 31, ASPP 144 vs 135) - profiles/r03_bp_ab.txt.  Variant bit 7 flips it.
+        const bool bp = (taps == 9 && M >= 512 && !small_f16) != ((g_variant & 128) != 0);
+        if (bp) {
           f16x8* planes = reinterpret_cast<f16x8*>((char*)ws + fwd_piece_bytes(pl));
           const long long n = (long long)a.ncb * 2 * P;
           const dim3 sgrid((unsigned)std::min<long long>(cdiv(n, 256), 8192));
