@@ -4,7 +4,8 @@
 
 A "step" is one iteration of tools/solve_gta5.py:335-387: one source image
 (fwd, CE, bwd) + one target image (fwd, MaxSquare, bwd) + the gradient
-all-reduce (N > 1) + the SGD step, i.e. 2 images per rank per step.  Workload =
+all-reduce (N > 1) + the SGD step, i.e. 2 images per rank per step (by default
+the two images run as one pair: per-image BN statistics, one GEMM per conv).  Workload =
 BASELINE.json configs[1]: GTA5->Cityscapes MaxSquare, 1024x512, bs=1/GPU,
 random-init (counter generator) weights, synthetic inputs already in HBM,
 --multi False, lambda_target 0.1, fp32.  Scaling is weak (bs=1 per GPU).
@@ -66,8 +67,11 @@ def parse():
                     help="matrix-core form of the fp32 convs (default: the library's)")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: iterations after the first replay one captured hipGraph (single process); 0: eager")
+    ap.add_argument("--pair", type=int, default=1,
+                    help="1: source and target images run through the network as one image pair (one GEMM per conv "
+                         "over both, per-image BN statistics, one backward); 0: two forward/backward passes")
     ap.add_argument("--overlap", type=int, default=1,
-                    help="1: the target forward runs on a side stream concurrently with the source backward")
+                    help="with --pair 0: the target forward runs on a side stream concurrently with the source backward")
     ap.add_argument("--async-wgrad", type=int, default=0,
                     help="1: in-place weight gradients on a side stream beside the data-gradient chain (ops.ASYNC_WGRAD)")
     ap.add_argument("--variant", type=int, default=0, help="msl_conv_set_variant (kernel-form A/B experiments)")
@@ -86,7 +90,7 @@ def main():
             "--imagenet_pretrained", "False", "--save_dir", "", "--num_classes", str(a.num_classes),
             "--target_mode", a.target_mode, "--multi", a.multi, "--lambda_target", str(a.lambda_target),
             "--iter_max", "200000", "--conv_math", a.conv_math, "--graph", str(bool(a.graph)),
-            "--overlap", str(bool(a.overlap))]
+            "--overlap", str(bool(a.overlap)), "--pair", str(bool(a.pair))]
     if a.f32_form:
         argv += ["--f32_form", a.f32_form]
     args, _, _ = init_args(build_parser().parse_args(argv))
@@ -109,7 +113,8 @@ def main():
     torch.cuda.synchronize()
 
     h3, w3 = feat_hw(H), feat_hw(W)
-    key = (1, 256, 256, h3, w3, 2)
+    nimg = 2 if tr.pair else 1  # images per layer3 conv call
+    key = (1, 256, 256, h3, w3, 2, nimg)
     graphed = bool(tr.use_graph)
     first_losses = None
     for i in range(max(a.warmup, 1 if graphed else 0)):
@@ -119,7 +124,7 @@ def main():
     torch.cuda.synchronize()
     if not graphed:
         ops.PROBE[key] = []
-        if tr.overlap:  # eager: time the probe's kernel on its own in one sequential iteration below
+        if tr.overlap and not tr.pair:  # eager: time the probe's kernel on its own in one sequential iteration below
             ops.PROBE.pop(key)
 
     if dist.is_initialized():
@@ -157,7 +162,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    flops = 2.0 * 256 * 256 * 9 * h3 * w3
+    flops = 2.0 * 256 * 256 * 9 * h3 * w3 * nimg
     achieved = flops / (kern_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(a.pmc):
@@ -178,9 +183,9 @@ def main():
                 "traffic_source": (os.path.relpath(a.pmc, ROOT) + ": committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                    "passes of this kernel (scripts/gpu_bench_prof.sh), not measured in this run; "
                                    "memory-side bytes incl. Infinity-Cache hits") if traffic is not None else None,
-                "frac_of_fp32_spec": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "frac_of_bf16x6_bound": round(achieved / (BF16_MFMA_PEAK_TFLOPS / 6), 4),
-                "kernel": "dconv3x3 fwd layer3 d=2 (one op call: stream-K k_igemm_fwd_sk(2) + k_sk_reduce; the weight planes are split at pack time, once per SGD step; f16x3: the input's absmax partials come from the BN kernel that produced it)",
+                "fp32_equiv_tflops_over_fp32_spec": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "fp32_equiv_tflops_over_bf16x6_bound": round(achieved / (BF16_MFMA_PEAK_TFLOPS / 6), 4),
+                "kernel": f"dconv3x3 fwd layer3 d=2 over {nimg} image(s) (one op call: stream-K k_igemm_fwd_sk(2) + k_sk_reduce; the weight planes are split at pack time, once per SGD step; f16x3: the input's absmax partials come from the BN kernel that produced it)",
                 "form": form, "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
 
@@ -217,7 +222,7 @@ def main():
         "data": "synthetic (counter-generated uint8 images -> BGR-mean, uniform labels; random-init weights)",
         "config": {"workload": f"{'SYNTHIA' if C == 16 else 'GTA5'}->Cityscapes {args.target_mode} UDA step "
                                f"(solve_gta5.py), {W}x{H}, bs=1/GPU",
-                   "conv_math": a.conv_math, "bn_form": a.bn_form, "hipgraph": graphed, "overlap": bool(a.overlap), "async_wgrad": bool(a.async_wgrad), "variant": a.variant, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
+                   "conv_math": a.conv_math, "bn_form": a.bn_form, "hipgraph": graphed, "pair": bool(a.pair), "overlap": bool(a.overlap), "async_wgrad": bool(a.async_wgrad), "variant": a.variant, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
                    "target_mode": args.target_mode, "multi": args.multi, "lambda_target": args.lambda_target,
                    "num_classes": C, "global_batch": 2 * world, "parallelism": f"dp{world}"},
         "roofline": roofline, "cpu_baseline": cpu,

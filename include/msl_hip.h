@@ -95,6 +95,10 @@ int msl_conv_set_variant(int variant);
  * or the live part of an ASPP head (nbranch = 2: conv_d6(x) + conv_d12(x) with
  * biases, Classifier_Module.forward, deeplab_multi.py:62-66 incl. quirk Q1).
  * Weights of branch b start at w + b*branch_stride, shape [cout][cin][3][3].
+ * Images: x / y / dy / dx hold nimg images of h x w as [channels][nimg][h][w] (nimg = 1: the
+ * reference's bs = 1 NCHW layout).  Each image is convolved on its own (a tap never reads across
+ * into the neighbouring image); the weight gradient sums over all of them.  The trainer runs the
+ * source and target images of an iteration as one pair (nimg = 2).
  * ---------------------------------------------------------------------- */
 
 /* Elements (fp32 units) of the packed operand produced by msl_dconv_pack (for_dgrad = 0:
@@ -124,22 +128,22 @@ int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin
 
 /* y[cout][h][w] = sum_b conv3x3(x, W_b, dil_b) (+ sum_b bias[b][cout] if bias)
  * replaces nn.Conv2d.forward at deeplab_multi.py:35 (layer3/4) and :63-65 (ASPP). */
-size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w);
+size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w, int nimg);
 int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                  int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                   size_t ws_bytes, msl_stream_t stream);
 
 /* dx[cin][h][w] = sum_b conv3x3^T(dy, W_b, dil_b)   (autograd of the same sites) */
-size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w);
+size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg);
 int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                     size_t ws_bytes, msl_stream_t stream);
 
 /* dw[b][cout][cin][3][3] (= or += when accumulate) and, if dbias != NULL,
  * dbias[b][cout] = sum_px dy (identical for both branches). */
-size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w);
+size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg);
 int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
                     size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
@@ -189,10 +193,12 @@ int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cou
  *   - x[:, :, ::s, ::s] (the stride of layer2.0's 1x1 conv1 and downsample, deeplab_multi.py:12-13,
  *     96-99) and its transpose (zeros elsewhere) for the gradient.
  * ---------------------------------------------------------------------- */
-int msl_im2col(const float* x, int c, int h, int w, int kh, int kw, int stride, int pad, int dil, int ho, int wo,
-               float* col, msl_stream_t stream);
-int msl_col2im(const float* col, int c, int h, int w, int kh, int kw, int stride, int pad, int dil, int ho, int wo,
-               float* x, msl_stream_t stream);
+/* im2col / col2im over nimg images: x [c][nimg][h][w], col [c*kh*kw][nimg][ho][wo].  The pooling
+ * and subsample entry points are per plane: call them with c = channels * nimg. */
+int msl_im2col(const float* x, int c, int h, int w, int nimg, int kh, int kw, int stride, int pad, int dil, int ho,
+               int wo, float* col, msl_stream_t stream);
+int msl_col2im(const float* col, int c, int h, int w, int nimg, int kh, int kw, int stride, int pad, int dil, int ho,
+               int wo, float* x, msl_stream_t stream);
 int msl_maxpool_fwd(const float* x, int c, int h, int w, int k, int stride, int pad, int ho, int wo, float* y,
                     int32_t* idx, msl_stream_t stream);
 int msl_maxpool_bwd(const float* dy, const int32_t* idx, int c, int h, int w, int k, int stride, int pad, int ho,
@@ -219,13 +225,13 @@ int msl_subsample_bwd(const float* dy, int c, int h, int w, int stride, int ho, 
  * ---------------------------------------------------------------------- */
 int msl_absmax_partials(const float* x, int rows, int row_len, float* part, msl_stream_t stream);
 int msl_dconv_fwd_sc(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                     int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                     int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                      size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart);
 int msl_dconv_dgrad_sc(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                       int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                       int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                        size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart);
 int msl_dconv_wgrad_sc(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                       int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                       int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
                        size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
                        const float* dy_part, int dy_npart);
 int msl_pconv_fwd_sc(const float* x, const float* packed, float* y, int cin, int cout, int p,
@@ -245,13 +251,13 @@ int msl_pconv_wgrad_sc(const float* x, const float* dy, float* dw, int cin, int 
  * v_mfma_f32_32x32x16_bf16 with fp32 accumulation.  Same reference sites.
  * ---------------------------------------------------------------------- */
 int msl_dconv_fwd_bf16(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                       int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                       int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                        size_t ws_bytes, msl_stream_t stream);
 int msl_dconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                         int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                         int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                          size_t ws_bytes, msl_stream_t stream);
 int msl_dconv_wgrad_bf16(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
-                         int cin, int cout, int h, int w, int dil0, int dil1, int accumulate,
+                         int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate,
                          void* ws, size_t ws_bytes, msl_stream_t stream);
 int msl_pconv_fwd_bf16(const float* x, const float* packed, float* y, int cin, int cout, int p,
                        int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
@@ -271,13 +277,13 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
  * accumulate flag of msl_pconv_dgrad_acc.  Same workspaces and results layout.
  * ---------------------------------------------------------------------- */
 int msl_dconv_fwd_f16(const float* x, const float* packed, const float* bias, float* y, int nbranch, int cin,
-                      int cout, int h, int w, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                      int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
                       msl_stream_t stream, const float* x_part, int x_npart);
 int msl_dconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin, int cout,
-                        int h, int w, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                        int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
                         msl_stream_t stream, const float* dy_part, int dy_npart);
 int msl_dconv_wgrad_f16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin, int cout,
-                        int h, int w, int dil0, int dil1, int accumulate, void* ws, size_t ws_bytes,
+                        int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws, size_t ws_bytes,
                         msl_stream_t stream, const float* x_part, int x_npart, const float* dy_part, int dy_npart);
 int msl_pconv_fwd_f16(const float* x, const float* packed, float* y, int cin, int cout, int p, int* counters,
                       void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart);
@@ -372,16 +378,19 @@ int msl_iw_maxsquare_prob_bwd(const float* prob, int c, int hw, const float* wei
 /* ------------------------------------------------------------------------
  * BatchNorm2d fused with the Bottleneck's ReLU / residual add (deeplab_multi.py:31-46,
  * :115-117): y = act(bn(x) [+ residual]), act = ReLU if relu else identity.
- * training = 1: batch statistics over the p = H*W pixels of each of the c channels
- * (bs = 1, quirk Q9), accumulated in fp64; running stats updated with momentum and
- * the unbiased variance when update_running; num_batches_tracked (nullable) += 1.
- * training = 0: running statistics (model.eval() / --freeze_bn).
- * save_mean / save_invstd [c] are outputs consumed by msl_bn_bwd.
+ * Layout [c][nimg][p]: nimg images of p = H*W pixels each.
+ * training = 1: batch statistics over the p pixels of each channel of each image on its own
+ * (bs = 1, quirk Q9: the reference's source and target forwards are separate batches),
+ * accumulated in fp64; running stats updated with momentum and the unbiased variance when
+ * update_running, image by image in order (exactly nimg sequential bs=1 calls);
+ * num_batches_tracked (nullable) += nimg.  training = 0: running statistics (model.eval() /
+ * --freeze_bn).  save_mean / save_invstd [c][nimg] are outputs consumed by msl_bn_bwd, which sums
+ * dgamma / dbeta image by image in order (as nimg accumulating calls would).
  * ---------------------------------------------------------------------- */
-size_t msl_bn_workspace(int c, int p);
+size_t msl_bn_workspace(int c, int p, int nimg);
 int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const float* residual,
                float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
-               float* save_mean, float* save_invstd, int c, int p, int training,
+               float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
                int update_running, float momentum, float eps, int relu, void* ws,
                size_t ws_bytes, msl_stream_t stream);
 /* dx (nullable), dres = d residual (nullable), dgamma / dbeta (nullable, = or += when
@@ -389,7 +398,7 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
  * y is the forward output (needed when relu). */
 int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gamma,
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
-               float* dgamma, float* dbeta, int c, int p, int training, int relu,
+               float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
                int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream);
 /* msl_bn_fwd / msl_bn_bwd that also write absmax[c] = max |y[c][.]| (forward) or max |dx[c][.]|
  * (backward; dx required): the per-channel absmax partials (c of them) that the f16x3 conv
@@ -398,12 +407,12 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
  * kernels reduce it in registers; the split forms add one pass over the output. */
 int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const float* residual,
                   float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
-                  float* save_mean, float* save_invstd, int c, int p, int training,
+                  float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
                   int update_running, float momentum, float eps, int relu, void* ws,
                   size_t ws_bytes, msl_stream_t stream, float* absmax);
 int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* gamma,
                   const float* save_mean, const float* save_invstd, float* dx, float* dres,
-                  float* dgamma, float* dbeta, int c, int p, int training, int relu,
+                  float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
                   int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx);
 /* 1 if msl_bn_fwd / msl_bn_bwd run the fused one-block-per-channel kernels for this shape (their
  * _am absmax output is then free; the split forms add a pass over the output). */

@@ -8,7 +8,10 @@
 // statistics are accumulated in fp64 around a per-channel shift (its first element), which
 // is at least as accurate as the CPU's two-pass fp32 sums.
 //
-// Layout [C][P] (N = 1).  Train mode on layer1-4 maps: one fused launch per call (see
+// Layout [C][NI][P]: NI images (bs = 1 each: every image gets its own batch statistics, as the
+// reference's separate source and target forwards do), P pixels per image; row r = c*NI + n holds
+// channel c of image n.  Running statistics are updated image by image in order (n = 0 first),
+// dgamma / dbeta summed image by image in order.  Train mode on layer1-4 maps: one fused launch per call (see
 // k_bn_fwd_fused).  Otherwise: forward: stats kernel (grid C x S partial fp64 sums per channel) +
 // a flat apply kernel over the whole tensor in float4s (each block folds the partials of the
 // channels it touches).  Backward: per-channel reduce (sum g, sum g*xhat with g = dy masked by
@@ -98,54 +101,72 @@ struct BnArgs {
   float* save_invstd;
   long long* num_batches;
   const double* part;
-  int C, P, S, chunk, relu, training, update_running;
+  int C, NI, P, S, chunk, relu, training, update_running;  // C channels, NI images, P pixels per image
   float eps, momentum;
   float* absmax;  // [C] max |y| per channel (msl_bn_fwd_am: the next conv's f16x3 partials) or null
 };
 
-// Flat apply: block b covers elements [b*chunk, (b+1)*chunk) of the [C][P] tensor (possibly
-// several channels).  Each block derives the (alpha, beta') of the channels it touches from the
-// fp64 partial sums; the block holding a channel's first element also publishes its saved /
-// running statistics.
+// Batch statistics of row r (channel r / NI of image r % NI) from the fp64 partial sums.
+__device__ __forceinline__ void bn_row_stats(const BnArgs& a, int r, float& mean, float& invstd, double& var) {
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < a.S; ++s) {
+    s1 += a.part[((long long)r * a.S + s) * 2];
+    s2 += a.part[((long long)r * a.S + s) * 2 + 1];
+  }
+  const double n = (double)a.P;
+  const double shift = (double)a.x[(long long)r * a.P];
+  const double dm = s1 / n;
+  var = s2 / n - dm * dm;
+  if (var < 0.0) var = 0.0;
+  mean = (float)(shift + dm);
+  invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+}
+
+// running statistics of channel c <- image n's batch statistics (one image after the other)
+__device__ __forceinline__ void bn_running_update(const BnArgs& a, int c, float mean, double var) {
+  const double n = (double)a.P;
+  const float m = a.momentum;
+  const float unbiased = (float)(a.P > 1 ? var * n / (n - 1.0) : var);
+  a.running_mean[c] = (1.f - m) * a.running_mean[c] + m * mean;
+  a.running_var[c] = (1.f - m) * a.running_var[c] + m * unbiased;
+}
+
+// Flat apply: block b covers elements [b*chunk, (b+1)*chunk) of the [C*NI][P] tensor (possibly
+// several rows).  Each block derives the (alpha, beta') of the rows it touches from the fp64
+// partial sums; the block holding a row's first element also publishes its saved statistics, and
+// the one holding a channel's first row (image 0) updates its running statistics image by image.
 template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_apply(BnArgs a) {
   __shared__ float coef[2][256];
-  const long long N = (long long)a.C * a.P;
+  const long long N = (long long)a.C * a.NI * a.P;
   const long long start = (long long)blockIdx.x * a.chunk;
   const long long end = min(N, start + a.chunk);
   const int c0 = (int)(start / a.P);
   const int nch = (int)((end - 1) / a.P) - c0 + 1;
   if ((int)threadIdx.x < nch) {
-    const int c = c0 + threadIdx.x;
-    const bool owner = (long long)c * a.P >= start;  // this block holds the channel's first element
+    const int r = c0 + threadIdx.x;  // row = (channel, image)
+    const int c = r / a.NI;
+    const bool owner = (long long)r * a.P >= start;  // this block holds the row's first element
     float mean, invstd;
     if (a.training) {
-      double s1 = 0.0, s2 = 0.0;
-      for (int s = 0; s < a.S; ++s) {
-        s1 += a.part[((long long)c * a.S + s) * 2];
-        s2 += a.part[((long long)c * a.S + s) * 2 + 1];
-      }
-      const double n = (double)a.P;
-      const double shift = (double)a.x[(long long)c * a.P];
-      const double dm = s1 / n;
-      double var = s2 / n - dm * dm;
-      if (var < 0.0) var = 0.0;
-      mean = (float)(shift + dm);
-      invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-      if (owner && a.update_running) {
-        const float m = a.momentum;
-        const float unbiased = (float)(a.P > 1 ? var * n / (n - 1.0) : var);
-        a.running_mean[c] = (1.f - m) * a.running_mean[c] + m * mean;
-        a.running_var[c] = (1.f - m) * a.running_var[c] + m * unbiased;
-        if (c == 0 && a.num_batches) a.num_batches[0] += 1;
+      double var;
+      bn_row_stats(a, r, mean, invstd, var);
+      if (owner && a.update_running && r % a.NI == 0) {
+        for (int n = 0; n < a.NI; ++n) {
+          float mn, is;
+          double vn;
+          bn_row_stats(a, r + n, mn, is, vn);
+          bn_running_update(a, c, mn, vn);
+        }
+        if (c == 0 && a.num_batches) a.num_batches[0] += a.NI;
       }
     } else {
       mean = a.running_mean[c];
       invstd = 1.f / sqrtf(a.running_var[c] + a.eps);
     }
     if (owner) {
-      a.save_mean[c] = mean;
-      a.save_invstd[c] = invstd;
+      a.save_mean[r] = mean;
+      a.save_invstd[r] = invstd;
     }
     // y = x * alpha + beta'  (batch_norm_cpu_transform_input form)
     const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
@@ -190,7 +211,7 @@ struct BnBwdArgs {
   float* dgamma;
   float* dbeta;
   double* part;
-  int C, P, S, chunk, relu, training, accumulate;
+  int C, NI, P, S, chunk, relu, training, accumulate;
   float* absmax;  // [C] max |dx| per channel (msl_bn_bwd_am) or null
 };
 
@@ -229,28 +250,44 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(BnBwdArgs a) {
 template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
   __shared__ float coef[5][256];
-  const long long N = (long long)a.C * a.P;
+  const long long N = (long long)a.C * a.NI * a.P;
   const long long start = (long long)blockIdx.x * a.chunk;
   const long long end = min(N, start + a.chunk);
   const int c0 = (int)(start / a.P);
   const int nch = (int)((end - 1) / a.P) - c0 + 1;
-  if ((int)threadIdx.x < nch) {
-    const int c = c0 + threadIdx.x;
-    double sg = 0.0, sgx = 0.0;
+  auto sums = [&](int r, double& sg, double& sgx) {
+    sg = sgx = 0.0;
     for (int s = 0; s < a.S; ++s) {
-      sg += a.part[((long long)c * a.S + s) * 2];
-      sgx += a.part[((long long)c * a.S + s) * 2 + 1];
+      sg += a.part[((long long)r * a.S + s) * 2];
+      sgx += a.part[((long long)r * a.S + s) * 2 + 1];
     }
-    if ((long long)c * a.P >= start) {
-      if (a.dgamma) a.dgamma[c] = a.accumulate ? a.dgamma[c] + (float)sgx : (float)sgx;
-      if (a.dbeta) a.dbeta[c] = a.accumulate ? a.dbeta[c] + (float)sg : (float)sg;
+  };
+  if ((int)threadIdx.x < nch) {
+    const int r = c0 + threadIdx.x;  // row = (channel, image)
+    const int c = r / a.NI;
+    double sg, sgx;
+    sums(r, sg, sgx);
+    if ((long long)r * a.P >= start && r % a.NI == 0) {  // the channel's parameter gradients, image by image
+      float dg = sgx, db = sg;
+      if (a.accumulate) {
+        dg = a.dgamma ? a.dgamma[c] + (float)sgx : 0.f;
+        db = a.dbeta ? a.dbeta[c] + (float)sg : 0.f;
+      }
+      for (int n = 1; n < a.NI; ++n) {
+        double g1, g2;
+        sums(r + n, g1, g2);
+        dg += (float)g2;
+        db += (float)g1;
+      }
+      if (a.dgamma) a.dgamma[c] = dg;
+      if (a.dbeta) a.dbeta[c] = db;
     }
     const float w = a.gamma ? a.gamma[c] : 1.f;
-    coef[0][threadIdx.x] = a.save_invstd[c] * w;  // invstd * gamma
+    coef[0][threadIdx.x] = a.save_invstd[r] * w;  // invstd * gamma
     coef[1][threadIdx.x] = a.training ? (float)(sg / (double)a.P) : 0.f;
     coef[2][threadIdx.x] = a.training ? (float)(sgx / (double)a.P) : 0.f;
-    coef[3][threadIdx.x] = a.save_mean[c];
-    coef[4][threadIdx.x] = a.save_invstd[c];
+    coef[3][threadIdx.x] = a.save_mean[r];
+    coef[4][threadIdx.x] = a.save_invstd[r];
   }
   __syncthreads();
   const long long cbound = (long long)(c0 + 1) * a.P;
@@ -374,7 +411,11 @@ template <int EPT>
 __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
   __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
-  const long long base = (long long)c * P;
+  float am = 0.f;
+  for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
+  if (img) __syncthreads();               // red[] is reused
+  const int r = c * a.NI + img;
+  const long long base = (long long)r * P;
   const float* xc = a.x + base;
   float xv[EPT], rv[EPT];
 #pragma unroll
@@ -412,13 +453,12 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
       a.running_var[c] = (1.f - m) * a.running_var[c] + m * unbiased;
       if (c == 0 && a.num_batches) a.num_batches[0] += 1;
     }
-    a.save_mean[c] = mean;
-    a.save_invstd[c] = invstd;
+    a.save_mean[r] = mean;
+    a.save_invstd[r] = invstd;
   }
   const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
   const float bsh = (a.beta ? a.beta[c] : 0.f) - mean * alpha;
   float* yc = a.y + base;
-  float am = 0.f;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
@@ -430,6 +470,7 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
       am = fmaxf(am, fabsf(v));
     }
   }
+  }  // images
   if (a.absmax) {
     __shared__ float redm[kBnFusedThreads / 64];
     am = block_max16(am, redm);
@@ -441,8 +482,13 @@ template <int EPT>
 __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
   __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
-  const long long base = (long long)c * P;
-  const float mean = a.save_mean[c], invstd = a.save_invstd[c];
+  float am = 0.f;
+  float dg = 0.f, db = 0.f;  // the parameter gradients, image by image (thread 0)
+  for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
+  if (img) __syncthreads();               // red[] is reused
+  const int r = c * a.NI + img;
+  const long long base = (long long)r * P;
+  const float mean = a.save_mean[r], invstd = a.save_invstd[r];
   float g[EPT], xv[EPT];
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
@@ -466,12 +512,16 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
   }
   block_sum2_d16(sg, sgx, red);
   if (t == 0) {
-    if (a.dgamma) a.dgamma[c] = a.accumulate ? a.dgamma[c] + (float)sgx : (float)sgx;
-    if (a.dbeta) a.dbeta[c] = a.accumulate ? a.dbeta[c] + (float)sg : (float)sg;
+    if (img == 0) {
+      dg = (a.accumulate && a.dgamma) ? a.dgamma[c] + (float)sgx : (float)sgx;
+      db = (a.accumulate && a.dbeta) ? a.dbeta[c] + (float)sg : (float)sg;
+    } else {
+      dg += (float)sgx;
+      db += (float)sg;
+    }
   }
   const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
   const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
-  float am = 0.f;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
@@ -482,6 +532,11 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
       if (a.dx) a.dx[base + e] = d;
       am = fmaxf(am, fabsf(d));
     }
+  }
+  }  // images
+  if (t == 0) {
+    if (a.dgamma) a.dgamma[c] = dg;
+    if (a.dbeta) a.dbeta[c] = db;
   }
   if (a.absmax) {
     __shared__ float redm[kBnFusedThreads / 64];
@@ -518,38 +573,40 @@ int msl_bn_uses_fused(int c, int p, int training) {
   return training && bn_fused_enabled() && c >= 1 && p >= 1 && bn_fused_shape(c, p) ? 1 : 0;
 }
 
-size_t msl_bn_workspace(int c, int p) {
-  return align_up((size_t)c * bn_splits(p) * 2 * sizeof(double), 256);
+size_t msl_bn_workspace(int c, int p, int nimg) {
+  return align_up((size_t)c * std::max(nimg, 1) * bn_splits(p) * 2 * sizeof(double), 256);
 }
 
 int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const float* residual,
                float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
-               float* save_mean, float* save_invstd, int c, int p, int training,
+               float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
                int update_running, float momentum, float eps, int relu, void* ws,
                size_t ws_bytes, msl_stream_t stream) {
   return msl_bn_fwd_am(x, gamma, beta, residual, y, running_mean, running_var, num_batches_tracked, save_mean,
-                       save_invstd, c, p, training, update_running, momentum, eps, relu, ws, ws_bytes, stream,
+                       save_invstd, c, p, nimg, training, update_running, momentum, eps, relu, ws, ws_bytes, stream,
                        nullptr);
 }
 
 int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const float* residual,
                   float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
-                  float* save_mean, float* save_invstd, int c, int p, int training,
+                  float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
                   int update_running, float momentum, float eps, int relu, void* ws,
                   size_t ws_bytes, msl_stream_t stream, float* absmax) {
-  if (!x || !y || !save_mean || !save_invstd || c < 1 || p < 1) return MSL_ERR_ARG;
+  if (!x || !y || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
+    return MSL_ERR_ARG;
   if ((!training || update_running) && (!running_mean || !running_var)) return MSL_ERR_ARG;
   hipStream_t st = as_stream(stream);
   const int S = bn_splits(p);
-  if (training && ws_bytes < msl_bn_workspace(c, p)) return MSL_ERR_WORKSPACE;
+  const int R = c * nimg;  // rows (channel, image)
+  if (training && ws_bytes < msl_bn_workspace(c, p, nimg)) return MSL_ERR_WORKSPACE;
   double* part = (double*)ws;
   const bool vec = al16(x) && al16(y) && (!residual || al16(residual));
   const bool fused = training && bn_fused_enabled() && bn_fused_shape(c, p);
   if (training && !fused) {
     if (vec)
-      hipLaunchKernelGGL(k_bn_stats<true>, dim3(c, S), dim3(256), 0, st, x, p, S, part);
+      hipLaunchKernelGGL(k_bn_stats<true>, dim3(R, S), dim3(256), 0, st, x, p, S, part);
     else
-      hipLaunchKernelGGL(k_bn_stats<false>, dim3(c, S), dim3(256), 0, st, x, p, S, part);
+      hipLaunchKernelGGL(k_bn_stats<false>, dim3(R, S), dim3(256), 0, st, x, p, S, part);
     MSL_CHECK_LAUNCH();
   }
   BnArgs a;
@@ -565,6 +622,7 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
   a.num_batches = num_batches_tracked;
   a.part = part;
   a.C = c;
+  a.NI = nimg;
   a.P = p;
   a.S = S;
   a.chunk = bn_flat_chunk(p);
@@ -575,33 +633,36 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
   a.momentum = momentum;
   a.absmax = absmax;
   if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>, c, p, st, a);
-  const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
+  const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec)
     hipLaunchKernelGGL(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(k_bn_apply<false>, dim3(blocks), dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
-  if (absmax) return absmax_rows(y, c, p, absmax, st);  // the split forms: a pass of its own over y
+  if (absmax) return absmax_rows(y, c, nimg * p, absmax, st);  // the split forms: a pass of its own over y
   return MSL_OK;
 }
 
 int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gamma,
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
-               float* dgamma, float* dbeta, int c, int p, int training, int relu,
+               float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
                int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream) {
-  return msl_bn_bwd_am(dy, x, y, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, training, relu,
+  return msl_bn_bwd_am(dy, x, y, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, nimg, training, relu,
                        accumulate_params, ws, ws_bytes, stream, nullptr);
 }
 
 int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* gamma,
                   const float* save_mean, const float* save_invstd, float* dx, float* dres,
-                  float* dgamma, float* dbeta, int c, int p, int training, int relu,
+                  float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
                   int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
-  if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || (relu && !y)) return MSL_ERR_ARG;
+  if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31) ||
+      (relu && !y))
+    return MSL_ERR_ARG;
   if (absmax_dx && !dx) return MSL_ERR_ARG;
-  if (ws_bytes < msl_bn_workspace(c, p)) return MSL_ERR_WORKSPACE;
+  if (ws_bytes < msl_bn_workspace(c, p, nimg)) return MSL_ERR_WORKSPACE;
   hipStream_t st = as_stream(stream);
   const int S = bn_splits(p);
+  const int R = c * nimg;  // rows (channel, image)
   BnBwdArgs a;
   a.dy = dy;
   a.x = x;
@@ -615,6 +676,7 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
   a.dbeta = dbeta;
   a.part = (double*)ws;
   a.C = c;
+  a.NI = nimg;
   a.P = p;
   a.S = S;
   a.chunk = bn_flat_chunk(p);
@@ -625,18 +687,18 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
   if (training && bn_fused_enabled() && bn_fused_shape(c, p))
     return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
-  const unsigned blocks = (unsigned)cdiv((long long)c * p, (long long)a.chunk);
+  const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec) {
-    hipLaunchKernelGGL(k_bn_bwd_reduce<true>, dim3(c, S), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_bn_bwd_reduce<true>, dim3(R, S), dim3(256), 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_bn_bwd_apply<true>, dim3(blocks), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(c, S), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(R, S), dim3(256), 0, st, a);
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_bn_bwd_apply<false>, dim3(blocks), dim3(256), 0, st, a);
   }
   MSL_CHECK_LAUNCH();
-  if (absmax_dx) return absmax_rows(dx, c, p, absmax_dx, st);  // the split forms: a pass over dx
+  if (absmax_dx) return absmax_rows(dx, c, nimg * p, absmax_dx, st);  // the split forms: a pass over dx
   return MSL_OK;
 }
 

@@ -443,10 +443,10 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
 
 template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
-                           int nbias, float* out, int nbranch, int taps, int h, int w, int dil0,
+                           int nbias, float* out, int nbranch, int taps, int h, int w, int nimg, int dil0,
                            int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st,
                            int accum = 0, const float* img_part = nullptr, int img_npart = 0) {
-  const int P = h * w;
+  const int P = nimg * h * w;  // nimg images of h x w stacked along the pixel axis
   FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
   // The x6 form runs one K-step per stage, three stages deep (scripts/tune_dconv.hip x6, layer3:
   // 87 us vs 115 with two K-steps per stage; f32 is indifferent); its 64- and 32-row tiles stay
@@ -651,9 +651,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   return MSL_OK;
 }
 
-static bool bad_dims(int nbranch, int cin, int cout, int h, int w) {
-  return nbranch < 1 || nbranch > 2 || cin < 1 || cout < 1 || h < 1 || w < 1 ||
-         (long long)h * w > (1LL << 30);
+static bool bad_dims(int nbranch, int cin, int cout, int h, int w, int nimg = 1) {
+  return nbranch < 1 || nbranch > 2 || cin < 1 || cout < 1 || h < 1 || w < 1 || nimg < 1 ||
+         (long long)nimg * h * w > (1LL << 30);
 }
 
 // ---------------------------------------------------------------- shared by 3x3 and pointwise
@@ -744,11 +744,11 @@ static size_t wgrad_ws_bytes(int nbranch, int taps, int cin, int cout, int P, in
 
 template <int MT>
 static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
-                        int taps, int cin, int cout, int h, int w, int dil0, int dil1,
+                        int taps, int cin, int cout, int h, int w, int nimg, int dil0, int dil1,
                         int accumulate, void* ws, size_t ws_bytes, hipStream_t st,
                         const float* x_part = nullptr, int x_npart = 0, const float* dy_part = nullptr,
                         int dy_npart = 0) {
-  const int P = h * w;
+  const int P = nimg * h * w;
   constexpr bool F16 = MT == kMathH3P || MT == kMathH1P;
   constexpr bool X6L = MT == kMathX6 || F16;
   constexpr int MS = X6L ? kMathF32 : MT;  // the split forms only on 128x128 tiles (plan_wgrad)
@@ -786,6 +786,7 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   a.accumulate = accumulate;
   a.slots = pl.slots;
   a.invW = 1.0f / (float)w;
+  a.invH = 1.0f / (float)h;
   a.tiles_m = pl.tiles_m;
   a.tiles_n = pl.tiles_n;
   a.KS = pl.KS;
@@ -977,50 +978,53 @@ int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, i
   return MSL_OK;
 }
 
-size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w) {
-  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
+size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w, int nimg) {
+  if (bad_dims(nbranch, cin, cout, h, w, nimg)) return 0;
+  const int P = nimg * h * w;
   // large enough with or without a bias (the plan depends on it)
-  return std::max(fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, h * w, false), cout, h * w, cin),
-                  fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, h * w, true), cout, h * w, cin));
+  return std::max(fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, P, false), cout, P, cin),
+                  fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, P, true), cout, P, cin));
 }
 
 int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                  int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                   size_t ws_bytes, msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return fwd_f32(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
+  return fwd_f32(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
-size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
-  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
-  return fwd_ws_bytes(plan_fwd(nbranch, 9, cout, cin, h * w, false), cin, h * w, cout);
+size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg) {
+  if (bad_dims(nbranch, cin, cout, h, w, nimg)) return 0;
+  const int P = nimg * h * w;
+  return fwd_ws_bytes(plan_fwd(nbranch, 9, cout, cin, P, false), cin, P, cout);
 }
 
 int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                     size_t ws_bytes, msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
-size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w) {
-  if (bad_dims(nbranch, cin, cout, h, w)) return 0;
-  return wgrad_ws_bytes(nbranch, 9, cin, cout, h * w, w);
+size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg) {
+  if (bad_dims(nbranch, cin, cout, h, w, nimg)) return 0;
+  const int P = nimg * h * w;
+  return wgrad_ws_bytes(nbranch, 9, cin, cout, P, w);
 }
 
 int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
                     size_t ws_bytes, msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return wgrad_f32(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
+  return wgrad_f32(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws,
                       ws_bytes, as_stream(stream));
 }
 
@@ -1044,7 +1048,7 @@ size_t msl_pconv_fwd_workspace(int cin, int cout, int p) {
 int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
                   int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return fwd_f32(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
+  return fwd_f32(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws,
                          ws_bytes, as_stream(stream));
 }
 
@@ -1056,7 +1060,7 @@ size_t msl_pconv_dgrad_workspace(int cin, int cout, int p) {
 int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters,
                          ws, ws_bytes, as_stream(stream));
 }
 
@@ -1064,9 +1068,9 @@ int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, i
                         int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
   if (!accumulate)
-    return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+    return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
                    as_stream(stream));
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
                  as_stream(stream), 1);
 }
 
@@ -1078,36 +1082,36 @@ int msl_absmax_partials(const float* x, int rows, int row_len, float* part, msl_
 }
 
 int msl_dconv_fwd_sc(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                     int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                     int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                      size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart) {
   if (bad_parts(x_part, x_npart)) return MSL_ERR_ARG;
-  if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return fwd_f32(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1, counters, ws, ws_bytes,
+  return fwd_f32(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1, counters, ws, ws_bytes,
                  as_stream(stream), 0, x_part, x_npart);
 }
 
 int msl_dconv_dgrad_sc(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                       int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                       int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                        size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart) {
   if (bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
-  if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1, counters, ws,
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1, counters, ws,
                  ws_bytes, as_stream(stream), 0, dy_part, dy_npart);
 }
 
 int msl_dconv_wgrad_sc(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                       int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                       int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
                        size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
                        const float* dy_part, int dy_npart) {
   if (bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
-  if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return wgrad_f32(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws, ws_bytes,
+  return wgrad_f32(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws, ws_bytes,
                    as_stream(stream), x_part, x_npart, dy_part, dy_npart);
 }
 
@@ -1116,7 +1120,7 @@ int msl_pconv_fwd_sc(const float* x, const float* packed, float* y, int cin, int
                      int x_npart) {
   if (bad_parts(x_part, x_npart)) return MSL_ERR_ARG;
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return fwd_f32(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+  return fwd_f32(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
                  as_stream(stream), 0, x_part, x_npart);
 }
 
@@ -1125,7 +1129,7 @@ int msl_pconv_dgrad_acc_sc(const float* dy, const float* packed_dgrad, float* dx
                            const float* dy_part, int dy_npart) {
   if (bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
                  as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart);
 }
 
@@ -1134,7 +1138,7 @@ int msl_pconv_wgrad_sc(const float* x, const float* dy, float* dw, int cin, int 
                        int x_npart, const float* dy_part, int dy_npart) {
   if (bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
-  return wgrad_f32(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes, as_stream(stream),
+  return wgrad_f32(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes, as_stream(stream),
                    x_part, x_npart, dy_part, dy_npart);
 }
 
@@ -1146,7 +1150,7 @@ size_t msl_pconv_wgrad_workspace(int cin, int cout, int p) {
 int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,
                     int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
-  return wgrad_f32(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+  return wgrad_f32(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes,
                       as_stream(stream));
 }
 
@@ -1155,53 +1159,53 @@ int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cou
 // Same operands, workspaces and results layout; products in bf16 (RNE from the fp32 operands),
 // sums in fp32 (BASELINE config 5's fp16/bf16 MFMA path).
 int msl_dconv_fwd_bf16(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                  int cin, int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                   size_t ws_bytes, msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathBf16>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1,
+  return launch_fwd_form<kMathBf16>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
 int msl_dconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, int* counters, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
                     size_t ws_bytes, msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+  return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1,
                          counters, ws, ws_bytes, as_stream(stream));
 }
 
 int msl_dconv_wgrad_bf16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                    int cout, int h, int w, int dil0, int dil1, int accumulate, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
                     size_t ws_bytes, msl_stream_t stream) {
-  if (bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 ||
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_wgrad<kMathBf16>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws,
+  return launch_wgrad<kMathBf16>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws,
                       ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_fwd_bf16(const float* x, const float* packed, float* y, int cin, int cout, int p,
                   int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return launch_fwd_form<kMathBf16>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws,
+  return launch_fwd_form<kMathBf16>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws,
                          ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters,
+  return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters,
                          ws, ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, int cout, int p,
                     int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
-  return launch_wgrad<kMathBf16>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+  return launch_wgrad<kMathBf16>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes,
                       as_stream(stream));
 }
 
@@ -1214,32 +1218,32 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
 static bool f16_ready() { return g_f32_form == kMathH3P; }
 
 int msl_dconv_fwd_f16(const float* x, const float* packed, const float* bias, float* y, int nbranch, int cin,
-                      int cout, int h, int w, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                      int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
                       msl_stream_t stream, const float* x_part, int x_npart) {
-  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_dims(nbranch, cin, cout, h, w) || !x || !packed || !y ||
+  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y ||
       dil0 < 1 || (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, dil0, dil1, counters,
+  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1, counters,
                                    ws, ws_bytes, as_stream(stream), 0, x_part, x_npart);
 }
 
 int msl_dconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin, int cout,
-                        int h, int w, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                        int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
                         msl_stream_t stream, const float* dy_part, int dy_npart) {
-  if (!f16_ready() || bad_parts(dy_part, dy_npart) || bad_dims(nbranch, cin, cout, h, w) || !dy || !packed_dgrad ||
+  if (!f16_ready() || bad_parts(dy_part, dy_npart) || bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad ||
       !dx || dil0 < 1 || (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, dil0, dil1,
+  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1,
                                    counters, ws, ws_bytes, as_stream(stream), 0, dy_part, dy_npart);
 }
 
 int msl_dconv_wgrad_f16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin, int cout,
-                        int h, int w, int dil0, int dil1, int accumulate, void* ws, size_t ws_bytes,
+                        int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws, size_t ws_bytes,
                         msl_stream_t stream, const float* x_part, int x_npart, const float* dy_part, int dy_npart) {
   if (!f16_ready() || bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart) ||
-      bad_dims(nbranch, cin, cout, h, w) || !x || !dy || !dw || dil0 < 1 || (nbranch == 2 && dil1 < 1))
+      bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !dy || !dw || dil0 < 1 || (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_wgrad<kMathH1P>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, dil0, dil1, accumulate, ws, ws_bytes,
+  return launch_wgrad<kMathH1P>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws, ws_bytes,
                                 as_stream(stream), x_part, x_npart, dy_part, dy_npart);
 }
 
@@ -1247,7 +1251,7 @@ int msl_pconv_fwd_f16(const float* x, const float* packed, float* y, int cin, in
                       void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart) {
   if (!f16_ready() || bad_parts(x_part, x_npart) || bad_dims(1, cin, cout, 1, p) || !x || !packed || !y)
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 0, 0, counters, ws, ws_bytes,
+  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
                                    as_stream(stream), 0, x_part, x_npart);
 }
 
@@ -1256,7 +1260,7 @@ int msl_pconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, i
                         const float* dy_part, int dy_npart) {
   if (!f16_ready() || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx)
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 0, 0, counters, ws,
+  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws,
                                    ws_bytes, as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart);
 }
 
@@ -1266,7 +1270,7 @@ int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int
   if (!f16_ready() || bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) ||
       !x || !dy || !dw)
     return MSL_ERR_ARG;
-  return launch_wgrad<kMathH1P>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 0, 0, accumulate, ws, ws_bytes,
+  return launch_wgrad<kMathH1P>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes,
                                 as_stream(stream), x_part, x_npart, dy_part, dy_npart);
 }
 

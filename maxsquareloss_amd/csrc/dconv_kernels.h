@@ -18,6 +18,9 @@ struct FwdArgs {
   float* C;           // out [M][P] or slabs [S][M][P]
   const float* bias;  // [nbias][M] or null (only used when S == 1)
   int nbias;
+  // H x W = one image; P = nimg * H * W pixels: a batch of images stacked along the pixel axis
+  // ([C][nimg][H][W]), a tap's shifted read never crossing into the neighbouring image (its row
+  // is validated modulo H)
   int M, lda, H, W, P, cimg, ncb, dil0, dil1, ksteps, kps;  // ksteps counts BK-deep steps
   int taps;           // 9 (3x3) or 1 (pointwise: dil0 = 0, so the single tap has no shift)
   long long slab;
@@ -604,7 +607,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
   constexpr int BPASS = kCB / BROWS;     // passes per tap-group
   const int bn = tid % BN, brow0 = tid / BN;
   const int p = n0 + bn;
-  const int py = p / a.W, px = p - py * a.W;
+  const int pq = p / a.W, px = p - pq * a.W, py = pq % a.H;  // row within its image
   const bool pin = p < a.P;
 
   constexpr int A_F4_ROW = BM / 4;
@@ -741,7 +744,7 @@ __global__ void __launch_bounds__(256) k_igemm_wgrad(WgradArgs a) {
   auto gload = [&](int s) {
     const int p = s * BK + kl;
     const bool pv = p < a.P;
-    const int py = p / a.W, px = p - py * a.W;
+    const int pq = p / a.W, px = p - pq * a.W, py = pq % a.H;
     const bool vb = pv && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
     const int off = p + dh * a.W + dw;
 #pragma unroll
@@ -856,8 +859,9 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
   for (int h = 0; h < NH; ++h) {
     const int p = n0 + h * 64 + lane;
     pin[h] = p < a.P;
-    py[h] = p / a.W;
-    px[h] = p - py[h] * a.W;
+    const int pq = p / a.W;
+    px[h] = p - pq * a.W;
+    py[h] = pq % a.H;
   }
   const int per_b = a.ncb * a.taps;
   constexpr unsigned OOB = 0x80000000u;
@@ -1143,8 +1147,9 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     for (int h = 0; h < NH; ++h) {
       const int p = n0 + h * 64 + lane;
       pin[h] = p < a.P;
-      py[h] = p / a.W;
-      px[h] = p - py[h] * a.W;
+      const int pq = p / a.W;
+      px[h] = p - pq * a.W;
+      py[h] = pq % a.H;
     }
     // Issue cursor over the K-steps, in order (K is tap-major: ks = (branch*taps + tap)*ncb + cb):
     // the wave-uniform (tap, channel block) advances incrementally and the per-lane shifted pixel
@@ -1153,7 +1158,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     unsigned vrow[NH];
     unsigned vbd = OOB;  // BD: this lane's shifted pixel byte offset (OOB outside the image)
     const int pbd = n0 + wn + (lane & 31);
-    const int pyd = pbd / a.W, pxd = pbd - pyd * a.W;
+    const int pqd = pbd / a.W, pxd = pbd - pqd * a.W, pyd = pqd % a.H;
     {
       const int ks0 = k_a * G;
       if (a.tapinner) {  // logical K-step = cb * nz + z
@@ -1701,8 +1706,9 @@ __global__ void __launch_bounds__(256) k_conv_rg(FwdArgs a, SkArgs sk) {
     for (int j = 0; j < TN; ++j) {
       const int p = n0 + wn + j * 32 + (lane & 31);
       pin[j] = p < a.P;
-      py[j] = p / a.W;
-      px[j] = p - py[j] * a.W;
+      const int pq = p / a.W;
+      px[j] = p - pq * a.W;
+      py[j] = pq % a.H;
     }
     // K-step ks -> branch, tap row, channel block, dilation, window start
     auto decode = [&](int ks, int& br, int& ty, int& cb, int& d, int& s) {
@@ -1826,8 +1832,8 @@ struct WskArgs {
   const float* x;   // [N][P]
   float* dw;        // [nbranch][M][N][taps]
   float* part;      // [NW][slots][BM][BN]: worker w's piece of tile t in slot t - first_tile(w)
-  int M, N, H, W, P, dil0, dil1, taps, accumulate, slots;
-  float invW;
+  int M, N, H, W, P, dil0, dil1, taps, accumulate, slots;  // H x W one image, P = nimg * H * W
+  float invW, invH;
   int tiles_m, tiles_n, KS, NW, T;
   long long cbranch;  // M * N * taps
   const void* dyx6;   // k_wgrad_x6: dY split into bf16 planes by k_split_rows
@@ -1906,8 +1912,9 @@ __global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
       const int p = s * kWskBK + lane;
-      const int py = (int)(((float)p + 0.5f) * a.invW);
-      const int px = p - py * a.W;
+      const int pq = (int)(((float)p + 0.5f) * a.invW);
+      const int px = p - pq * a.W;
+      const int py = pq - a.H * (int)(((float)pq + 0.5f) * a.invH);  // row within its image
       const unsigned va = p < a.P ? (unsigned)p * 4u : OOB;
       const bool vb = p < a.P && (unsigned)(py + dh) < (unsigned)a.H && (unsigned)(px + dw) < (unsigned)a.W;
       const unsigned vbo = vb ? (unsigned)(p + shift) * 4u : OOB;
@@ -2345,7 +2352,8 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
     const int shift = dh * a.W + dw;
     // pixel cursor of the next K-step to load (scalar): ks*16 = cy*W + cx
     int ld_ks = k_a;
-    int cy = (k_a * kWx6BK) / a.W, cx = k_a * kWx6BK - cy * a.W;
+    int cy = (k_a * kWx6BK) / a.W, cx = k_a * kWx6BK - cy * a.W;  // cy: row within its image
+    cy %= a.H;
     const int clo = max(0, -dw), chi = a.W - max(0, dw);  // valid source columns px + dw
     auto seg = [](int lo, int hi) -> unsigned {      // bits lo .. hi-1 of a 16-bit mask
       lo = max(lo, 0);
@@ -2356,12 +2364,18 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       unsigned m16 = 0;
       if (ld_ks < k_b) {
         const int L1 = a.W - cx;  // pixels of the K-step left in row cy
+        const int cy1 = cy + 1 == a.H ? 0 : cy + 1;  // the next row (of the next image after the last)
         if ((unsigned)(cy + dh) < (unsigned)a.H) m16 |= seg(clo - cx, min(L1, chi - cx));
-        if ((unsigned)(cy + 1 + dh) < (unsigned)a.H) m16 |= seg(L1 + clo, L1 + chi);
+        if ((unsigned)(cy1 + dh) < (unsigned)a.H) m16 |= seg(L1 + clo, L1 + chi);
+        const int left = a.P - ld_ks * kWx6BK;  // none past the last pixel
+        if (left < kWx6BK) m16 &= (1u << max(left, 0)) - 1u;
       }
       ++ld_ks;
       cx += kWx6BK;
-      if (cx >= a.W) { cx -= a.W; ++cy; }
+      if (cx >= a.W) {
+        cx -= a.W;
+        if (++cy == a.H) cy = 0;
+      }
       return m16;
     };
     if constexpr (H3) {

@@ -5,7 +5,7 @@
 #include <algorithm>
 #include "../../include/msl_hip.h"
 
-#define MSL_ABI_VERSION 1
+#define MSL_ABI_VERSION 2
 
 #define MSL_CHECK_LAUNCH()                         \
   do {                                             \

@@ -13,22 +13,26 @@
 
 namespace msl {
 
-// col[(c*KH + i)*KW + j][oy*WO + ox] = x[c][oy*S - PAD + i*D][ox*S - PAD + j*D] (0 outside the image).
-// Thread per (row k, output row oy, 4 output columns): the 4 stores are one float4 when WO % 4 == 0.
-__global__ void __launch_bounds__(256) k_im2col(const float* __restrict__ x, int H, int W, int KH, int KW, int S,
-                                                int PAD, int D, int HO, int WO, int K, float* __restrict__ col) {
+// col[(c*KH + i)*KW + j][n][oy*WO + ox] = x[c][n][oy*S - PAD + i*D][ox*S - PAD + j*D] (0 outside the
+// image) for the NI images n of a [C][NI][H][W] batch.  Thread per (row k, image, output row oy, 4
+// output columns): the 4 stores are one float4 when WO % 4 == 0.
+__global__ void __launch_bounds__(256) k_im2col(const float* __restrict__ x, int H, int W, int NI, int KH, int KW,
+                                                int S, int PAD, int D, int HO, int WO, int K,
+                                                float* __restrict__ col) {
   const int wq = (WO + 3) >> 2;
-  const long long total = (long long)K * HO * wq;
-  const long long P = (long long)HO * WO;
+  const long long total = (long long)K * NI * HO * wq;
+  const long long P = (long long)NI * HO * WO;
   for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
     const int q = (int)(e % wq);
     const long long r = e / wq;
     const int oy = (int)(r % HO);
-    const int k = (int)(r / HO);
+    const long long r2 = r / HO;
+    const int n = (int)(r2 % NI);
+    const int k = (int)(r2 / NI);
     const int j = k % KW, i = (k / KW) % KH, c = k / (KW * KH);
     const int iy = oy * S - PAD + i * D;
     const bool rowok = (unsigned)iy < (unsigned)H;
-    const float* src = x + ((long long)c * H + (rowok ? iy : 0)) * W;
+    const float* src = x + (((long long)c * NI + n) * H + (rowok ? iy : 0)) * W;
     float v[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -36,7 +40,7 @@ __global__ void __launch_bounds__(256) k_im2col(const float* __restrict__ x, int
       const int ix = ox * S - PAD + j * D;
       v[t] = (rowok && ox < WO && (unsigned)ix < (unsigned)W) ? src[ix] : 0.f;
     }
-    float* dst = col + (long long)k * P + (long long)oy * WO + q * 4;
+    float* dst = col + (long long)k * P + ((long long)n * HO + oy) * WO + q * 4;
     if ((WO & 3) == 0) {
       *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
     } else {
@@ -45,17 +49,19 @@ __global__ void __launch_bounds__(256) k_im2col(const float* __restrict__ x, int
   }
 }
 
-// x[c][y][xx] = sum over (i, j) (i-major) of col[(c*KH + i)*KW + j][oy][ox] for every window
+// x[c][n][y][xx] = sum over (i, j) (i-major) of col[(c*KH + i)*KW + j][n][oy][ox] for every window
 // position that maps (oy, ox) onto (y, xx).
-__global__ void __launch_bounds__(256) k_col2im(const float* __restrict__ col, int C, int H, int W, int KH, int KW,
-                                                int S, int PAD, int D, int HO, int WO, float* __restrict__ x) {
-  const long long total = (long long)C * H * W;
-  const long long P = (long long)HO * WO;
+__global__ void __launch_bounds__(256) k_col2im(const float* __restrict__ col, int C, int H, int W, int NI, int KH,
+                                                int KW, int S, int PAD, int D, int HO, int WO, float* __restrict__ x) {
+  const long long total = (long long)C * NI * H * W;
+  const long long P = (long long)NI * HO * WO;
   for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
     const int xx = (int)(e % W);
     const long long r = e / W;
     const int y = (int)(r % H);
-    const int c = (int)(r / H);
+    const long long r2 = r / H;
+    const int n = (int)(r2 % NI);
+    const int c = (int)(r2 / NI);
     float s = 0.f;
     for (int i = 0; i < KH; ++i) {
       const int ty = y + PAD - i * D;
@@ -67,7 +73,7 @@ __global__ void __launch_bounds__(256) k_col2im(const float* __restrict__ col, i
         if (tx < 0 || tx % S) continue;
         const int ox = tx / S;
         if (ox >= WO) continue;
-        s += col[((long long)(c * KH + i) * KW + j) * P + (long long)oy * WO + ox];
+        s += col[((long long)(c * KH + i) * KW + j) * P + ((long long)n * HO + oy) * WO + ox];
       }
     }
     x[e] = s;
@@ -169,26 +175,28 @@ using namespace msl;
 
 extern "C" {
 
-int msl_im2col(const float* x, int c, int h, int w, int kh, int kw, int stride, int pad, int dil, int ho, int wo,
-               float* col, msl_stream_t stream) {
-  if (!x || !col || bad_geom(c, h, w, std::max(kh, kw), stride, pad, ho, wo) || kh < 1 || kw < 1 || dil < 1 ||
-      (long long)c * kh * kw * ho * wo >= (1LL << 40))
+int msl_im2col(const float* x, int c, int h, int w, int nimg, int kh, int kw, int stride, int pad, int dil, int ho,
+               int wo, float* col, msl_stream_t stream) {
+  if (!x || !col || nimg < 1 || bad_geom(c * nimg, h, w, std::max(kh, kw), stride, pad, ho, wo) || kh < 1 ||
+      kw < 1 || dil < 1 || (long long)c * kh * kw * nimg * ho * wo >= (1LL << 40) ||
+      (long long)nimg * ho * wo >= (1LL << 31))
     return MSL_ERR_ARG;
   const int K = c * kh * kw;
-  const long long n = (long long)K * ho * ((wo + 3) / 4);
-  hipLaunchKernelGGL(k_im2col, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, kh, kw, stride, pad, dil,
-                     ho, wo, K, col);
+  const long long n = (long long)K * nimg * ho * ((wo + 3) / 4);
+  hipLaunchKernelGGL(k_im2col, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, nimg, kh, kw, stride, pad,
+                     dil, ho, wo, K, col);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
 
-int msl_col2im(const float* col, int c, int h, int w, int kh, int kw, int stride, int pad, int dil, int ho, int wo,
-               float* x, msl_stream_t stream) {
-  if (!x || !col || bad_geom(c, h, w, std::max(kh, kw), stride, pad, ho, wo) || kh < 1 || kw < 1 || dil < 1)
+int msl_col2im(const float* col, int c, int h, int w, int nimg, int kh, int kw, int stride, int pad, int dil, int ho,
+               int wo, float* x, msl_stream_t stream) {
+  if (!x || !col || nimg < 1 || bad_geom(c * nimg, h, w, std::max(kh, kw), stride, pad, ho, wo) || kh < 1 ||
+      kw < 1 || dil < 1 || (long long)nimg * ho * wo >= (1LL << 31))
     return MSL_ERR_ARG;
-  const long long n = (long long)c * h * w;
-  hipLaunchKernelGGL(k_col2im, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), col, c, h, w, kh, kw, stride, pad,
-                     dil, ho, wo, x);
+  const long long n = (long long)c * nimg * h * w;
+  hipLaunchKernelGGL(k_col2im, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), col, c, h, w, nimg, kh, kw, stride,
+                     pad, dil, ho, wo, x);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }

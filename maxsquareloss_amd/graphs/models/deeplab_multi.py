@@ -185,18 +185,34 @@ class ResNetMulti(nn.Module):
     def _make_pred_layer(self, block, inplanes, dilation_series, padding_series, num_classes):
         return block(inplanes, dilation_series, padding_series, num_classes)
 
-    def forward(self, x):
-        input_size = x.size()[2:]
+    def _heads(self, x):
+        """The trunk and both heads on (1,3,H,W) or an image batch (1,3,N,H,W): (layer6, layer5)
+        low-resolution logits."""
         x = self.maxpool(ops.bn_act(self.bn1, self.conv1(x), relu=True))
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)
         x1 = self.layer5(x)
-        x1 = ops.upsample_bilinear(x1, input_size)
         x2 = self.layer4(x)
         x2 = self.layer6(x2)
-        x2 = ops.upsample_bilinear(x2, input_size)
         return x2, x1
+
+    def forward(self, x):
+        input_size = x.size()[2:]
+        x2, x1 = self._heads(x)
+        return ops.upsample_bilinear(x2, input_size), ops.upsample_bilinear(x1, input_size)
+
+    def forward_pair(self, x_s, x_t):
+        """forward(x_s), forward(x_t) as one image pair (not in the reference): every conv GEMM runs
+        once over both images, while each image keeps its own bs=1 BatchNorm statistics (the
+        running statistics are updated source first, then target, as two forwards would) and its
+        own padding.  Returns [(x2_s, x1_s), (x2_t, x1_t)]."""
+        if x_s.shape != x_t.shape:
+            raise ValueError("forward_pair: source and target images must have the same size")
+        input_size = x_s.size()[2:]
+        x2, x1 = self._heads(ops.pair_join(x_s, x_t))
+        return [(ops.upsample_bilinear(a, input_size), ops.upsample_bilinear(b, input_size))
+                for a, b in zip(ops.pair_split(x2), ops.pair_split(x1))]
 
     def get_1x_lr_params_NOscale(self):
         """Backbone parameters, each yielded once per enclosing module (quirk Q2)."""

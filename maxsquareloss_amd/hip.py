@@ -23,18 +23,18 @@ SIGNATURES = {
     "msl_dconv_pack": (c_int, [c_p, c_ll, c_int, c_int, c_int, c_int, c_p, c_p]),
     "msl_conv_pack_blocks": (c_ll, [c_int] * 5),
     "msl_conv_pack_many": (c_int, [c_p, c_p, c_int, c_int, c_ll, c_p]),
-    "msl_dconv_fwd_workspace": (c_sz, [c_int] * 5),
+    "msl_dconv_fwd_workspace": (c_sz, [c_int] * 6),
     "msl_counter_elems": (c_int, []),
     "msl_conv_set_f32_form": (c_int, [c_int]),
     "msl_conv_f32_form": (c_int, []),
     "msl_conv_set_sk_hybrid": (c_int, [c_int]),
     "msl_conv_set_variant": (c_int, [c_int]),
     "msl_conv_set_pack_form": (c_int, [c_int]),
-    "msl_dconv_fwd": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
-    "msl_dconv_dgrad_workspace": (c_sz, [c_int] * 5),
-    "msl_dconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
-    "msl_dconv_wgrad_workspace": (c_sz, [c_int] * 5),
-    "msl_dconv_wgrad": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p]),
+    "msl_dconv_fwd": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
+    "msl_dconv_dgrad_workspace": (c_sz, [c_int] * 6),
+    "msl_dconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
+    "msl_dconv_wgrad_workspace": (c_sz, [c_int] * 6),
+    "msl_dconv_wgrad": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_sz, c_p]),
     "msl_pconv_packed_elems": (c_ll, [c_int] * 3),
     "msl_pconv_pack": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p]),
     "msl_pconv_fwd_workspace": (c_sz, [c_int] * 3),
@@ -45,21 +45,21 @@ SIGNATURES = {
     "msl_pconv_wgrad_workspace": (c_sz, [c_int] * 3),
     "msl_pconv_wgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
     "msl_absmax_partials": (c_int, [c_p, c_int, c_int, c_p, c_p]),
-    "msl_dconv_fwd_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
-    "msl_dconv_dgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
-    "msl_dconv_wgrad_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_dconv_fwd_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_dconv_dgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_dconv_wgrad_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
     "msl_pconv_fwd_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_dgrad_acc_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_wgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
-    "msl_dconv_fwd_f16": (c_int, [c_p] * 4 + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
-    "msl_dconv_dgrad_f16": (c_int, [c_p] * 3 + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
-    "msl_dconv_wgrad_f16": (c_int, [c_p] * 4 + [c_int] * 8 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_dconv_fwd_f16": (c_int, [c_p] * 4 + [c_int] * 8 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_dconv_dgrad_f16": (c_int, [c_p] * 3 + [c_int] * 8 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
+    "msl_dconv_wgrad_f16": (c_int, [c_p] * 4 + [c_int] * 9 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
     "msl_pconv_fwd_f16": (c_int, [c_p] * 3 + [c_int] * 3 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_dgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_wgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
-    "msl_dconv_fwd_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
-    "msl_dconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p, c_p, c_sz, c_p]),
-    "msl_dconv_wgrad_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_sz, c_p]),
+    "msl_dconv_fwd_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
+    "msl_dconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
+    "msl_dconv_wgrad_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_sz, c_p]),
     "msl_pconv_fwd_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_wgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
@@ -85,15 +85,15 @@ SIGNATURES = {
     "msl_bn_set_fused": (c_int, [c_int]),
     "msl_bn_fused": (c_int, []),
     "msl_bn_uses_fused": (c_int, [c_int, c_int, c_int]),
-    "msl_bn_workspace": (c_sz, [c_int, c_int]),
-    "msl_bn_fwd": (c_int, [c_p] * 10 + [c_int] * 4 + [c_f, c_f, c_int, c_p, c_sz, c_p]),
-    "msl_bn_bwd": (c_int, [c_p] * 10 + [c_int] * 5 + [c_p, c_sz, c_p]),
-    "msl_bn_fwd_am": (c_int, [c_p] * 10 + [c_int] * 4 + [c_f, c_f, c_int, c_p, c_sz, c_p, c_p]),
-    "msl_bn_bwd_am": (c_int, [c_p] * 10 + [c_int] * 5 + [c_p, c_sz, c_p, c_p]),
+    "msl_bn_workspace": (c_sz, [c_int] * 3),
+    "msl_bn_fwd": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_sz, c_p]),
+    "msl_bn_bwd": (c_int, [c_p] * 10 + [c_int] * 6 + [c_p, c_sz, c_p]),
+    "msl_bn_fwd_am": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_sz, c_p, c_p]),
+    "msl_bn_bwd_am": (c_int, [c_p] * 10 + [c_int] * 6 + [c_p, c_sz, c_p, c_p]),
     "msl_image_transform": (c_int, [c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p, c_p]),
     "msl_label_transform": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
-    "msl_im2col": (c_int, [c_p] + [c_int] * 10 + [c_p, c_p]),
-    "msl_col2im": (c_int, [c_p] + [c_int] * 10 + [c_p, c_p]),
+    "msl_im2col": (c_int, [c_p] + [c_int] * 11 + [c_p, c_p]),
+    "msl_col2im": (c_int, [c_p] + [c_int] * 11 + [c_p, c_p]),
     "msl_maxpool_fwd": (c_int, [c_p] + [c_int] * 8 + [c_p, c_p, c_p]),
     "msl_maxpool_bwd": (c_int, [c_p, c_p] + [c_int] * 8 + [c_p, c_p]),
     "msl_subsample": (c_int, [c_p] + [c_int] * 6 + [c_p, c_p]),
@@ -104,7 +104,7 @@ SIGNATURES = {
     "msl_sgd_step_lr_dev": (c_int, [c_p, c_p, c_p, c_ll, c_p, c_f, c_f, c_f, c_p]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _lib = None
 
 

@@ -3,7 +3,11 @@
 Each Function is a thin shim: shape checks on the host, then one or two C-ABI
 calls on torch's current HIP stream.  Tensors are bs=1 NCHW fp32 (the
 reference only runs bs=1: IW_MaxSquareloss broadcasts (N,H,W) weights against
-(N,C,H,W) probabilities, which only works for N=1 - SURVEY.md quirk Q3).
+(N,C,H,W) probabilities, which only works for N=1 - SURVEY.md quirk Q3), or an
+image PAIR (1, C, 2, H, W): the source and target images of one UDA iteration laid
+out [C][2][H][W], each image convolved, pooled and batch-normalised on its own (its
+own bs=1 statistics) while every conv GEMM runs once over both (pair_join /
+pair_split; the trunk ops take either form, the losses one image).
 """
 from contextlib import nullcontext as _nullctx
 
@@ -128,11 +132,25 @@ def _split_gemm(m, k_other):
     return m > 64 or min(m, k_other) >= 128
 
 
-def _check_act(x, name):
-    if not x.is_cuda or x.dtype != _f32 or x.dim() != 4 or x.size(0) != 1:
-        raise hip.MSLError(f"{name}: expected a CUDA fp32 tensor of shape (1,C,H,W), got "
+def _check_act(x, name, images=False):
+    """x contiguous; with `images`, (1,C,H,W) or an image batch (1,C,N,H,W) ([C][N][H][W])."""
+    ok = x.is_cuda and x.dtype == _f32 and x.size(0) == 1 and (x.dim() == 4 or (images and x.dim() == 5))
+    if not ok:
+        shapes = "(1,C,H,W) or (1,C,N,H,W)" if images else "(1,C,H,W)"
+        raise hip.MSLError(f"{name}: expected a CUDA fp32 tensor of shape {shapes}, got "
                            f"{tuple(x.shape)} {x.dtype} {x.device}")
     return x.contiguous()
+
+
+def _nimg(x):
+    """Images in an activation: 1 for (1,C,H,W), N for (1,C,N,H,W)."""
+    return x.size(2) if x.dim() == 5 else 1
+
+
+def _like(x, c, h, w, dtype=_f32):
+    """An empty activation with x's image count and c channels of h x w."""
+    shape = (1, c, x.size(2), h, w) if x.dim() == 5 else (1, c, h, w)
+    return torch.empty(shape, dtype=dtype, device=x.device)
 
 
 # --------------------------------------------------------------------------- gradient sinks
@@ -352,44 +370,45 @@ class _DConv3x3(Function):
 
     @staticmethod
     def forward(ctx, x, w0, w1, b0, b1, dil0, dil1, cache):
-        x = _check_act(x, "dconv3x3")
+        x = _check_act(x, "dconv3x3", images=True)
+        n = _nimg(x)
         weights = [w0] if w1 is None else [w0, w1]
         nb = len(weights)
         cout, cin = w0.shape[0], w0.shape[1]
         if w0.shape[2:] != (3, 3) or x.size(1) != cin:
             raise hip.MSLError(f"dconv3x3: weight {tuple(w0.shape)} does not match input {tuple(x.shape)}")
-        h, w = x.shape[2], x.shape[3]
+        h, w = x.shape[-2], x.shape[-1]
         lib = hip.load()
         packed = cache.get(weights, cin, cout, 0)
         bias = None
         if b0 is not None:
             bias = torch.stack([b0] if nb == 1 else [b0, b1]).contiguous()
-        y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
-        wsb = lib.msl_dconv_fwd_workspace(nb, cin, cout, h, w)
+        y = _like(x, cout, h, w)
+        wsb = lib.msl_dconv_fwd_workspace(nb, cin, cout, h, w, n)
         ws = hip.workspace(wsb, x.device)
-        probe = PROBE.get((nb, cin, cout, h, w, dil0)) if PROBE else None
+        probe = PROBE.get((nb, cin, cout, h, w, dil0, n)) if PROBE else None
         if probe is not None:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         math = CONV_MATH
         xpart = _parts(x, math, compute=_split_gemm(cout, cin))
         hip.check(_conv_call(lib, "msl_dconv_fwd", math,
-                             (x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb, cin, cout, h, w, dil0,
-                              dil1 if nb > 1 else 0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                             (x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb, cin, cout, h, w, n,
+                              dil0, dil1 if nb > 1 else 0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
                               hip.stream_ptr()), (xpart,)), "msl_dconv_fwd")
         if probe is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             probe.append((ev0, ev1))
         ctx.save_for_backward(x, *weights)
-        ctx.meta = (nb, cin, cout, h, w, dil0, dil1, b0 is not None, cache, math)
+        ctx.meta = (nb, cin, cout, h, w, n, dil0, dil1, b0 is not None, cache, math)
         ctx.xpart = xpart
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, *weights = ctx.saved_tensors
-        nb, cin, cout, h, w, dil0, dil1, has_bias, cache, math = ctx.meta
+        nb, cin, cout, h, w, n, dil0, dil1, has_bias, cache, math = ctx.meta
         gy = gy.contiguous()
         lib = hip.load()
         s = hip.stream_ptr()
@@ -400,21 +419,21 @@ class _DConv3x3(Function):
         if ctx.needs_input_grad[0]:
             packed_d = cache.get(weights, cin, cout, 1)
             dx = torch.empty_like(x)
-            wsb = lib.msl_dconv_dgrad_workspace(nb, cin, cout, h, w)
+            wsb = lib.msl_dconv_dgrad_workspace(nb, cin, cout, h, w, n)
             ws = hip.workspace(wsb, x.device)
             hip.check(_conv_call(lib, "msl_dconv_dgrad", math,
-                                 (gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin, cout, h, w, dil0, d1,
+                                 (gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin, cout, h, w, n, dil0, d1,
                                   hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (gpart,)),
                       "msl_dconv_dgrad")
         sink = grad_sink(weights[0]) if (nb == 1 and not has_bias and ctx.needs_input_grad[1]) else None
-        wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w)
+        wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w, n)
         if sink is not None:
             g, fg, i = sink
             side = _wgrad_stream(x) if ASYNC_WGRAD else None
             with torch.cuda.stream(side) if side is not None else _nullctx():
                 ws = hip.workspace(wsb, x.device)
                 hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
-                                     (x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w, dil0, 0, 1,
+                                     (x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w, n, dil0, 0, 1,
                                       ws.data_ptr(), wsb, hip.stream_ptr()), (xpart, gpart)), "msl_dconv_wgrad")
             if side is not None:
                 _keep(side, x, gy, *(q[0] for q in (xpart, gpart) if q is not None))
@@ -425,7 +444,7 @@ class _DConv3x3(Function):
         db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
         hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
                              (x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb, cin, cout, h, w,
-                              dil0, d1, 0, ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
+                              n, dil0, d1, 0, ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
         dw0 = dw_all[0]
         dw1 = dw_all[1] if nb > 1 else None
         db0 = db_all[0] if has_bias else None
@@ -455,15 +474,15 @@ class _PConv(Function):
 
     @staticmethod
     def forward(ctx, x, weight, cache, hold=None):
-        x = _check_act(x, "pconv")
+        x = _check_act(x, "pconv", images=True)
         cout, cin = weight.shape[0], weight.shape[1]
         if weight.shape[2:] != (1, 1) or x.size(1) != cin:
             raise hip.MSLError(f"pconv: weight {tuple(weight.shape)} does not match input {tuple(x.shape)}")
-        h, w = x.shape[2], x.shape[3]
-        p = h * w
+        h, w = x.shape[-2], x.shape[-1]
+        p = h * w * _nimg(x)  # every image: the pixel axis of a pointwise GEMM
         lib = hip.load()
         packed = cache.get([weight], cin, cout, 0)
-        y = torch.empty((1, cout, h, w), dtype=_f32, device=x.device)
+        y = _like(x, cout, h, w)
         wsb = lib.msl_pconv_fwd_workspace(cin, cout, p)
         ws = hip.workspace(wsb, x.device)
         math = CONV_MATH
@@ -569,21 +588,21 @@ class _StemConv(Function):
 
     @staticmethod
     def forward(ctx, x, weight, stride, pad, cache):
-        x = _check_act(x, "stem_conv")
+        x = _check_act(x, "stem_conv", images=True)
         cout, cin, kh, kw = weight.shape
         if x.size(1) != cin:
             raise hip.MSLError(f"stem_conv: weight {tuple(weight.shape)} does not match input {tuple(x.shape)}")
-        h, w = x.shape[2], x.shape[3]
+        h, w, n = x.shape[-2], x.shape[-1], _nimg(x)
         ho, wo = (h + 2 * pad - kh) // stride + 1, (w + 2 * pad - kw) // stride + 1
-        kk, p = cin * kh * kw, ho * wo
+        kk, p = cin * kh * kw, ho * wo * n
         lib = hip.load()
         s = hip.stream_ptr()
-        col = torch.empty((1, kk, ho, wo), dtype=_f32, device=x.device)
-        hip.check(lib.msl_im2col(x.data_ptr(), cin, h, w, kh, kw, stride, pad, 1, ho, wo, col.data_ptr(), s),
+        col = _like(x, kk, ho, wo)
+        hip.check(lib.msl_im2col(x.data_ptr(), cin, h, w, n, kh, kw, stride, pad, 1, ho, wo, col.data_ptr(), s),
                   "msl_im2col")
         wmat = weight.detach().contiguous()
         packed = cache.get([wmat], kk, cout, 0)
-        y = torch.empty((1, cout, ho, wo), dtype=_f32, device=x.device)
+        y = _like(x, cout, ho, wo)
         wsb = lib.msl_pconv_fwd_workspace(kk, cout, p)
         ws = hip.workspace(wsb, x.device)
         # the bf16 conv math keeps the stem (the raw image, values ~1e2) in fp32: 8 significant bits
@@ -595,15 +614,15 @@ class _StemConv(Function):
                              (col.data_ptr(), packed.data_ptr(), y.data_ptr(), kk, cout, p,
                               hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (cpart,)), "msl_pconv_fwd")
         ctx.save_for_backward(col, weight)
-        ctx.meta = (cin, h, w, kh, kw, stride, pad, ho, wo, cache, math)
+        ctx.meta = (cin, h, w, n, kh, kw, stride, pad, ho, wo, cache, math)
         ctx.cpart = cpart
         return y
 
     @staticmethod
     def backward(ctx, gy):
         col, weight = ctx.saved_tensors
-        cin, h, w, kh, kw, stride, pad, ho, wo, cache, math = ctx.meta
-        cout, kk, p = weight.shape[0], col.size(1), ho * wo
+        cin, h, w, n, kh, kw, stride, pad, ho, wo, cache, math = ctx.meta
+        cout, kk, p = weight.shape[0], col.size(1), ho * wo * n
         gy = gy.contiguous()
         lib = hip.load()
         s = hip.stream_ptr()
@@ -623,8 +642,8 @@ class _StemConv(Function):
                 st = fn(gy.data_ptr(), packed_d.data_ptr(), dcol.data_ptr(), kk, cout, p, 0, cnt, ws.data_ptr(), wsb,
                         s, *_pp(gpart))
             hip.check(st, "msl_pconv_dgrad")
-            dx = torch.empty((1, cin, h, w), dtype=_f32, device=gy.device)
-            hip.check(lib.msl_col2im(dcol.data_ptr(), cin, h, w, kh, kw, stride, pad, 1, ho, wo, dx.data_ptr(), s),
+            dx = _like(col, cin, h, w)
+            hip.check(lib.msl_col2im(dcol.data_ptr(), cin, h, w, n, kh, kw, stride, pad, 1, ho, wo, dx.data_ptr(), s),
                       "msl_col2im")
         if not ctx.needs_input_grad[1]:
             return dx, None, None, None, None
@@ -653,15 +672,17 @@ def stem_conv(x, weight, stride, pad, cache):
 class _MaxPool(Function):
     @staticmethod
     def forward(ctx, x, k, s, p, ceil):
-        x = _check_act(x, "maxpool")
-        c, h, w = x.shape[1:]
+        x = _check_act(x, "maxpool", images=True)
+        h, w = x.shape[-2:]
+        c = x.size(1) * _nimg(x)  # per plane: every (channel, image)
         ho, wo = pool_out(h, k, s, p, ceil), pool_out(w, k, s, p, ceil)
-        y = torch.empty((1, c, ho, wo), dtype=_f32, device=x.device)
-        idx = torch.empty((1, c, ho, wo), dtype=torch.int32, device=x.device)
+        y = _like(x, x.size(1), ho, wo)
+        idx = _like(x, x.size(1), ho, wo, dtype=torch.int32)
         hip.check(hip.load().msl_maxpool_fwd(x.data_ptr(), c, h, w, k, s, p, ho, wo, y.data_ptr(), idx.data_ptr(),
                                              hip.stream_ptr()), "msl_maxpool_fwd")
         ctx.save_for_backward(idx)
         ctx.meta = (c, h, w, k, s, p, ho, wo)
+        ctx.xshape = x.shape
         ctx.mark_non_differentiable(idx)
         return y, idx
 
@@ -670,7 +691,7 @@ class _MaxPool(Function):
         (idx,) = ctx.saved_tensors
         c, h, w, k, s, p, ho, wo = ctx.meta
         gy = gy.contiguous()
-        dx = torch.empty((1, c, h, w), dtype=_f32, device=gy.device)
+        dx = torch.empty(ctx.xshape, dtype=_f32, device=gy.device)
         hip.check(hip.load().msl_maxpool_bwd(gy.data_ptr(), idx.data_ptr(), c, h, w, k, s, p, ho, wo, dx.data_ptr(),
                                              hip.stream_ptr()), "msl_maxpool_bwd")
         return dx, None, None, None, None
@@ -684,20 +705,22 @@ def maxpool2d(x, kernel_size, stride, padding, ceil_mode):
 class _Subsample(Function):
     @staticmethod
     def forward(ctx, x, s):
-        x = _check_act(x, "subsample")
-        c, h, w = x.shape[1:]
+        x = _check_act(x, "subsample", images=True)
+        h, w = x.shape[-2:]
+        c = x.size(1) * _nimg(x)  # per plane
         ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
-        y = torch.empty((1, c, ho, wo), dtype=_f32, device=x.device)
+        y = _like(x, x.size(1), ho, wo)
         hip.check(hip.load().msl_subsample(x.data_ptr(), c, h, w, s, ho, wo, y.data_ptr(), hip.stream_ptr()),
                   "msl_subsample")
         ctx.meta = (c, h, w, s, ho, wo)
+        ctx.xshape = x.shape
         return y
 
     @staticmethod
     def backward(ctx, gy):
         c, h, w, s, ho, wo = ctx.meta
         gy = gy.contiguous()
-        dx = torch.empty((1, c, h, w), dtype=_f32, device=gy.device)
+        dx = torch.empty(ctx.xshape, dtype=_f32, device=gy.device)
         hip.check(hip.load().msl_subsample_bwd(gy.data_ptr(), c, h, w, s, ho, wo, dx.data_ptr(), hip.stream_ptr()),
                   "msl_subsample_bwd")
         return dx, None
@@ -742,6 +765,17 @@ def upsample_bilinear(x, size):
     y = _Upsample.apply(x, int(size[0]), int(size[1]))
     y._msl_low = (x, y._version, x._version)
     return y
+
+
+# --------------------------------------------------------------------------- image pairs
+def pair_join(x_s, x_t):
+    """(1,C,H,W) x 2 -> the pair (1,C,2,H,W) ([C][2][H][W]) the trunk ops run as one batch."""
+    return torch.stack([x_s, x_t], dim=2)
+
+
+def pair_split(y):
+    """(1,C,N,H,W) -> N contiguous (1,C,H,W) images (autograd stacks their gradients back)."""
+    return tuple(t.contiguous() for t in y.unbind(2))
 
 
 # --------------------------------------------------------------------------- fused losses
@@ -1005,17 +1039,18 @@ class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, training, momentum,
                 eps, relu, hold=None):
-        x = _check_act(x, "bn_act")
-        c, p = x.size(1), x.size(2) * x.size(3)
+        x = _check_act(x, "bn_act", images=True)
+        n = _nimg(x)
+        c, p = x.size(1), x.size(-2) * x.size(-1)  # p: pixels of one image
         if residual is not None:
             residual = residual.contiguous()
             if residual.shape != x.shape:
                 raise hip.MSLError("bn_act: residual shape mismatch")
         lib = hip.load()
         y = torch.empty_like(x)
-        save_mean = torch.empty(c, dtype=_f32, device=x.device)
-        save_invstd = torch.empty(c, dtype=_f32, device=x.device)
-        wsb = lib.msl_bn_workspace(c, p)
+        save_mean = torch.empty(c * n, dtype=_f32, device=x.device)
+        save_invstd = torch.empty(c * n, dtype=_f32, device=x.device)
+        wsb = lib.msl_bn_workspace(c, p, n)
         ws = hip.workspace(wsb, x.device)
         update = bool(training) and running_mean is not None
         # f16x3: the per-channel absmax of y for the convs that read it (their operand scales), where
@@ -1025,21 +1060,21 @@ class _BNAct(Function):
             _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(bool(training)))) else None
         hip.check(lib.msl_bn_fwd_am(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
                                     hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
-                                    save_mean.data_ptr(), save_invstd.data_ptr(), c, p, int(bool(training)),
+                                    save_mean.data_ptr(), save_invstd.data_ptr(), c, p, n, int(bool(training)),
                                     int(update), float(momentum), float(eps), int(bool(relu)), ws.data_ptr(), wsb,
                                     hip.stream_ptr(), hip.ptr(am)), "msl_bn_fwd")
         if am is not None:
             _tag_absmax(y, am)
         ctx.save_for_backward(x, weight, y if relu else None, save_mean, save_invstd)
         ctx.bias = bias
-        ctx.meta = (c, p, bool(training), bool(relu))
+        ctx.meta = (c, p, n, bool(training), bool(relu))
         ctx.hold = hold
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, weight, y, save_mean, save_invstd = ctx.saved_tensors
-        c, p, training, relu = ctx.meta
+        c, p, n, training, relu = ctx.meta
         gy = gy.contiguous()
         lib = hip.load()
         nig = ctx.needs_input_grad
@@ -1054,14 +1089,14 @@ class _BNAct(Function):
         else:
             dgamma = torch.empty(c, dtype=_f32, device=x.device) if nig[1] else None
             dbeta = torch.empty(c, dtype=_f32, device=x.device) if nig[2] else None
-        wsb = lib.msl_bn_workspace(c, p)
+        wsb = lib.msl_bn_workspace(c, p, n)
         ws = hip.workspace(wsb, x.device)
         # f16x3: the per-channel absmax of dx, the gradient the conv before this BN reads twice
         am = torch.empty(c, dtype=_f32, device=x.device) if (
             dx is not None and _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(training))) else None
         hip.check(lib.msl_bn_bwd_am(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight), save_mean.data_ptr(),
                                     save_invstd.data_ptr(), hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma),
-                                    hip.ptr(dbeta), c, p, int(training), int(relu), int(direct), ws.data_ptr(), wsb,
+                                    hip.ptr(dbeta), c, p, n, int(training), int(relu), int(direct), ws.data_ptr(), wsb,
                                     hip.stream_ptr(), hip.ptr(am)), "msl_bn_bwd")
         if am is not None:
             _tag_absmax(dx, am)

@@ -9,6 +9,11 @@ One iteration (solve_gta5.py:335-387), with the same method names:
 Gradients of the two backward passes accumulate; with WORLD_SIZE > 1 the
 bucketed RCCL all-reduce is armed for the target backward and overlaps it.
 
+With --pair (default) the two forwards run as one image pair (model.forward_pair:
+every conv GEMM once over both images, each image with its own bs=1 BatchNorm
+statistics) and the two losses share one backward pass; the gradients are the
+same sums, added inside the weight-gradient GEMMs instead of by a second pass.
+
 The losses run fused from the low-resolution logits (utils/loss.py), so the
 two softmax tensors of the reference (:182-183) are never materialised.
 Style-transfer augmentation (exp_tag source_aug/target_aug) and the
@@ -53,6 +58,7 @@ class UDATrainer(Trainer):
         self.use_graph = bool(getattr(self.args, "graph", False))
         self._graphed = None
         self.overlap = bool(getattr(self.args, "overlap", True))
+        self.pair = bool(getattr(self.args, "pair", True))
         self._side = None
 
     def _reset_meters(self):
@@ -66,8 +72,8 @@ class UDATrainer(Trainer):
         self.loss_target_value, self.loss_target_value_2 = z(), z()
 
     # ---------------------------------------------------------------- the two halves
-    def train_source(self, pred, y):
-        """solve_gta5.py:220-235."""
+    def source_loss(self, pred, y):
+        """The source objective of solve_gta5.py:220-235 (meters updated), without its backward."""
         if isinstance(pred, tuple):
             pred_2 = pred[1]
             pred = pred[0]
@@ -78,11 +84,12 @@ class UDATrainer(Trainer):
             loss_2 = self.args.lambda_seg * self.loss(pred_2, y)
             loss_ = loss_ + loss_2
             self.loss_seg_value_2 += loss_2.detach() / self.iter_num
-        loss_.backward()
         self.loss_seg_value += self.loss_val.detach() / self.iter_num
+        return loss_
 
-    def train_target(self, pred):
-        """solve_gta5.py:178-218 (maxsquare / IW_maxsquare target modes)."""
+    def target_loss_total(self, pred):
+        """The target objective of solve_gta5.py:178-218 (maxsquare / IW_maxsquare target modes; meters
+        updated), without its backward."""
         pred_2 = None
         if isinstance(pred, tuple):
             pred_2 = pred[1]
@@ -94,10 +101,19 @@ class UDATrainer(Trainer):
                                   multi_level_guidance_ce(pred, pred_2, self.threshold))
             loss_target_ = loss_target_ + self.loss_target_2
             self.loss_target_value_2 += self.loss_target_2.detach() / self.iter_num
+        self.loss_target_value += self.loss_target.detach() / self.iter_num
+        return loss_target_
+
+    def train_source(self, pred, y):
+        """solve_gta5.py:220-235."""
+        self.source_loss(pred, y).backward()
+
+    def train_target(self, pred):
+        """solve_gta5.py:178-218 (maxsquare / IW_maxsquare target modes)."""
+        loss_target_ = self.target_loss_total(pred)
         if self.reducer:
             self.reducer.prepare_for_backward()
         loss_target_.backward()
-        self.loss_target_value += self.loss_target.detach() / self.iter_num
 
     def uda_step(self, x_s, y_s, x_t):
         """One iteration of the hot loop (solve_gta5.py:336-383), inputs already on the device.
@@ -118,6 +134,16 @@ class UDATrainer(Trainer):
         self.current_iter += 1
 
     def _uda_grads(self, x_s, y_s, x_t):
+        if self.pair and x_s.shape == x_t.shape:
+            # one image pair through the network, one backward pass for both objectives
+            pred_s, pred_t = self.model.forward_pair(x_s, x_t)
+            loss_s = self.source_loss(pred_s, y_s)
+            loss_t = self.target_loss_total(pred_t)
+            if self.reducer:
+                self.reducer.prepare_for_backward()
+            torch.autograd.backward([loss_s, loss_t])
+            ops.wgrad_join(self.device)
+            return
         if not self.overlap:
             pred = self.model(x_s)
             self.train_source(pred, y_s)
@@ -219,9 +245,12 @@ def add_UDA_train_args(arg_parser):
     a("--IW_ratio", type=float, default=0.2)
     a("--threshold", type=float, default=0.95)
     a("--target_solo_epoch", type=int, default=0)
+    a("--pair", type=str2bool, default=True,
+      help="run the source and target images of an iteration as one image pair (per-image BatchNorm "
+           "statistics, one backward pass; not in the reference, which runs two forward/backward passes)")
     a("--overlap", type=str2bool, default=True,
-      help="run the target forward on a side stream concurrently with the source backward (same "
-           "results; not in the reference, whose loop is sequential)")
+      help="with --pair False: run the target forward on a side stream concurrently with the source "
+           "backward (same results; not in the reference, whose loop is sequential)")
     a("--graph", type=str2bool, default=False,
       help="replay each iteration after the first as one captured hipGraph (single process; not in the "
            "reference, whose loop is eager)")

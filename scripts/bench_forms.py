@@ -43,9 +43,9 @@ def case(name, cin, cout, h, w, d, forms):
         dw = torch.empty_like(wt)
         cnt = hip.counters(x.device).data_ptr()
         if d:
-            wf = lib.msl_dconv_fwd_workspace(1, cin, cout, h, w)
-            wd = lib.msl_dconv_dgrad_workspace(1, cin, cout, h, w)
-            ww = lib.msl_dconv_wgrad_workspace(1, cin, cout, h, w)
+            wf = lib.msl_dconv_fwd_workspace(1, cin, cout, h, w, 1)
+            wd = lib.msl_dconv_dgrad_workspace(1, cin, cout, h, w, 1)
+            ww = lib.msl_dconv_wgrad_workspace(1, cin, cout, h, w, 1)
         else:
             wf = lib.msl_pconv_fwd_workspace(cin, cout, p)
             wd = lib.msl_pconv_dgrad_workspace(cin, cout, p)
@@ -54,12 +54,12 @@ def case(name, cin, cout, h, w, d, forms):
         wsd = torch.empty(wd, dtype=torch.uint8, device="cuda")
         wsw = torch.empty(ww, dtype=torch.uint8, device="cuda")
         if d:
-            fwd = lambda: hip.check(lib.msl_dconv_fwd(x.data_ptr(), pk.data_ptr(), None, y.data_ptr(), 1, cin, cout, h, w,
+            fwd = lambda: hip.check(lib.msl_dconv_fwd(x.data_ptr(), pk.data_ptr(), None, y.data_ptr(), 1, cin, cout, h, w, 1,
                                                       d, 0, cnt, wsf.data_ptr(), wf, st), "fwd")
-            dgr = lambda: hip.check(lib.msl_dconv_dgrad(gy.data_ptr(), pd.data_ptr(), dx.data_ptr(), 1, cin, cout, h, w,
+            dgr = lambda: hip.check(lib.msl_dconv_dgrad(gy.data_ptr(), pd.data_ptr(), dx.data_ptr(), 1, cin, cout, h, w, 1,
                                                         d, 0, cnt, wsd.data_ptr(), wd, st), "dgrad")
             wgr = lambda: hip.check(lib.msl_dconv_wgrad(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), None, 1, cin, cout,
-                                                        h, w, d, 0, 0, wsw.data_ptr(), ww, st), "wgrad")
+                                                        h, w, 1, d, 0, 0, wsw.data_ptr(), ww, st), "wgrad")
         else:
             fwd = lambda: hip.check(lib.msl_pconv_fwd(x.data_ptr(), pk.data_ptr(), y.data_ptr(), cin, cout, p, cnt,
                                                       wsf.data_ptr(), wf, st), "fwd")

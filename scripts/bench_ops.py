@@ -36,21 +36,21 @@ def timed(fn, reps):
     return e0.elapsed_time(e1) / reps * 1e3  # us
 
 
-def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W):
+def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W, nimg=1):
     """(label, fwd, dgrad, wgrad callables, flops, reference checker) for one conv shape."""
     g = torch.Generator().manual_seed(cin + cout)
-    x = torch.relu(torch.randn(1, cin, h, w, generator=g)).to(DEV)
+    x = torch.relu(torch.randn(1, cin, nimg, h, w, generator=g)).to(DEV)  # [C][nimg][h][w]
     wt = (torch.randn(cout, cin, k, k, generator=g) * 0.02).to(DEV)
-    gy = torch.randn(1, cout, h, w, generator=g).to(DEV)
+    gy = torch.randn(1, cout, nimg, h, w, generator=g).to(DEV)
     lib = hip.load()
     s = hip.stream_ptr()
-    p = h * w
+    p = h * w * nimg
     cnt = hip.counters(x.device).data_ptr()
     cache = ops.PackCache(pointwise=(k == 1))
     xpart = ops._parts(x)
     gpart = ops._parts(gy)
-    y = torch.empty(1, cout, h, w, device=DEV)
-    dx = torch.empty(1, cin, h, w, device=DEV)
+    y = torch.empty(1, cout, nimg, h, w, device=DEV)
+    dx = torch.empty(1, cin, nimg, h, w, device=DEV)
     dw = torch.empty_like(wt)
     if k == 1:
         pf, pd = cache.get([wt], cin, cout, 0), cache.get([wt], cin, cout, 1)
@@ -67,32 +67,36 @@ def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W):
         ref = lambda xx, ww: F.conv2d(xx, ww)  # noqa: E731
     else:
         pf, pd = cache.get([wt], cin, cout, 0), cache.get([wt], cin, cout, 1)
-        wsf = hip.workspace(lib.msl_dconv_fwd_workspace(1, cin, cout, h, w), DEV)
-        wsd = hip.workspace(lib.msl_dconv_dgrad_workspace(1, cin, cout, h, w), DEV)
-        wsw = hip.workspace(lib.msl_dconv_wgrad_workspace(1, cin, cout, h, w), DEV)
+        wsf = hip.workspace(lib.msl_dconv_fwd_workspace(1, cin, cout, h, w, nimg), DEV)
+        wsd = hip.workspace(lib.msl_dconv_dgrad_workspace(1, cin, cout, h, w, nimg), DEV)
+        wsw = hip.workspace(lib.msl_dconv_wgrad_workspace(1, cin, cout, h, w, nimg), DEV)
         fwd = lambda: hip.check(lib.msl_dconv_fwd_sc(x.data_ptr(), pf.data_ptr(), None, y.data_ptr(), 1, cin, cout,  # noqa: E731
-                                                     h, w, d, 0, cnt, wsf.data_ptr(), wsf.numel(), s,
+                                                     h, w, nimg, d, 0, cnt, wsf.data_ptr(), wsf.numel(), s,
                                                      *ops._pp(xpart)), "fwd")
         dgr = lambda: hip.check(lib.msl_dconv_dgrad_sc(gy.data_ptr(), pd.data_ptr(), dx.data_ptr(), 1, cin, cout, h,  # noqa: E731
-                                                       w, d, 0, cnt, wsd.data_ptr(), wsd.numel(), s,
+                                                       w, nimg, d, 0, cnt, wsd.data_ptr(), wsd.numel(), s,
                                                        *ops._pp(gpart)), "dgrad")
         wgr = lambda: hip.check(lib.msl_dconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), None, 1, cin,  # noqa: E731
-                                                       cout, h, w, d, 0, 0, wsw.data_ptr(), wsw.numel(), s,
+                                                       cout, h, w, nimg, d, 0, 0, wsw.data_ptr(), wsw.numel(), s,
                                                        *ops._pp(xpart), *ops._pp(gpart)), "wgrad")
         ref = lambda xx, ww: F.conv2d(xx, ww, padding=d, dilation=d)  # noqa: E731
-    flops = 2.0 * cin * cout * k * k * p
+    flops = 2.0 * cin * cout * k * k * p  # p counts every image
+
+    def nchw(t):  # [1][C][nimg][h][w] -> the images as an NCHW batch, fp64 on the host
+        return t.double().cpu()[0].transpose(0, 1).contiguous()
 
     def check():
-        xr, wr = x.double().cpu().requires_grad_(), wt.double().cpu().requires_grad_()
+        xr, wr = nchw(x).requires_grad_(), wt.double().cpu().requires_grad_()
         yr = ref(xr, wr)
-        yr.backward(gy.double().cpu())
-        xa, wa = x.double().cpu().abs().requires_grad_(), wt.double().cpu().abs().requires_grad_()
+        yr.backward(nchw(gy))
+        xa, wa = nchw(x).abs().requires_grad_(), wt.double().cpu().abs().requires_grad_()
         ya = ref(xa, wa)
-        ya.backward(gy.double().cpu().abs())
+        ya.backward(nchw(gy).abs())
         fwd(); dgr(); wgr()  # noqa: E702
         torch.cuda.synchronize()
-        e = lambda o, r, b: ((o.double().cpu() - r).abs() / b.clamp_min(1e-300)).max().item()  # noqa: E731
-        return e(y, yr.detach(), ya.detach()), e(dx, xr.grad, xa.grad), e(dw, wr.grad, wa.grad)
+        e = lambda o, r, b: ((o - r).abs() / b.clamp_min(1e-300)).max().item()  # noqa: E731
+        return (e(nchw(y), yr.detach(), ya.detach()), e(nchw(dx), xr.grad, xa.grad),
+                e(dw.double().cpu(), wr.grad, wa.grad))
     return name, fwd, dgr, wgr, flops, check
 
 
@@ -107,15 +111,17 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--only", default=None, help="substring of the shape names to run")
+    ap.add_argument("--hw", type=int, nargs=2, default=[H, W], help="map size (default the step's 65 x 129)")
+    ap.add_argument("--nimg", type=int, default=1, help="images per call ([C][nimg][h][w]; 2 = the trainer's pair)")
     a = ap.parse_args()
     lib = hip.load()
-    ops_list = [conv_ops(*s) for s in SHAPES if a.only is None or a.only in s[0]]
+    ops_list = [conv_ops(*s, h=a.hw[0], w=a.hw[1], nimg=a.nimg) for s in SHAPES if a.only is None or a.only in s[0]]
     for v in a.variant:
         if hasattr(lib, "msl_conv_set_variant"):
             hip.check(lib.msl_conv_set_variant(v), "msl_conv_set_variant")
         for name, fwd, dgr, wgr, flops, check in ops_list:
             t = [timed(f, a.reps) for f in (fwd, dgr, wgr)]
-            rec = {"variant": v, "op": name, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
+            rec = {"variant": v, "hw": a.hw, "nimg": a.nimg, "op": name, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
                    "wgrad_us": round(t[2], 1), "fwd_tf": round(flops / t[0] / 1e6, 1),
                    "wgrad_tf": round(flops / t[2] / 1e6, 1)}
             if a.check:

@@ -808,7 +808,7 @@ def test_bn_absmax_outputs(c, h, w, res, relu, fused):
         gamma = (torch.rand(c, generator=g) + 0.5).to(DEV)
         beta = torch.randn(c, generator=g).to(DEV)
         gy = torch.randn(c, p, generator=g).to(DEV)
-        wsb = lib.msl_bn_workspace(c, p)
+        wsb = lib.msl_bn_workspace(c, p, 1)
         ws = hip.workspace(wsb, x.device)
         s = hip.stream_ptr()
         outs = []
@@ -819,10 +819,10 @@ def test_bn_absmax_outputs(c, h, w, res, relu, fused):
             dg, db = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
             fa, ba = torch.full((c,), -1.0, device=DEV), torch.full((c,), -1.0, device=DEV)
             fargs = (x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), hip.ptr(r), y.data_ptr(), rm.data_ptr(),
-                     rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, 1, 1, 0.1, 1e-5, int(relu), ws.data_ptr(),
+                     rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, 1, 1, 1, 0.1, 1e-5, int(relu), ws.data_ptr(),
                      wsb, s)
             bargs = (gy.data_ptr(), x.data_ptr(), y.data_ptr(), gamma.data_ptr(), sm.data_ptr(), si.data_ptr(),
-                     dx.data_ptr(), dres.data_ptr(), dg.data_ptr(), db.data_ptr(), c, p, 1, int(relu), 0, ws.data_ptr(),
+                     dx.data_ptr(), dres.data_ptr(), dg.data_ptr(), db.data_ptr(), c, p, 1, 1, int(relu), 0, ws.data_ptr(),
                      wsb, s)
             if am:
                 assert lib.msl_bn_fwd_am(*fargs, fa.data_ptr()) == 0

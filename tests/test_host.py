@@ -53,7 +53,7 @@ def test_pure_host_entry_points():
     assert lib.msl_dconv_packed_elems(1, 256, 256, 0) == 16 * 9 * 16 * 256 * 5 // 2 + 320
     assert lib.msl_dconv_packed_elems(2, 2048, 19, 0) == 2 * 128 * 9 * 16 * 128 * 5 // 2 + 320
     assert lib.msl_dconv_packed_elems(2, 2048, 19, 1) == 2 * 2 * 9 * 16 * 2048 * 5 // 2 + 320
-    assert lib.msl_dconv_fwd_workspace(1, 256, 256, 65, 129) > 0  # split-K slabs at this size
+    assert lib.msl_dconv_fwd_workspace(1, 256, 256, 65, 129, 1) > 0  # split-K slabs at this size
     assert lib.msl_loss_stats_elems() == 64
     be = lib.msl_sgd_block_elems()
     numels = np.array([10, be, be + 1, 0], dtype=np.int64)
