@@ -373,9 +373,18 @@ __global__ void __launch_bounds__(256) k_absmax_rows(const float* __restrict__ t
               __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
+__global__ void __launch_bounds__(256) k_zero_rows(float* __restrict__ v, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = 0.f;
+}
+
+// The maxima are zeroed by a kernel, not hipMemsetAsync: inside a captured hipGraph (utils/graph.py)
+// the memset node was not ordered against the atomicMax kernel that follows it - replays left stale
+// or garbage maxima (up to 1e38) in the partials, i.e. wrong f16x3 operand scales (r03 pair-mode
+// graph test; scripts/diag_graph_pair.py).  Kernel nodes keep the stream order.
 int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
-  const hipError_t e = hipMemsetAsync(absmax, 0, (size_t)c * sizeof(float), st);
-  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_zero_rows, dim3(cdiv(c, 256)), dim3(256), 0, st, absmax, c);
+  MSL_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_absmax_rows, dim3(c, cdiv(p, kAbsChunk)), dim3(256), 0, st, t, p, absmax);
   MSL_CHECK_LAUNCH();
   return MSL_OK;

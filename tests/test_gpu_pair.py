@@ -12,8 +12,11 @@ bs=1 statistics.  Held here:
     outputs, saved statistics, running statistics (source then target), num_batches_tracked,
     input / residual gradients, and dgamma / dbeta (= the second call accumulating into the first);
   - maxpool, subsample: bit-identical per image;
-  - the model: forward_pair = forward per image (1e-5), and one UDA iteration with --pair against
-    the two-pass iteration (losses 1e-4, BN running statistics 1e-4).
+  - the model: forward_pair = forward per image (eval 1e-5; train 1e-3, the bar the single-image
+    forward is held to against the oracle: the pair's GEMMs split the doubled pixel axis at other stream-K
+    points, i.e. another fp32 summation order, which train-mode bs=1 BatchNorm over 104 layers amplifies -
+    3.7e-4 measured), and one UDA iteration with --pair against the two-pass iteration (losses 1e-4, BN
+    running statistics 1e-4).
 """
 import copy
 
@@ -234,11 +237,12 @@ def test_forward_pair_matches_forward(train):
         outs = m.forward_pair(xs, xt)
         single = [m1(xs), m1(xt)]
     torch.cuda.synchronize()
+    bar = 1e-3 if train else 1e-5
     for (p2, p1), (s2, s1) in zip(outs, single):
-        assert _rel(p2, s2) < 1e-5 and _rel(p1, s1) < 1e-5
+        assert _rel(p2, s2) < bar and _rel(p1, s1) < bar
     for (n, a), b in zip(m.named_buffers(), m1.buffers()):
         if "running" in n:
-            assert _rel(a, b) < 1e-5, n
+            assert _rel(a, b) < bar, n
 
 
 @pytest.mark.parametrize("mode,multi", [("maxsquare", False), ("IW_maxsquare", True)])
