@@ -176,8 +176,10 @@ def main():
     # and FP16 MFMA (same rate) at three products per fp32 product (the f16x3 form): 833.3
     peak = {"mfma_f32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "fp16": BF16_MFMA_PEAK_TFLOPS,
             "bf16x6": round(BF16_MFMA_PEAK_TFLOPS / 6, 1), "f16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1)}[form]
-    if traffic is not None and json.load(open(a.pmc)).get("form", "mfma_f32") != form:
-        traffic = None  # the committed PMC figure belongs to another form of the kernel
+    if traffic is not None:
+        rec = json.load(open(a.pmc))
+        if rec.get("form", "mfma_f32") != form or rec.get("nimg", 1) != nimg:
+            traffic = None  # the committed PMC figure belongs to another form or image count of the kernel
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_source": (os.path.relpath(a.pmc, ROOT) + ": committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "

@@ -26,7 +26,8 @@ fs = [per_launch(fetch_csv, "FETCH_SIZE", n) for n in names]
 ws = [per_launch(write_csv, "WRITE_SIZE", n) for n in names]
 f, nf = sum(v for v, _ in fs), [n for _, n in fs]
 w, nw = sum(v for v, _ in ws), [n for _, n in ws]
-res = {"kernel": kernels, "form": form, "launches": [nf, nw], "fetch_size_kib": f, "write_size_kib": w,
+import os  # noqa: E402
+res = {"kernel": kernels, "form": form, "nimg": int(os.environ.get("NIMG", "2")), "launches": [nf, nw], "fetch_size_kib": f, "write_size_kib": w,
        "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024),
        "note": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), gfx950 FETCH_SIZE correction; "
                "per-launch figures of the listed kernels summed"}

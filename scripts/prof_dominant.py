@@ -2,7 +2,10 @@
 1024x512 feature size (65x129), launched through the same op as the training step.  Profiled
 with rocprofv3 (--kernel-trace --stats, then separate --pmc passes) by scripts/gpu_counters.sh.
 
-    prof_dominant.py [N] [H W MATH]     e.g. 20 96 161 fp16 (BASELINE configs[4]: 1280x760, fp16 MFMA)"""
+    prof_dominant.py [N] [H W MATH]     e.g. 20 96 161 fp16 (BASELINE configs[4]: 1280x760, fp16 MFMA)
+
+NIMG (env, default 2): images per call - the trainer runs the source and target images as one pair
+([C][2][H][W]), so the bench's dominant op covers two images."""
 import os
 import sys
 
@@ -16,7 +19,8 @@ H, W = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (65, 129)
 if len(sys.argv) > 4:
     ops.set_conv_math(sys.argv[4])
 g = torch.Generator(device="cuda").manual_seed(0)
-x = torch.randn(1, 256, H, W, device="cuda", generator=g)
+nimg = int(os.environ.get("NIMG", "2"))
+x = torch.randn((1, 256, nimg, H, W) if nimg > 1 else (1, 256, H, W), device="cuda", generator=g)
 w = torch.randn(256, 256, 3, 3, device="cuda", generator=g) * 0.02
 cache = ops.PackCache()
 # f16x3: in the step the input's absmax partials come from the BN kernel that produced it, so the
