@@ -122,13 +122,20 @@ __device__ __forceinline__ void bn_row_stats(const BnArgs& a, int r, float& mean
   invstd = (float)(1.0 / sqrt(var + (double)a.eps));
 }
 
+// (1 - m) * old + m * v with every operation rounded on its own: whether the compiler contracts
+// this into an fma depended on the kernel around it, so the pair, per-image and split forms rounded
+// the running variance differently (r03: the pair form's running_var was 1 ulp off the per-image loop)
+__device__ __forceinline__ float running_blend(float old, float m, float v) {
+  return __fadd_rn(__fmul_rn(__fsub_rn(1.f, m), old), __fmul_rn(m, v));
+}
+
 // running statistics of channel c <- image n's batch statistics (one image after the other)
 __device__ __forceinline__ void bn_running_update(const BnArgs& a, int c, float mean, double var) {
   const double n = (double)a.P;
   const float m = a.momentum;
   const float unbiased = (float)(a.P > 1 ? var * n / (n - 1.0) : var);
-  a.running_mean[c] = (1.f - m) * a.running_mean[c] + m * mean;
-  a.running_var[c] = (1.f - m) * a.running_var[c] + m * unbiased;
+  a.running_mean[c] = running_blend(a.running_mean[c], m, mean);
+  a.running_var[c] = running_blend(a.running_var[c], m, unbiased);
 }
 
 // Flat apply: block b covers elements [b*chunk, (b+1)*chunk) of the [C*NI][P] tensor (possibly
@@ -443,14 +450,14 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
   for (int j = 0; j < EPT; ++j) {
     if (j * kBnFusedThreads + t < P) {
       const double d = (double)xv[j] - shift;
-      s1 += d;
-      s2 += d * d;
+      s1 = __dadd_rn(s1, d);  // explicit roundings: the single-image and pair forms agree bit for bit
+      s2 = __fma_rn(d, d, s2);
     }
   }
   block_sum2_d16(s1, s2, red);
   const double n = (double)P;
   const double dm = s1 / n;
-  double var = s2 / n - dm * dm;
+  double var = __fma_rn(-dm, dm, __ddiv_rn(s2, n));
   if (var < 0.0) var = 0.0;
   const float mean = (float)(shift + dm);
   const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
@@ -458,21 +465,21 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
     if (a.update_running) {
       const float m = a.momentum;
       const float unbiased = (float)(P > 1 ? var * n / (n - 1.0) : var);
-      a.running_mean[c] = (1.f - m) * a.running_mean[c] + m * mean;
-      a.running_var[c] = (1.f - m) * a.running_var[c] + m * unbiased;
+      a.running_mean[c] = running_blend(a.running_mean[c], m, mean);
+      a.running_var[c] = running_blend(a.running_var[c], m, unbiased);
       if (c == 0 && a.num_batches) a.num_batches[0] += 1;
     }
     a.save_mean[r] = mean;
     a.save_invstd[r] = invstd;
   }
   const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
-  const float bsh = (a.beta ? a.beta[c] : 0.f) - mean * alpha;
+  const float bsh = __fmaf_rn(-mean, alpha, a.beta ? a.beta[c] : 0.f);
   float* yc = a.y + base;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
     if (e < P) {
-      float v = xv[j] * alpha + bsh;
+      float v = __fmaf_rn(xv[j], alpha, bsh);
       v += rv[j];
       v = a.relu ? fmaxf(v, 0.f) : v;
       yc[e] = v;
@@ -516,8 +523,8 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const float xh = (xv[j] - mean) * invstd;
-    sg += (double)g[j];  // g = 0 past P
-    sgx += (double)g[j] * (double)xh;
+    sg = __dadd_rn(sg, (double)g[j]);  // g = 0 past P
+    sgx = __fma_rn((double)g[j], (double)xh, sgx);
   }
   block_sum2_d16(sg, sgx, red);
   if (t == 0) {
@@ -537,7 +544,7 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
     if (e < P) {
       const float xh = (xv[j] - mean) * invstd;
       if (a.dres) a.dres[base + e] = g[j];
-      const float d = (g[j] - m1 - xh * m2) * w;
+      const float d = __fmul_rn(__fmaf_rn(-xh, m2, __fsub_rn(g[j], m1)), w);
       if (a.dx) a.dx[base + e] = d;
       am = fmaxf(am, fabsf(d));
     }
@@ -553,6 +560,7 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
     if (t == 0) a.absmax[c] = am;
   }
 }
+
 
 template <typename K, typename A>
 static int bn_launch_fused(K k4, K k9, K k16, K k33, int c, int p, hipStream_t st, const A& a) {

@@ -407,18 +407,7 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
                       bool bp = false) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
     if constexpr ((BM == 128 || (BM == 64 && MT == kMathH3P)) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
-      // the image operand's register loads opaque to the compiler's waitcnt pass (OPQ; variant bit 8)
-      const bool opq = (g_variant & 256) != 0;
       if (bp) {  // the image operand pre-split by k_split_img (variant bit 7)
-        if (opq) {
-          if (accum)
-            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true, true>), grid, block,
-                               0, st, a, sk);
-          else
-            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true, true, true>), grid,
-                               block, 0, st, a, sk);
-          return;
-        }
         if (accum)
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0, st,
                              a, sk);
@@ -432,15 +421,6 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
       // 256 -> 1024 fwd 32.7 vs 31.0 us, 2048 -> 512 82.7 vs 75.1; layer3 3x3 fwd 52.4 vs 55.0,
       // layer4 172 vs 190; profiles/r03_fwd_forms_ab.txt)
       if (!PW && !(g_variant & 4)) {
-        if (opq) {
-          if (accum)
-            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, false, true>), grid, block,
-                               0, st, a, sk);
-          else
-            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true, false, true>), grid,
-                               block, 0, st, a, sk);
-          return;
-        }
         if (accum)
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a, sk);
         else

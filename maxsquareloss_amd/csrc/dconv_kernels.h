@@ -808,42 +808,6 @@ __global__ void __launch_bounds__(256) k_igemm_wgrad(WgradArgs a) {
 // is padding) gets an out-of-range offset, which loads 0.
 typedef __attribute__((address_space(3))) void lds_void;
 
-// Register loads the compiler does not track (r03).  A load through the builtin writes a VGPR the
-// compiler's waitcnt pass follows; across the K-step loops' back edges (and the conditional issues
-// of their last steps) that pass merges its per-register state conservatively and emits
-// s_waitcnt vmcnt(0..7) before the values are used - draining every younger prefetch (the BD forward
-// form waited for all in-flight loads in 2 of its 4 unrolled K-steps).  These asm loads are invisible
-// to it: the kernel's own counted wait_vmcnt<N>() orders them, and pin_regs() (an empty asm that reads
-// and rewrites the registers after that wait) keeps every use of the values behind the wait.
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4 raw_rsrc(const void* base, long long bytes) {
-  const unsigned long long a = (unsigned long long)base;
-  i32x4 d;
-  d.x = (int)(unsigned)a;
-  d.y = (int)(unsigned)((a >> 32) & 0xffffu);  // stride 0
-  d.z = (int)min(0x7fffffffLL, bytes);        // num_records (bytes, raw buffer)
-  d.w = 0x00020000;                            // as __builtin_amdgcn_make_buffer_rsrc(.., 0x00020000)
-  d.x = __builtin_amdgcn_readfirstlane(d.x);
-  d.y = __builtin_amdgcn_readfirstlane(d.y);
-  d.z = __builtin_amdgcn_readfirstlane(d.z);
-  return d;
-}
-__device__ __forceinline__ float opaque_load_b32(i32x4 r, unsigned voff) {
-  float v;
-  asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(r));
-  return v;
-}
-__device__ __forceinline__ u32x4 opaque_load_b128(i32x4 r, unsigned voff) {
-  u32x4 v;
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(r));
-  return v;
-}
-template <int N>
-__device__ __forceinline__ void pin_regs(float (&v)[N]) {
-#pragma unroll
-  for (int j = 0; j < N; ++j) asm volatile("" : "+v"(v[j]));
-}
-
 __device__ __forceinline__ void dma_b32(__amdgpu_buffer_rsrc_t r, float* lds_row, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_row, 4, voff, 0, 0, 0);
 }
@@ -1066,7 +1030,7 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
 // each, more than the K-step's 12 MFMAs).  Every wave of the 1 x 4 layout reads its own 32 columns,
 // so nothing is lost by not sharing B through LDS.
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false, bool BP = false, bool OPQ = false>
+          bool BD = false, bool BP = false>
 __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -1141,13 +1105,6 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       (int)min(0x7fffffffLL, (long long)a.ncb * (BP ? (H1 ? 2 : 4) : 6) * a.P * 16), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
   const unsigned chan_bytes = (unsigned)a.P * 4u;
-  // OPQ (BD / BP forms): the image operand's register loads through opaque_load_* (see raw_rsrc)
-  i32x4 rbq = {0, 0, 0, 0};
-  if constexpr (OPQ) {
-    rbq = BP ? raw_rsrc(a.Bx6, (long long)a.ncb * (H1 ? 2 : 4) * a.P * 16)
-             : raw_rsrc(a.B, (long long)a.cimg * a.P * 4);
-  }
-  static_assert(!OPQ || BD, "OPQ: the BD / BP forms");
   // f16x3: B's scale from its absmax partials, A's from the pack; the result is unscaled by both
   float sB = 1.f, iA = 1.f, iB = 1.f;
   if constexpr (H3) {
@@ -1286,10 +1243,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
           for (int q = 0; q < NPB; ++q) {
             const unsigned row = (unsigned)((c_cb * NPB + q) * 2 + (lane >> 5)) * pl_bytes;
             union { u32x4 u; float f[4]; } c;
-            if constexpr (OPQ)
-              c.u = opaque_load_b128(rbq, vbd + row);
-            else
-              c.u = __builtin_amdgcn_raw_buffer_load_b128(rbx, vbd + row, 0, 0);
+            c.u = __builtin_amdgcn_raw_buffer_load_b128(rbx, vbd + row, 0, 0);
 #pragma unroll
             for (int j = 0; j < 4; ++j) bq[4 * q + j] = c.f[j];
           }
@@ -1300,10 +1254,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const unsigned off = ci0 + j < a.cimg ? vbd + (unsigned)(ci0 + j) * chan_bytes : OOB;
-            if constexpr (OPQ)
-              bq[j] = opaque_load_b32(rbq, off);
-            else
-              bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0));
+            bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0));
           }
         } else if constexpr (BPRE) {
           // piece (plane*2 + k half, 64-pixel half): lane = pixel, 16 B = 8 channels of a plane
@@ -1374,7 +1325,6 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         else if (younger == 1) wait_vmcnt<INST_W>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
-        if constexpr (OPQ) pin_regs(cur);  // K-step i's image values landed (the wait above): uses stay behind it
         const float* As = smem + (i % STAGES) * STAGE;
         const bool more = i + STAGES - 1 < nst;
         auto mid = [&] {
@@ -1531,9 +1481,9 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 // The same kernel held to two waves per SIMD (<= 256 VGPRs + AGPRs): the f16x3 form, left to the
 // compiler's default budget, takes 199 VGPRs + 64 AGPRs and one wave per SIMD.
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false, bool BP = false, bool OPQ = false>
+          bool BD = false, bool BP = false>
 __global__ void __launch_bounds__(256, 2) k_igemm_fwd_sk2(FwdArgs a, SkArgs sk) {
-  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD, BP, OPQ>(a, sk);
+  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD, BP>(a, sk);
 }
 
 // sum of pieces w_lo..w_hi in that order (deterministic), eight loads in flight per step: a tile
