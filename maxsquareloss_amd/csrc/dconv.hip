@@ -139,13 +139,8 @@ __device__ __forceinline__ void pack_split_block(const float* __restrict__ w, lo
     out[k * lda + m0 + ml] = s[cl * TAPS + t][ml];
   }
   if (!split) return;
-  if (tail) {  // f16x3: two fp16 planes of W * sA, sA from the weights' absmax partials (tail[0..])
-    float inv;
-    const float sc = pow2_scale(partials_max(tail, kNPart, threadIdx.x & 63), inv);
-    if (mx == 0 && cb == 0 && b == 0 && threadIdx.x == 0) {
-      tail[kNPart] = sc;
-      tail[kNPart + 1] = inv;
-    }
+  if (tail) {  // f16x3: two fp16 planes of W * sA; {sA, 1/sA} written by k_pack_scale* before this launch
+    const float sc = tail[kNPart];
     f16x8* pl = reinterpret_cast<f16x8*>(planes);
     for (int i = threadIdx.x; i < TAPS * 2 * kPackTileM; i += 256) {
       const int ml = i % kPackTileM, h = (i / kPackTileM) & 1, t = i / (2 * kPackTileM);
@@ -199,6 +194,32 @@ __global__ void __launch_bounds__(256) k_absmax_jobs(const msl_pack_job* __restr
                jb.packed + pack_tail_offset(f32) + blockIdx.x);
 }
 
+// {sA, 1/sA} of a pack from its kNPart weight absmax partials, once per pack (the pack blocks read
+// sA: every one of them reducing the 256 partials itself read 4x its own 1-KB tile - 0.44 ms per
+// step for the ~170k blocks of the step's packs, r03)
+__device__ __forceinline__ void pack_scale(float* __restrict__ tail) {
+  float inv;
+  const float sc = pow2_scale(partials_max(tail, kNPart, threadIdx.x & 63), inv);
+  if (threadIdx.x == 0) {
+    tail[kNPart] = sc;
+    tail[kNPart + 1] = inv;
+  }
+}
+__global__ void __launch_bounds__(64) k_pack_scale(float* __restrict__ tail) { pack_scale(tail); }
+template <int TAPS>
+__global__ void __launch_bounds__(64) k_pack_scale_jobs(const msl_pack_job* __restrict__ jobs) {
+  const msl_pack_job jb = jobs[blockIdx.x];
+  const int cimg = jb.for_dgrad ? jb.cout : jb.cin;
+  const int m = jb.for_dgrad ? jb.cin : jb.cout;
+  const long long f32 = (long long)jb.nbranch * ((cimg + kCB - 1) / kCB) * TAPS * kCB * ((m + kPackPad - 1) / kPackPad * kPackPad);
+  pack_scale(jb.packed + pack_tail_offset(f32));
+}
+
+// (m chunk, channel block) tiles per block of the batched pack: a pointwise tile is only 256 floats
+// (one per thread), and the ~300k one-tile blocks of a step's pointwise packs took 288 us (r03)
+template <int TAPS>
+constexpr int kPackSub() { return TAPS == 1 ? 8 : 1; }
+
 // Every weight pack of a step in one launch (per tap count): block b runs block b - start[j] of
 // job j (start[] ascending, start[njobs] = the total), each job exactly as msl_*_pack would.
 template <int TAPS>
@@ -218,14 +239,21 @@ __global__ void __launch_bounds__(256) k_pack_split_many(const msl_pack_job* __r
   const int lda = (m + kPackPad - 1) / kPackPad * kPackPad;
   const int ncb = (cimg + kCB - 1) / kCB;
   const int nmx = lda / kPackTileM;
-  const long long local = b - start[lo];
-  const int mx = (int)(local % nmx);
-  const long long rest = local / nmx;
-  const int cb = (int)(rest % ncb), br = (int)(rest / ncb);
+  const long long tiles = (long long)nmx * ncb * jb.nbranch;
   const long long f32 = (long long)jb.nbranch * ncb * TAPS * kCB * lda;
-  pack_split_block<TAPS>(jb.w, jb.branch_stride, jb.cin, jb.cout, jb.for_dgrad, ncb, lda, m > 64 || h3, jb.packed,
-                         reinterpret_cast<__bf16*>(jb.packed + f32), mx, cb, br, s,
-                         h3 ? jb.packed + pack_tail_offset(f32) : nullptr);
+  constexpr int SUB = kPackSub<TAPS>();
+#pragma unroll 1
+  for (int sub = 0; sub < SUB; ++sub) {
+    const long long local = (b - start[lo]) * SUB + sub;
+    if (local >= tiles) break;  // block-uniform
+    if (sub) __syncthreads();   // the previous tile's LDS reads are done
+    const int mx = (int)(local % nmx);
+    const long long rest = local / nmx;
+    const int cb = (int)(rest % ncb), br = (int)(rest / ncb);
+    pack_split_block<TAPS>(jb.w, jb.branch_stride, jb.cin, jb.cout, jb.for_dgrad, ncb, lda, m > 64 || h3, jb.packed,
+                           reinterpret_cast<__bf16*>(jb.packed + f32), mx, cb, br, s,
+                           h3 ? jb.packed + pack_tail_offset(f32) : nullptr);
+  }
 }
 
 // ---------------------------------------------------------------- planning
@@ -708,6 +736,8 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
     hipLaunchKernelGGL(k_absmax, dim3(kNPart), dim3(256), 0, st, w, (long long)cout * cin * taps, branch_stride,
                        nbranch, tail);
     MSL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_pack_scale, dim3(1), dim3(64), 0, st, tail);
+    MSL_CHECK_LAUNCH();
   }
   if (taps == 9)
     hipLaunchKernelGGL(k_pack_split<9>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
@@ -951,7 +981,8 @@ long long msl_conv_pack_blocks(int nbranch, int taps, int cin, int cout, int for
   if (bad_dims(nbranch, cin, cout, 1, 1) || (taps != 1 && taps != 9)) return -1;
   const int cimg = for_dgrad ? cout : cin;
   const int m = for_dgrad ? cin : cout;
-  return (long long)(pad_to(m, kPackPad) / kPackTileM) * cdiv(cimg, kCB) * nbranch;
+  const long long tiles = (long long)(pad_to(m, kPackPad) / kPackTileM) * cdiv(cimg, kCB) * nbranch;
+  return taps == 1 ? cdiv(tiles, (long long)kPackSub<1>()) : tiles;  // blocks of msl_conv_pack_many
 }
 
 int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, int njobs, int taps,
@@ -966,6 +997,11 @@ int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, i
       hipLaunchKernelGGL(k_absmax_jobs<9>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
     else
       hipLaunchKernelGGL(k_absmax_jobs<1>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
+    MSL_CHECK_LAUNCH();
+    if (taps == 9)
+      hipLaunchKernelGGL(k_pack_scale_jobs<9>, dim3((unsigned)njobs), dim3(64), 0, st, jobs);
+    else
+      hipLaunchKernelGGL(k_pack_scale_jobs<1>, dim3((unsigned)njobs), dim3(64), 0, st, jobs);
     MSL_CHECK_LAUNCH();
   }
   if (taps == 9)
