@@ -466,15 +466,15 @@ __global__ void __launch_bounds__(256) k_bwd_cols(const float* __restrict__ T, G
 // ---------------------------------------------------------------- upsample forward
 __global__ void __launch_bounds__(256) k_upsample_fwd(const float* __restrict__ in, Geo g,
                                                        float* __restrict__ out) {
-  const int wq = (g.Wo + 3) / 4;
-  const long long n = (long long)g.C * g.Ho * wq;
+  const unsigned wq = (g.Wo + 3) / 4;
+  const unsigned n = (unsigned)g.C * g.Ho * wq;  // < 2^31 (msl_upsample_fwd checks): 32-bit decode
   const long long hwo = (long long)g.Ho * g.Wo;
   const bool vec = (g.Wo & 3) == 0;
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u) {
     const int q = (int)(e % wq);
-    const long long r = e / wq;
-    const int oy = (int)(r % g.Ho);
-    const int c = (int)(r / g.Ho);
+    const unsigned r = e / wq;
+    const int oy = (int)(r % (unsigned)g.Ho);
+    const int c = (int)(r / (unsigned)g.Ho);
     const Lin ly = lin(oy, g.sh, g.Hi);
     const float* plane = in + (long long)c * g.Hi * g.Wi;
     float v[4];
@@ -722,7 +722,8 @@ int msl_loss_stats_elems(void) { return kStats; }
 
 int msl_upsample_fwd(const float* in, float* out, int c, int hi, int wi, int ho, int wo,
                      msl_stream_t stream) {
-  if (c < 1 || hi < 1 || wi < 1 || ho < 1 || wo < 1 || !in || !out) return MSL_ERR_ARG;
+  if (c < 1 || hi < 1 || wi < 1 || ho < 1 || wo < 1 || !in || !out || (long long)c * ho * wo >= (1LL << 31))
+    return MSL_ERR_ARG;
   const Geo g = make_geo(c, hi, wi, ho, wo);
   const long long n = (long long)c * ho * ((wo + 3) / 4);
   const int blocks = (int)std::min<long long>(cdiv(n, 256), 8192);

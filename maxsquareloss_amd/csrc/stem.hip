@@ -8,7 +8,8 @@
 //     windows covering each input pixel, summed in torch-CPU's scatter order (bit-exact);
 //   - x[:, :, ::s, ::s] for layer2.0's stride-2 1x1 conv1 and downsample (deeplab_multi.py:12-13,
 //     96-99: Caffe-style, the stride sits on the 1x1 convs), and its transpose for the gradient.
-// Every kernel is a plain gather: one thread per output element, no atomics, no float reordering.
+// Every kernel is a plain gather: one thread per output element, no atomics, no float reordering;
+// element indices in 32-bit arithmetic (the entry points keep the counts below 2^31).
 #include "msl_internal.h"
 
 namespace msl {
@@ -19,16 +20,16 @@ namespace msl {
 __global__ void __launch_bounds__(256) k_im2col(const float* __restrict__ x, int H, int W, int NI, int KH, int KW,
                                                 int S, int PAD, int D, int HO, int WO, int K,
                                                 float* __restrict__ col) {
-  const int wq = (WO + 3) >> 2;
-  const long long total = (long long)K * NI * HO * wq;
+  const unsigned wq = (WO + 3) >> 2;
+  const unsigned total = (unsigned)K * NI * HO * wq;  // < 2^31 (msl_im2col checks): 32-bit index math
   const long long P = (long long)NI * HO * WO;
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < total; e += gridDim.x * 256u) {
     const int q = (int)(e % wq);
-    const long long r = e / wq;
-    const int oy = (int)(r % HO);
-    const long long r2 = r / HO;
-    const int n = (int)(r2 % NI);
-    const int k = (int)(r2 / NI);
+    const unsigned r = e / wq;
+    const int oy = (int)(r % (unsigned)HO);
+    const unsigned r2 = r / (unsigned)HO;
+    const int n = (int)(r2 % (unsigned)NI);
+    const int k = (int)(r2 / (unsigned)NI);
     const int j = k % KW, i = (k / KW) % KH, c = k / (KW * KH);
     const int iy = oy * S - PAD + i * D;
     const bool rowok = (unsigned)iy < (unsigned)H;
@@ -53,15 +54,15 @@ __global__ void __launch_bounds__(256) k_im2col(const float* __restrict__ x, int
 // position that maps (oy, ox) onto (y, xx).
 __global__ void __launch_bounds__(256) k_col2im(const float* __restrict__ col, int C, int H, int W, int NI, int KH,
                                                 int KW, int S, int PAD, int D, int HO, int WO, float* __restrict__ x) {
-  const long long total = (long long)C * NI * H * W;
+  const unsigned total = (unsigned)C * NI * H * W;  // < 2^31 (checked by the entry point)
   const long long P = (long long)NI * HO * WO;
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int xx = (int)(e % W);
-    const long long r = e / W;
-    const int y = (int)(r % H);
-    const long long r2 = r / H;
-    const int n = (int)(r2 % NI);
-    const int c = (int)(r2 / NI);
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < total; e += gridDim.x * 256u) {
+    const int xx = (int)(e % (unsigned)W);
+    const unsigned r = e / (unsigned)W;
+    const int y = (int)(r % (unsigned)H);
+    const unsigned r2 = r / (unsigned)H;
+    const int n = (int)(r2 % (unsigned)NI);
+    const int c = (int)(r2 / (unsigned)NI);
     float s = 0.f;
     for (int i = 0; i < KH; ++i) {
       const int ty = y + PAD - i * D;
@@ -86,11 +87,11 @@ __global__ void __launch_bounds__(256) k_col2im(const float* __restrict__ col, i
 __global__ void __launch_bounds__(256) k_maxpool_fwd(const float* __restrict__ x, int H, int W, int K, int S, int PAD,
                                                      int HO, int WO, long long total, float* __restrict__ y,
                                                      int32_t* __restrict__ idx) {
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int ox = (int)(e % WO);
-    const long long r = e / WO;
-    const int oy = (int)(r % HO);
-    const long long c = r / HO;
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < (unsigned)total; e += gridDim.x * 256u) {
+    const int ox = (int)(e % (unsigned)WO);
+    const unsigned r = e / (unsigned)WO;
+    const int oy = (int)(r % (unsigned)HO);
+    const long long c = r / (unsigned)HO;
     int y0 = oy * S - PAD, x0 = ox * S - PAD;
     const int y1 = min(y0 + K, H), x1 = min(x0 + K, W);
     y0 = max(y0, 0);
@@ -116,11 +117,11 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const float* __restrict__ x
 __global__ void __launch_bounds__(256) k_maxpool_bwd(const float* __restrict__ dy, const int32_t* __restrict__ idx,
                                                      int H, int W, int K, int S, int PAD, int HO, int WO,
                                                      long long total, float* __restrict__ dx) {
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int xx = (int)(e % W);
-    const long long r = e / W;
-    const int y = (int)(r % H);
-    const long long c = r / H;
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < (unsigned)total; e += gridDim.x * 256u) {
+    const int xx = (int)(e % (unsigned)W);
+    const unsigned r = e / (unsigned)W;
+    const int y = (int)(r % (unsigned)H);
+    const long long c = r / (unsigned)H;
     const int me = y * W + xx;
     // windows covering y: oy*S - PAD <= y <= oy*S - PAD + K - 1
     const int ly = y + PAD - (K - 1), lx = xx + PAD - (K - 1);
@@ -140,22 +141,22 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const float* __restrict__ d
 // y[c][oy][ox] = x[c][oy*S][ox*S]   (fwd)      x[c][y][xx] = (y % S || xx % S) ? 0 : y'[..]  (bwd)
 __global__ void __launch_bounds__(256) k_subsample(const float* __restrict__ x, int H, int W, int S, int HO, int WO,
                                                    long long total, float* __restrict__ y) {
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int ox = (int)(e % WO);
-    const long long r = e / WO;
-    const int oy = (int)(r % HO);
-    const long long c = r / HO;
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < (unsigned)total; e += gridDim.x * 256u) {
+    const int ox = (int)(e % (unsigned)WO);
+    const unsigned r = e / (unsigned)WO;
+    const int oy = (int)(r % (unsigned)HO);
+    const long long c = r / (unsigned)HO;
     y[e] = x[(c * H + (long long)oy * S) * W + (long long)ox * S];
   }
 }
 
 __global__ void __launch_bounds__(256) k_subsample_bwd(const float* __restrict__ dy, int H, int W, int S, int HO,
                                                        int WO, long long total, float* __restrict__ dx) {
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int xx = (int)(e % W);
-    const long long r = e / W;
-    const int y = (int)(r % H);
-    const long long c = r / H;
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < (unsigned)total; e += gridDim.x * 256u) {
+    const int xx = (int)(e % (unsigned)W);
+    const unsigned r = e / (unsigned)W;
+    const int y = (int)(r % (unsigned)H);
+    const long long c = r / (unsigned)H;
     float v = 0.f;
     if (y % S == 0 && xx % S == 0 && y / S < HO && xx / S < WO) v = dy[(c * HO + y / S) * WO + xx / S];
     dx[e] = v;
@@ -164,9 +165,11 @@ __global__ void __launch_bounds__(256) k_subsample_bwd(const float* __restrict__
 
 static unsigned grid_for(long long n) { return (unsigned)std::min<long long>((n + 255) / 256, 16384); }
 
+// every kernel above decodes its element index in 32-bit arithmetic (a 64-bit division per element
+// made the maxpool backward 5x slower than its bytes, r03): element counts stay below 2^31
 static bool bad_geom(int c, int h, int w, int k, int s, int pad, int ho, int wo) {
   return c < 1 || h < 1 || w < 1 || k < 1 || s < 1 || pad < 0 || ho < 1 || wo < 1 ||
-         (long long)c * h * w >= (1LL << 40) || (long long)h * w >= (1LL << 31);
+         (long long)c * h * w >= (1LL << 31) || (long long)c * ho * wo >= (1LL << 31);
 }
 
 }  // namespace msl
@@ -178,7 +181,7 @@ extern "C" {
 int msl_im2col(const float* x, int c, int h, int w, int nimg, int kh, int kw, int stride, int pad, int dil, int ho,
                int wo, float* col, msl_stream_t stream) {
   if (!x || !col || nimg < 1 || bad_geom(c * nimg, h, w, std::max(kh, kw), stride, pad, ho, wo) || kh < 1 ||
-      kw < 1 || dil < 1 || (long long)c * kh * kw * nimg * ho * wo >= (1LL << 40) ||
+      kw < 1 || dil < 1 || (long long)c * kh * kw * nimg * ho * wo >= (1LL << 31) ||
       (long long)nimg * ho * wo >= (1LL << 31))
     return MSL_ERR_ARG;
   const int K = c * kh * kw;
