@@ -290,6 +290,15 @@ def uda_step(model, opt, xs, ys, xt, cfg, it):
     ('maxsquare'|'IW_maxsquare'), multi, lambda_seg, lambda_target, IW_ratio, threshold."""
     lr = poly_lr(cfg["lr"], it, cfg["iter_max"])
     opt.groups[0]["lr"], opt.groups[1]["lr"] = lr, 10 * lr
+    out = uda_grads(model, xs, ys, xt, cfg)
+    opt.step()
+    opt.zero_grad()
+    return out
+
+
+def uda_grads(model, xs, ys, xt, cfg):
+    """The two forward/backward passes of uda_step (solve_gta5.py:344-381) without the optimizer step:
+    the gradients accumulate into the parameters' .grad (a data-parallel replica's local part)."""
     out = {}
     pred, pred_2 = model(xs)
     loss_s = ce(pred, ys)
@@ -317,8 +326,6 @@ def uda_step(model, opt, xs, ys, xt, cfg, it):
         out["loss_target_2"] = lt2.item()
     total.backward()
     out["loss_target"] = loss_t.item()
-    opt.step()
-    opt.zero_grad()
     return out
 
 

@@ -251,3 +251,137 @@ def test_graphed_dp_step_matches_eager_dp():
         assert np.array_equal(pe, pg), (r, int((pe != pg).sum()))
     for graph in (False, True):
         assert np.array_equal(got[0][graph][1], got[1][graph][1]), graph
+
+
+def _cfg2_worker(rank, world, port, q, outdir):
+    """One eager UDA iteration of BASELINE configs[2] (IW-MaxSquare, 1024x512, multi False, lambda_t 0.1)
+    on one of two data-parallel replicas; the initial weights (rank 0), the losses, the IW histogram
+    and the parameters after the step go to files."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK="0")
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from maxsquareloss_amd.tools.solve_gta5 import UDATrainer, build_parser
+        from maxsquareloss_amd.tools.train_source import init_args
+        from maxsquareloss_amd.utils.synthetic import synthetic_image, synthetic_labels
+        h, w = CFG2_HW
+        argv = ["--crop_size", f"{w},{h}", "--target_crop_size", f"{w},{h}", "--imagenet_pretrained", "False",
+                "--save_dir", "", "--target_mode", "IW_maxsquare", "--multi", "False", "--lambda_target", "0.1",
+                "--iter_max", "200000"]
+        args, _, _ = init_args(build_parser().parse_args(argv))
+        tr = UDATrainer(args, cuda=True)
+        assert tr.reducer is not None and tr.reducer.world == world and tr.pair
+        if rank == 0:
+            torch.save({k: v.detach().cpu() for k, v in tr.model.state_dict().items()},
+                       os.path.join(outdir, "init.pt"))
+        seed = 300 + rank
+        xs, ys, xt = synthetic_image(h, w, seed), synthetic_labels(h, w, 19, seed), synthetic_image(h, w, 600 + seed)
+        tr.optimizer.zero_grad()
+        tr.uda_step(xs.cuda(), ys.cuda(), xt.cuda())
+        torch.cuda.synchronize()
+        np.savez(os.path.join(outdir, f"params{rank}.npz"),
+                 **{n: p.detach().cpu().numpy() for n, p in tr.model.named_parameters()})
+        q.put((rank, "ok", tr.loss_val.item(), tr.loss_target.item(),
+               tr.target_loss.last_hist.cpu().numpy().astype(np.int64)))
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure to the parent instead of hanging it
+        import traceback
+        q.put((rank, "error", traceback.format_exc() + repr(e)))
+        raise
+
+
+CFG2_HW = (512, 1024)
+
+
+def test_dp_cfg2_full_size_matches_oracle(tmp_path):
+    """BASELINE configs[2] at its real size as a data-parallel step: two replicas (gloo, one GPU) each
+    run the pair-mode UDA iteration on their own 1024x512 images and exchange gradients once.  Held
+    against the CPU oracle of the same data-parallel step (each replica's gradients from its images,
+    averaged, one SGD step - oracle.uda_grads): every replica's losses within 1e-3 of the oracle at its
+    images, its IW histogram within 0.1 % of the pixels, both replicas' parameters identical after the
+    step, and the update per tensor within 3x the fp32 oracle's own distance to an fp64 oracle (the
+    bars of test_gpu_configs.py)."""
+    from oracle import msl_oracle as orc
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cfg2_worker, args=(r, world, port, q, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            item = q.get(timeout=600)
+            assert item[1] == "ok", item[2]
+            got[item[0]] = item[2:]
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    h, w = CFG2_HW
+    sd0 = torch.load(os.path.join(str(tmp_path), "init.pt"), weights_only=True)
+    cfg = dict(lr=2.5e-4, iter_max=200000, lambda_seg=0.1, IW_ratio=0.2, threshold=0.95, target_mode="IW_maxsquare",
+               multi=False, lambda_target=0.1)
+    from maxsquareloss_amd.tools.solve_gta5 import build_parser
+    from maxsquareloss_amd.tools.train_source import init_args
+    args, _, _ = init_args(build_parser().parse_args(["--imagenet_pretrained", "False", "--save_dir", ""]))
+    cfg.update(lr=args.lr, lambda_seg=args.lambda_seg, IW_ratio=args.IW_ratio, threshold=args.threshold)
+    res = {}
+    for dtype in (torch.float32, torch.float64):
+        model = orc.Model(sd0, 19, dtype=dtype)
+        opt = orc.SGDMult(model.params, model.names, cfg["lr"])
+        lr = orc.poly_lr(cfg["lr"], 0, cfg["iter_max"])
+        opt.groups[0]["lr"], opt.groups[1]["lr"] = lr, 10 * lr
+        outs = []
+        for r in range(world):
+            seed = 300 + r
+            outs.append(orc.uda_grads(model, orc_img(seed, h, w), orc_lab(seed, h, w), orc_img(600 + seed, h, w), cfg))
+        with torch.no_grad():
+            for p in model.params.values():
+                if p.grad is not None:
+                    p.grad.mul_(1.0 / world)  # the replicas' mean (the SGD kernel's grad_scale)
+        opt.step()
+        res[dtype] = (model, outs)
+    (m32, outs32), (m64, _) = res[torch.float32], res[torch.float64]
+    for r in range(world):
+        loss_s, loss_t, hist = got[r]
+        o = outs32[r]
+        for k, v in (("loss_seg", loss_s), ("loss_target", loss_t)):
+            rel = abs(v - o[k]) / max(abs(o[k]), 1e-30)
+            print(f"cfg2 dp rank {r} {k}: gpu {v:.7g} oracle {o[k]:.7g} rel {rel:.2e}")
+            assert v == pytest.approx(o[k], rel=1e-3), (r, k, v, o[k])
+        flips = int(np.abs(hist - o["hist"]).sum()) // 2
+        print(f"cfg2 dp rank {r} IW histogram: {flips} argmax flips of {h * w} pixels")
+        assert hist.sum() == o["hist"].sum() == h * w and flips <= 0.001 * h * w
+    p0, p1 = np.load(os.path.join(str(tmp_path), "params0.npz")), np.load(os.path.join(str(tmp_path), "params1.npz"))
+    e_gpu_all = e_cpu_all = 0.0
+    for n in m32.names:
+        assert np.array_equal(p0[n], p1[n]), n  # one exchange keeps the replicas in lock step
+        init = sd0[n].double()
+        du = torch.from_numpy(p0[n]).double() - init
+        dr = m32.params[n].detach().double() - init
+        d64 = m64.params[n].detach() - init
+        if d64.abs().max() == 0:
+            assert du.abs().max() == 0, n  # dead parameters (Q1) untouched
+            continue
+        e_gpu, e_cpu = (du - d64).norm().item(), (dr - d64).norm().item()
+        e_gpu_all += e_gpu ** 2
+        e_cpu_all += e_cpu ** 2
+        assert e_gpu <= max(3 * e_cpu, 1e-3 * d64.norm().item()), (n, e_gpu, e_cpu)
+    print(f"cfg2 dp SGD update vs fp64: gpu {e_gpu_all ** 0.5:.3e} cpu-fp32 {e_cpu_all ** 0.5:.3e}")
+    assert e_gpu_all <= 4 * e_cpu_all
+
+
+def orc_img(seed, h, w):
+    from maxsquareloss_amd.utils.synthetic import synthetic_image
+    return synthetic_image(h, w, seed)
+
+
+def orc_lab(seed, h, w):
+    from maxsquareloss_amd.utils.synthetic import synthetic_labels
+    return synthetic_labels(h, w, 19, seed)
