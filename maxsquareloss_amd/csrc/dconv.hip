@@ -494,7 +494,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   // operand straight to registers) instead of exact-f32 32 / 64-row tiles: 3 fp16 MFMAs per 16-deep
   // slice at 64 rows cost 2.7x less matrix time than 8 f32 MFMAs at 32 rows.  Variant bit 4 keeps
   // the exact-f32 tiles.
-  const bool small_f16 = MT == kMathH3P && pl.sk && pl.bm <= 64 && taps == 9 && !(g_variant & 16);
+  // (r03: also the pointwise / stem GEMMs with M <= 64 - layer1's 256 -> 64 convs, the 64-channel data
+  // gradients, the stem's 147 -> 64 - through the same form with one unshifted tap)
+  const bool small_f16 = MT == kMathH3P && pl.sk && pl.bm <= 64 && !(g_variant & 16);
   if (small_f16) {
     pl.G = 1;
     pl.bm = 64;
