@@ -211,6 +211,7 @@ struct BnBwdArgs {
   const float* x;
   const float* y;  // output (for the ReLU mask) or null
   const float* gamma;
+  const float* beta;  // fused form with relu and y = null: the mask recomputed from x (no residual)
   const float* save_mean;
   const float* save_invstd;
   float* dx;
@@ -424,7 +425,7 @@ __device__ __forceinline__ void block_sum2_d16(double& a, double& b, double* red
 }
 
 template <int EPT>
-__global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
+__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= 9 ? 8 : 1))) k_bn_fwd_fused(BnArgs a) {
   __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
   float am = 0.f;
@@ -433,16 +434,11 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
   const int r = c * a.NI + img;
   const long long base = (long long)r * P;
   const float* xc = a.x + base;
-  float xv[EPT], rv[EPT];
+  float xv[EPT];
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
     xv[j] = e < P ? xc[e] : 0.f;
-  }
-#pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = j * kBnFusedThreads + t;
-    rv[j] = (a.residual && e < P) ? a.residual[base + e] : 0.f;
   }
   const double shift = (double)xc[0];
   double s1 = 0.0, s2 = 0.0;
@@ -475,6 +471,14 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
   const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
   const float bsh = __fmaf_rn(-mean, alpha, a.beta ? a.beta[c] : 0.f);
   float* yc = a.y + base;
+  // the residual is loaded after the statistics: not live across the reduction, so the EPT <= 9
+  // forms fit 64 VGPRs (two 1024-thread blocks per CU)
+  float rv[EPT];
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    rv[j] = (a.residual && e < P) ? a.residual[base + e] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
@@ -495,7 +499,7 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_fwd_fused(BnArgs a) {
 }
 
 template <int EPT>
-__global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
+__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= 9 ? 8 : 1))) k_bn_bwd_fused(BnBwdArgs a) {
   __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
   float am = 0.f;
@@ -512,12 +516,18 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
     g[j] = e < P ? a.dy[base + e] : 0.f;
     xv[j] = e < P ? a.x[base + e] : 0.f;
   }
-  if (a.relu) {
+  const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
+  if (a.relu && a.y) {
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const int e = j * kBnFusedThreads + t;
       if (e < P && !(a.y[base + e] > 0.f)) g[j] = 0.f;
     }
+  } else if (a.relu) {  // y > 0 recomputed with k_bn_fwd_fused's operations (its alpha, bsh)
+    const float bsh = __fmaf_rn(-mean, w, a.beta ? a.beta[c] : 0.f);
+#pragma unroll
+    for (int j = 0; j < EPT; ++j)
+      if (!(__fmaf_rn(xv[j], w, bsh) > 0.f)) g[j] = 0.f;
   }
   double sg = 0.0, sgx = 0.0;
 #pragma unroll
@@ -536,7 +546,6 @@ __global__ void __launch_bounds__(kBnFusedThreads) k_bn_bwd_fused(BnBwdArgs a) {
       db += (float)sg;
     }
   }
-  const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
   const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
@@ -672,9 +681,19 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
                   const float* save_mean, const float* save_invstd, float* dx, float* dres,
                   float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
                   int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
-  if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31) ||
-      (relu && !y))
+  if (relu && !y) return MSL_ERR_ARG;
+  return msl_bn_bwd_am_beta(dy, x, y, gamma, nullptr, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, nimg,
+                            training, relu, accumulate_params, ws, ws_bytes, stream, absmax_dx);
+}
+
+int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const float* gamma, const float* beta,
+                       const float* save_mean, const float* save_invstd, float* dx, float* dres,
+                       float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
+                       int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
+  if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
     return MSL_ERR_ARG;
+  const bool fused = training && bn_fused_enabled() && bn_fused_shape(c, p);
+  if (relu && !y && !fused) return MSL_ERR_ARG;  // the mask recompute is the fused kernels' alone
   if (absmax_dx && !dx) return MSL_ERR_ARG;
   if (ws_bytes < msl_bn_workspace(c, p, nimg)) return MSL_ERR_WORKSPACE;
   hipStream_t st = as_stream(stream);
@@ -685,6 +704,7 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
   a.x = x;
   a.y = y;
   a.gamma = gamma;
+  a.beta = beta;
   a.save_mean = save_mean;
   a.save_invstd = save_invstd;
   a.dx = dx;
@@ -701,7 +721,7 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
   a.training = training;
   a.accumulate = accumulate_params;
   a.absmax = absmax_dx;
-  if (training && bn_fused_enabled() && bn_fused_shape(c, p))
+  if (fused)
     return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);

@@ -1065,7 +1065,10 @@ class _BNAct(Function):
                                     hip.stream_ptr(), hip.ptr(am)), "msl_bn_fwd")
         if am is not None:
             _tag_absmax(y, am)
-        ctx.save_for_backward(x, weight, y if relu else None, save_mean, save_invstd)
+        # ReLU without a residual under the fused kernels: the backward recomputes the mask from x
+        # (msl_bn_bwd_am_beta, y = NULL) instead of reading y
+        remask = bool(relu) and residual is None and bool(lib.msl_bn_uses_fused(c, p, int(bool(training))))
+        ctx.save_for_backward(x, weight, y if (relu and not remask) else None, save_mean, save_invstd)
         ctx.bias = bias
         ctx.meta = (c, p, n, bool(training), bool(relu))
         ctx.hold = hold
@@ -1094,10 +1097,11 @@ class _BNAct(Function):
         # f16x3: the per-channel absmax of dx, the gradient the conv before this BN reads twice
         am = torch.empty(c, dtype=_f32, device=x.device) if (
             dx is not None and _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(training))) else None
-        hip.check(lib.msl_bn_bwd_am(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight), save_mean.data_ptr(),
-                                    save_invstd.data_ptr(), hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma),
-                                    hip.ptr(dbeta), c, p, n, int(training), int(relu), int(direct), ws.data_ptr(), wsb,
-                                    hip.stream_ptr(), hip.ptr(am)), "msl_bn_bwd")
+        hip.check(lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight),
+                                         hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(),
+                                         hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n,
+                                         int(training), int(relu), int(direct), ws.data_ptr(), wsb,
+                                         hip.stream_ptr(), hip.ptr(am)), "msl_bn_bwd")
         if am is not None:
             _tag_absmax(dx, am)
         if direct:

@@ -841,6 +841,62 @@ def test_bn_absmax_outputs(c, h, w, res, relu, fused):
         ops.set_bn_fused(prev)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,h,w,nimg", [(256, 65, 129, 2), (512, 65, 129, 1), (128, 33, 65, 2), (2048, 17, 33, 2)])
+def test_bn_bwd_relu_mask_recompute(c, h, w, nimg):
+    """msl_bn_bwd_am_beta with y = NULL (the fused kernel recomputes the ReLU mask from x, beta and the
+    saved statistics): the same dx / dgamma / dbeta / absmax bytes as msl_bn_bwd_am reading y, incl.
+    pre-activations that are exactly 0 (x = mean, beta = 0 channels); y = NULL is refused where the
+    split kernels would run, and by msl_bn_bwd_am."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    prev = ops.set_bn_fused(True)
+    try:
+        g = torch.Generator().manual_seed(c + nimg)
+        p = h * w
+        x = torch.randn(c, nimg, p, generator=g) * 3 + 1
+        x[:, :, : p // 2] = x[:, :, :1]  # half of each row equal: many pre-activations at the mean
+        x = x.reshape(c, nimg * p).to(DEV)
+        gamma = (torch.rand(c, generator=g) + 0.5).to(DEV)
+        beta = torch.randn(c, generator=g)
+        beta[::3] = 0.0
+        beta = beta.to(DEV)
+        gy = torch.randn(c, nimg * p, generator=g).to(DEV)
+        wsb = lib.msl_bn_workspace(c, p, nimg)
+        ws = hip.workspace(wsb, x.device)
+        s = hip.stream_ptr()
+        rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+        y = torch.empty_like(x)
+        sm, si = torch.empty(c * nimg, device=DEV), torch.empty(c * nimg, device=DEV)
+        assert lib.msl_bn_fwd(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), None, y.data_ptr(), rm.data_ptr(),
+                              rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, nimg, 1, 1, 0.1, 1e-5, 1,
+                              ws.data_ptr(), wsb, s) == 0
+        assert lib.msl_bn_uses_fused(c, p, 1) == 1
+        outs = []
+        for remask in (False, True):
+            dx = torch.empty_like(x)
+            dg, db, am = (torch.empty(c, device=DEV) for _ in range(3))
+            args = (gy.data_ptr(), x.data_ptr(), None if remask else y.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                    sm.data_ptr(), si.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(), c, p, nimg, 1, 1, 0,
+                    ws.data_ptr(), wsb, s, am.data_ptr())
+            assert lib.msl_bn_bwd_am_beta(*args) == 0
+            torch.cuda.synchronize()
+            outs.append((dx, dg, db, am))
+        assert (y == 0).float().mean().item() > 0.2  # the mask matters
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
+        # refusals: the split forms read y; msl_bn_bwd_am always needs it
+        assert lib.msl_bn_bwd_am(gy.data_ptr(), x.data_ptr(), None, gamma.data_ptr(), sm.data_ptr(), si.data_ptr(),
+                                 dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(), c, p, nimg, 1, 1, 0, ws.data_ptr(),
+                                 wsb, s, None) == -3
+        ops.set_bn_fused(False)
+        assert lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), None, gamma.data_ptr(), beta.data_ptr(),
+                                      sm.data_ptr(), si.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(),
+                                      c, p, nimg, 1, 1, 0, ws.data_ptr(), wsb, s, None) == -3
+    finally:
+        ops.set_bn_fused(prev)
+
+
 # ---------------------------------------------------------------------------- stem / maxpool / stride 2
 @pytest.mark.parametrize("h,w", [(64, 128), (33, 47), (512, 1024)])
 def test_stem_conv_fwd_bwd(h, w, f32_form):
