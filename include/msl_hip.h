@@ -418,8 +418,8 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
  * then recomputes the ReLU mask from x (y > 0 <=> fma(x, invstd*gamma, fma(-mean, invstd*gamma,
  * beta)) > 0, the forward's own float operations on the saved mean / invstd, so the mask is
  * identical) instead of reading y - one read of the map less.  beta = the forward's beta
- * (nullable = 0).  y = NULL needs msl_bn_uses_fused(c, p, training) (else MSL_ERR_ARG); with y
- * given it is msl_bn_bwd_am. */
+ * (nullable = 0).  y = NULL needs msl_bn_uses_fused(c, p, training) and p <= 16384 (else
+ * MSL_ERR_ARG); with y given it is msl_bn_bwd_am. */
 int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const float* gamma,
                        const float* beta, const float* save_mean, const float* save_invstd, float* dx,
                        float* dres, float* dgamma, float* dbeta, int c, int p, int nimg, int training,

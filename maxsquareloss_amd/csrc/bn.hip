@@ -397,6 +397,7 @@ int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
+constexpr int kBnRemaskMaxEpt = 16;  // msl_bn_bwd_am_beta's y = NULL: p <= 16 * 1024
 constexpr int kBnFusedMaxP = 33 * kBnFusedThreads;  // layer1 at 1024x512: 257x129 = 33153 px
 static int g_bn_fused = 1;  // msl_bn_set_fused
 static bool bn_fused_enabled() { return g_bn_fused != 0; }
@@ -524,10 +525,12 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
       if (e < P && !(a.y[base + e] > 0.f)) g[j] = 0.f;
     }
   } else if (a.relu) {  // y > 0 recomputed with k_bn_fwd_fused's operations (its alpha, bsh)
-    const float bsh = __fmaf_rn(-mean, w, a.beta ? a.beta[c] : 0.f);
+    if constexpr (EPT <= kBnRemaskMaxEpt) {  // (the 33-element form spills twice as much with it)
+      const float bsh = __fmaf_rn(-mean, w, a.beta ? a.beta[c] : 0.f);
 #pragma unroll
-    for (int j = 0; j < EPT; ++j)
-      if (!(__fmaf_rn(xv[j], w, bsh) > 0.f)) g[j] = 0.f;
+      for (int j = 0; j < EPT; ++j)
+        if (!(__fmaf_rn(xv[j], w, bsh) > 0.f)) g[j] = 0.f;
+    }
   }
   double sg = 0.0, sgx = 0.0;
 #pragma unroll
@@ -693,7 +696,8 @@ int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const fl
   if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
     return MSL_ERR_ARG;
   const bool fused = training && bn_fused_enabled() && bn_fused_shape(c, p);
-  if (relu && !y && !fused) return MSL_ERR_ARG;  // the mask recompute is the fused kernels' alone
+  // the mask recompute is the fused kernels' alone, up to 16 elements per lane
+  if (relu && !y && !(fused && p <= kBnRemaskMaxEpt * kBnFusedThreads)) return MSL_ERR_ARG;
   if (absmax_dx && !dx) return MSL_ERR_ARG;
   if (ws_bytes < msl_bn_workspace(c, p, nimg)) return MSL_ERR_WORKSPACE;
   hipStream_t st = as_stream(stream);

@@ -1065,9 +1065,10 @@ class _BNAct(Function):
                                     hip.stream_ptr(), hip.ptr(am)), "msl_bn_fwd")
         if am is not None:
             _tag_absmax(y, am)
-        # ReLU without a residual under the fused kernels: the backward recomputes the mask from x
-        # (msl_bn_bwd_am_beta, y = NULL) instead of reading y
-        remask = bool(relu) and residual is None and bool(lib.msl_bn_uses_fused(c, p, int(bool(training))))
+        # ReLU without a residual under the fused kernels (p <= 16384): the backward recomputes the
+        # mask from x (msl_bn_bwd_am_beta, y = NULL) instead of reading y
+        remask = (bool(relu) and residual is None and p <= 16384
+                  and bool(lib.msl_bn_uses_fused(c, p, int(bool(training)))))
         ctx.save_for_backward(x, weight, y if (relu and not remask) else None, save_mean, save_invstd)
         ctx.bias = bias
         ctx.meta = (c, p, n, bool(training), bool(relu))

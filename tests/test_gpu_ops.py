@@ -889,6 +889,12 @@ def test_bn_bwd_relu_mask_recompute(c, h, w, nimg):
         assert lib.msl_bn_bwd_am(gy.data_ptr(), x.data_ptr(), None, gamma.data_ptr(), sm.data_ptr(), si.data_ptr(),
                                  dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(), c, p, nimg, 1, 1, 0, ws.data_ptr(),
                                  wsb, s, None) == -3
+        big = 129 * 257  # fused, but the 33-element form keeps reading y (checked before any launch)
+        assert lib.msl_bn_uses_fused(256, big, 1) == 1
+        assert lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), None, gamma.data_ptr(), beta.data_ptr(),
+                                      sm.data_ptr(), si.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(),
+                                      256, big, 1, 1, 1, 0, ws.data_ptr(), lib.msl_bn_workspace(256, big, 1), s,
+                                      None) == -3
         ops.set_bn_fused(False)
         assert lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), None, gamma.data_ptr(), beta.data_ptr(),
                                       sm.data_ptr(), si.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(),
