@@ -425,8 +425,23 @@ __device__ __forceinline__ void block_sum2_d16(double& a, double& b, double* red
   }
 }
 
+// Row accesses of the fused kernels as buffer instructions: one 32-bit lane offset (t * 4) plus the
+// element block j in the scalar offset, so the EPT loads and stores of a lane share one address VGPR
+// (flat addressing held a 64-bit pointer per j: 80-103 VGPRs, one 1024-thread block per CU).  Lanes
+// past the row are masked by the callers (no access is out of range).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bn_row(const float* p, int n) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, n * 4, 0x00020000);
+}
+__device__ __forceinline__ float bn_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, int j) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, j * kBnFusedThreads * 4, 0));
+}
+__device__ __forceinline__ void bn_st(__amdgpu_buffer_rsrc_t r, unsigned voff, int j, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, j * kBnFusedThreads * 4, 0);
+}
+constexpr int kBnTwoBlockEpt = 16;  // forms built for two blocks per CU (64 VGPRs)
+
 template <int EPT>
-__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= 9 ? 8 : 1))) k_bn_fwd_fused(BnArgs a) {
+__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= kBnTwoBlockEpt ? 8 : 1))) k_bn_fwd_fused(BnArgs a) {
   __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
   float am = 0.f;
@@ -435,11 +450,13 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
   const int r = c * a.NI + img;
   const long long base = (long long)r * P;
   const float* xc = a.x + base;
+  const unsigned vo = (unsigned)t * 4u;
+  const __amdgpu_buffer_rsrc_t rx = bn_row(xc, P);
   float xv[EPT];
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
-    xv[j] = e < P ? xc[e] : 0.f;
+    xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
   }
   const double shift = (double)xc[0];
   double s1 = 0.0, s2 = 0.0;
@@ -471,14 +488,17 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
   }
   const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
   const float bsh = __fmaf_rn(-mean, alpha, a.beta ? a.beta[c] : 0.f);
-  float* yc = a.y + base;
-  // the residual is loaded after the statistics: not live across the reduction, so the EPT <= 9
+  const __amdgpu_buffer_rsrc_t ry = bn_row(a.y + base, P);
+  // the residual is loaded after the statistics: not live across the reduction, so the EPT <= 16
   // forms fit 64 VGPRs (two 1024-thread blocks per CU)
   float rv[EPT];
+  if (a.residual) {
+    const __amdgpu_buffer_rsrc_t rr = bn_row(a.residual + base, P);
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = j * kBnFusedThreads + t;
-    rv[j] = (a.residual && e < P) ? a.residual[base + e] : 0.f;
+    for (int j = 0; j < EPT; ++j) rv[j] = j * kBnFusedThreads + t < P ? bn_ld(rr, vo, j) : 0.f;
+  } else {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) rv[j] = 0.f;
   }
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
@@ -487,7 +507,7 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
       float v = __fmaf_rn(xv[j], alpha, bsh);
       v += rv[j];
       v = a.relu ? fmaxf(v, 0.f) : v;
-      yc[e] = v;
+      bn_st(ry, vo, j, v);
       am = fmaxf(am, fabsf(v));
     }
   }
@@ -500,7 +520,7 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
 }
 
 template <int EPT>
-__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= 9 ? 8 : 1))) k_bn_bwd_fused(BnBwdArgs a) {
+__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= kBnTwoBlockEpt ? 8 : 1))) k_bn_bwd_fused(BnBwdArgs a) {
   __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
   float am = 0.f;
@@ -510,19 +530,22 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
   const int r = c * a.NI + img;
   const long long base = (long long)r * P;
   const float mean = a.save_mean[r], invstd = a.save_invstd[r];
+  const unsigned vo = (unsigned)t * 4u;
+  const __amdgpu_buffer_rsrc_t rdy = bn_row(a.dy + base, P), rx = bn_row(a.x + base, P);
   float g[EPT], xv[EPT];
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
-    g[j] = e < P ? a.dy[base + e] : 0.f;
-    xv[j] = e < P ? a.x[base + e] : 0.f;
+    g[j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
+    xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
   }
   const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
   if (a.relu && a.y) {
+    const __amdgpu_buffer_rsrc_t ryy = bn_row(a.y + base, P);
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const int e = j * kBnFusedThreads + t;
-      if (e < P && !(a.y[base + e] > 0.f)) g[j] = 0.f;
+      if (e < P && !(bn_ld(ryy, vo, j) > 0.f)) g[j] = 0.f;
     }
   } else if (a.relu) {  // y > 0 recomputed with k_bn_fwd_fused's operations (its alpha, bsh)
     if constexpr (EPT <= kBnRemaskMaxEpt) {  // (the 33-element form spills twice as much with it)
@@ -550,14 +573,16 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
     }
   }
   const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
+  const __amdgpu_buffer_rsrc_t rdres = bn_row(a.dres ? a.dres + base : nullptr, P);
+  const __amdgpu_buffer_rsrc_t rdx = bn_row(a.dx ? a.dx + base : nullptr, P);
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
     if (e < P) {
       const float xh = (xv[j] - mean) * invstd;
-      if (a.dres) a.dres[base + e] = g[j];
+      if (a.dres) bn_st(rdres, vo, j, g[j]);
       const float d = __fmul_rn(__fmaf_rn(-xh, m2, __fsub_rn(g[j], m1)), w);
-      if (a.dx) a.dx[base + e] = d;
+      if (a.dx) bn_st(rdx, vo, j, d);
       am = fmaxf(am, fabsf(d));
     }
   }
