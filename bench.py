@@ -48,6 +48,35 @@ def feat_hw(n):
     return (m - 1) // 2 + 1
 
 
+def pool_out(n, k, s, p, ceil):
+    """torch's pooling output size (dilation 1)."""
+    num = n + 2 * p - (k - 1) - 1 + ((s - 1) if ceil else 0)
+    o = num // s + 1
+    if ceil and (o - 1) * s >= n + p:
+        o -= 1
+    return o
+
+
+def conv_gflop(H, W, C):
+    """(forward GFLOP of every conv of DeeplabMulti for one H x W image, the stem's share): 2*cin*cout*k*k
+    per output pixel over the stem, the 33 Bottlenecks (3 / 4 / 23 / 3) with their downsamples and both
+    live ASPP branches of both heads (deeplab_multi.py:8-48, 51-66, 69-101).  1024x512, C = 19:
+    741.44 and 2.47."""
+    hs, ws = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    hm, wm = pool_out(hs, 3, 2, 1, True), pool_out(ws, 3, 2, 1, True)
+    h2, w2 = (hm - 1) // 2 + 1, (wm - 1) // 2 + 1
+    stem = 2.0 * 64 * 3 * 49 * hs * ws
+    f, inpl = stem, 64
+    for planes, blocks, p in ((64, 3, hm * wm), (128, 4, h2 * w2), (256, 23, h2 * w2), (512, 3, h2 * w2)):
+        for b in range(blocks):
+            f += 2.0 * inpl * planes * p + 2.0 * planes * planes * 9 * p + 2.0 * planes * planes * 4 * p
+            if b == 0:
+                f += 2.0 * inpl * planes * 4 * p  # downsample
+            inpl = planes * 4
+    f += 2 * (2.0 * 1024 * C * 9 * h2 * w2) + 2 * (2.0 * 2048 * C * 9 * h2 * w2)
+    return f / 1e9, stem / 1e9
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,32 +193,42 @@ def main():
 
     flops = 2.0 * 256 * 256 * 9 * h3 * w3 * nimg
     achieved = flops / (kern_ms * 1e-3) / 1e12
-    traffic = None
+    form = ops.f32_form() if a.conv_math == "fp32" else a.conv_math
+    # the op the probe timed: the GEMM alone when its stream-K pieces are summed by the BN kernel that
+    # follows it (ops.FOLD, conv -> BN fusion), else the GEMM + its piece-reduce launch
+    folded = ops._fold_math(a.conv_math) is not None
+    kernels = "k_igemm_fwd_sk2" if folded else "k_igemm_fwd_sk2,k_sk_reduce"
+    traffic, rec = None, None
     if os.path.exists(a.pmc):
         try:
-            traffic = json.load(open(a.pmc)).get("hbm_bytes_per_launch")
+            rec = json.load(open(a.pmc))
         except Exception:
-            traffic = None
-    form = ops.f32_form() if a.conv_math == "fp32" else a.conv_math
+            rec = None
+    # the committed PMC figure counts only if it was measured on this very kernel: form, image count,
+    # map size and the launches one op call makes
+    if rec is not None and (rec.get("form") == form and rec.get("nimg") == nimg and rec.get("h") == h3
+                            and rec.get("w") == w3 and rec.get("kernel") == kernels):
+        traffic = rec.get("hbm_bytes_per_launch")
     # the bound of the kernel's own arithmetic: FP32 MFMA, BF16 MFMA, or BF16 MFMA at six
     # products per fp32 product (the bf16x6 form): 2500 / 6 = 416.7 fp32-equivalent TFLOP/s
     # and FP16 MFMA (same rate) at three products per fp32 product (the f16x3 form): 833.3
     peak = {"mfma_f32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "fp16": BF16_MFMA_PEAK_TFLOPS,
             "bf16x6": round(BF16_MFMA_PEAK_TFLOPS / 6, 1), "f16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1)}[form]
-    if traffic is not None:
-        rec = json.load(open(a.pmc))
-        if rec.get("form", "mfma_f32") != form or rec.get("nimg", 1) != nimg:
-            traffic = None  # the committed PMC figure belongs to another form or image count of the kernel
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_source": (os.path.relpath(a.pmc, ROOT) + ": committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                    "passes of this kernel (scripts/gpu_bench_prof.sh), not measured in this run; "
                                    "memory-side bytes incl. Infinity-Cache hits") if traffic is not None else None,
-                "fp32_equiv_tflops_over_fp32_spec": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "fp32_equiv_tflops_over_bf16x6_bound": round(achieved / (BF16_MFMA_PEAK_TFLOPS / 6), 4),
-                "kernel": f"dconv3x3 fwd layer3 d=2 over {nimg} image(s) (one op call: stream-K k_igemm_fwd_sk(2) + k_sk_reduce; the weight planes are split at pack time, once per SGD step; f16x3: the input's absmax partials come from the BN kernel that produced it)",
+                "kernel": f"dconv3x3 fwd layer3 d=2 over {nimg} image(s): {kernels} (" + (
+                    "the stream-K pieces of its split tiles are summed by the BN kernel that reads the map, "
+                    "msl_bn_fwd_pend" if folded else "the stream-K GEMM and its piece reduce") +
+                "; the weight planes are split at pack time, once per SGD step; f16x3: the input's absmax "
+                "partials come from the BN kernel that produced it)",
                 "form": form, "kernel_ms": round(kern_ms, 4), "launches": len(probes),
-                "algorithmic_gflop_per_launch": round(flops / 1e9, 3)}
+                "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
+                # NOT a utilisation: fp32-equivalent TFLOP/s of the f16x3 / bf16x6 forms (3 / 6 MFMAs per
+                # fp32 product on the FP16 / BF16 pipes) compared with the FP32 matrix pipe's spec
+                "fp32_equiv_speedup_vs_fp32_mfma_spec": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)}
 
     cpu = None
     loss_delta = None
@@ -217,6 +256,20 @@ def main():
                "s_per_iter": round(s_per_iter, 3)}
 
     ms_per_step = elapsed / a.steps * 1e3
+    # the whole step against the conv roofline (north_star: "images/sec ... as fraction of the conv
+    # roofline"): every conv's algorithmic FLOPs of one iteration (2 images x (forward + data gradient +
+    # weight gradient), the stem without its data gradient) over the measured step time
+    fwd_gf, stem_gf = conv_gflop(H, W, C)
+    step_gf = 2 * (3 * fwd_gf - stem_gf)
+    step_tf = step_gf / ms_per_step
+    bound = {"f16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1), "bf16x6": round(BF16_MFMA_PEAK_TFLOPS / 6, 1),
+             "mfma_f32": FP32_MFMA_PEAK_TFLOPS, "fp16": BF16_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS}[form]
+    step_roofline = {"conv_gflop_per_step": round(step_gf, 1), "achieved_tflops": round(step_tf, 2),
+                     "frac_of_form_bound": round(step_tf / bound, 4), "form_bound_tflops": bound,
+                     "frac_of_fp32_mfma_spec": round(step_tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "note": "all conv FLOPs of one iteration / ms_per_step; the form bound is the MFMA peak of "
+                             "the conv math's form (f16x3: 2500/3 fp32-equivalent TFLOP/s); the FP32 spec "
+                             "fraction compares fp32-equivalent work with the FP32 matrix pipe"}
     line = {
         "metric": METRIC, "value": round(images / elapsed, 3), "unit": "images/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
@@ -227,7 +280,7 @@ def main():
                    "conv_math": a.conv_math, "bn_form": a.bn_form, "hipgraph": graphed, "pair": bool(a.pair), "overlap": bool(a.overlap), "async_wgrad": bool(a.async_wgrad), "variant": a.variant, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
                    "target_mode": args.target_mode, "multi": args.multi, "lambda_target": args.lambda_target,
                    "num_classes": C, "global_batch": 2 * world, "parallelism": f"dp{world}"},
-        "roofline": roofline, "cpu_baseline": cpu,
+        "roofline": roofline, "step_roofline": step_roofline, "cpu_baseline": cpu,
         "loss_delta_vs_cpu": None if loss_delta is None else {k: float(f"{v:.3g}") for k, v in loss_delta.items()},
         "iterations_per_s": round(a.steps * 1.0 / elapsed, 4),
     }

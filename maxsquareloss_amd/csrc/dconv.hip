@@ -429,6 +429,16 @@ static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials 
   return reinterpret_cast<float*>((char*)ws + ((ws_bytes - (size_t)k * kPartBytes) & ~(size_t)15));
 }
 
+// most pieces any split tile of a stream-K schedule leaves (workers its iteration range touches)
+static int sk_max_pieces(const SkArgs& sk, long long tiles) {
+  int mx = 1;
+  for (long long tl = 0; tl < tiles - sk.tdp; ++tl) {
+    const int lo = sk_worker_of((int)(tl * sk.KS), sk.T, sk.NW), hi = sk_worker_of((int)((tl + 1) * sk.KS - 1), sk.T, sk.NW);
+    mx = std::max(mx, hi - lo + 1);
+  }
+  return mx;
+}
+
 // The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
 template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk,
@@ -473,8 +483,10 @@ template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int nimg, int dil0,
                            int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st,
-                           int accum = 0, const float* img_part = nullptr, int img_npart = 0) {
+                           int accum = 0, const float* img_part = nullptr, int img_npart = 0,
+                           msl_sk_pending* pend = nullptr) {
   const int P = nimg * h * w;  // nimg images of h x w stacked along the pixel axis
+  if (pend) pend->pending = 0;
   FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
   // The x6 form runs one K-step per stage, three stages deep (scripts/tune_dconv.hip x6, layer3:
   // 87 us vs 115 with two K-steps per stage; f32 is indifferent); its 64- and 32-row tiles stay
@@ -585,7 +597,27 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     a.bias = bias;
     const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);  // (chunked: NW = items <= 512)
     const dim3 rgrid(pl.bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp));
-    const bool reduce = T > 0;
+    bool reduce = T > 0;
+    // conv -> BN fusion (msl_*_pend): the consumer sums the pieces; the f16x3 / fp16 forms, range-split
+    // stream-K, no bias, at most kFoldMaxPieces pieces per tile (the consumer's unrolled sum)
+    const int maxp = (pend && reduce) ? sk_max_pieces(sk, tiles) : 0;
+    if (pend && reduce && F16 && (pl.bm == 128 || small_f16) && sk.nchunk == 0 && !bias && maxp <= kFoldMaxPieces) {
+      reduce = false;
+      pend->maxp = maxp;
+      pend->part = sk.part;
+      pend->pending = 1;
+      pend->bm = pl.bm;
+      pend->bn = kSkBN;
+      pend->tiles_m = sk.tiles_m;
+      pend->tiles_n = sk.tiles_n;
+      pend->ks = sk.KS;
+      pend->nw = sk.NW;
+      pend->t = sk.T;
+      pend->tdp = sk.tdp;
+      pend->accum = accum;
+      pend->m = M;
+      pend->p = P;
+    }
     if (X6L && (pl.bm == 128 || small_f16)) {
       // the x6 kernel stages its weights from the bf16 planes that pack() split once, behind
       // the fp32 part of the same buffer (M > 64 <=> 128-row tiles; f16x3: every M)
@@ -910,6 +942,8 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   return MSL_OK;
 }
 
+static bool f16_ready() { return g_f32_form == kMathH3P; }  // the fp16 math reads the f16x3 packs
+
 template <typename... Args>
 static int fwd_f32(Args... args) {
   if (g_f32_form == kMathH3P) return launch_fwd_form<kMathH3P>(args...);
@@ -920,6 +954,12 @@ template <typename... Args>
 static int wgrad_f32(Args... args) {
   if (g_f32_form == kMathH3P) return launch_wgrad<kMathH3P>(args...);
   return g_f32_form == kMathX6 ? launch_wgrad<kMathX6>(args...) : launch_wgrad<kMathF32>(args...);
+}
+
+template <typename... Args>
+static int fwd_math(int fp16, Args... args) {
+  if (fp16) return f16_ready() ? launch_fwd_form<kMathH1P>(args...) : MSL_ERR_ARG;
+  return fwd_f32(args...);
 }
 
 }  // namespace msl
@@ -1192,6 +1232,69 @@ int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cou
                       as_stream(stream));
 }
 
+// ------------------------------------------------------------------ conv -> BN fusion (msl_sk_pending)
+int msl_dconv_fwd_pend(const float* x, const float* packed, float* y, int cin, int cout, int h, int w, int nimg,
+                       int dil, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                       const float* x_part, int x_npart, msl_sk_pending* pend) {
+  if (bad_parts(x_part, x_npart) || bad_dims(1, cin, cout, h, w, nimg) || !x || !packed || !y || dil < 1)
+    return MSL_ERR_ARG;
+  return fwd_math(fp16, x, cin, packed, cout, (const float*)nullptr, 0, y, 1, 9, h, w, nimg, dil, 0, counters, ws,
+                  ws_bytes, as_stream(stream), 0, x_part, x_npart, pend);
+}
+
+int msl_dconv_dgrad_pend(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int h, int w,
+                         int nimg, int dil, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                         const float* dy_part, int dy_npart, msl_sk_pending* pend) {
+  if (bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, h, w, nimg) || !dy || !packed_dgrad || !dx || dil < 1)
+    return MSL_ERR_ARG;
+  return fwd_math(fp16, dy, cout, packed_dgrad, cin, (const float*)nullptr, 0, dx, 1, 9, h, w, nimg, dil, 0, counters,
+                  ws, ws_bytes, as_stream(stream), 0, dy_part, dy_npart, pend);
+}
+
+int msl_pconv_fwd_pend(const float* x, const float* packed, float* y, int cin, int cout, int p, int fp16,
+                       int* counters, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                       int x_npart, msl_sk_pending* pend) {
+  if (bad_parts(x_part, x_npart) || bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
+  return fwd_math(fp16, x, cin, packed, cout, (const float*)nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws,
+                  ws_bytes, as_stream(stream), 0, x_part, x_npart, pend);
+}
+
+int msl_pconv_dgrad_pend(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                         int accumulate, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                         const float* dy_part, int dy_npart, msl_sk_pending* pend) {
+  if (bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx)
+    return MSL_ERR_ARG;
+  return fwd_math(fp16, dy, cout, packed_dgrad, cin, (const float*)nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws,
+                  ws_bytes, as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart, pend);
+}
+
+int msl_sk_finish(const msl_sk_pending* pend, float* out, msl_stream_t stream) {
+  if (!pend || !out) return MSL_ERR_ARG;
+  if (!pend->pending) return MSL_OK;
+  if (!pend->part || (pend->bm != 64 && pend->bm != 128) || pend->bn != kSkBN) return MSL_ERR_ARG;
+  FwdArgs a{};
+  a.C = out;
+  a.M = pend->m;
+  a.P = pend->p;
+  a.accum = pend->accum;
+  SkArgs sk{};
+  sk.part = const_cast<float*>(pend->part);
+  sk.tiles_m = pend->tiles_m;
+  sk.tiles_n = pend->tiles_n;
+  sk.KS = pend->ks;
+  sk.NW = pend->nw;
+  sk.T = pend->t;
+  sk.tdp = pend->tdp;
+  const long long tiles = (long long)pend->tiles_m * pend->tiles_n;
+  const dim3 rgrid(pend->bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp)), block(256);
+  hipStream_t st = as_stream(stream);
+  if (pend->bm == 64)
+    hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
+  else
+    hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
 
 // ------------------------------------------------------------------ BF16-MFMA forms
 // Same operands, workspaces and results layout; products in bf16 (RNE from the fp32 operands),
@@ -1253,7 +1356,6 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
 // so packs must be made in the f16x3 fp32 form, the default), one v_mfma_f32_32x32x16_f16 per
 // 16-deep slice, fp32 sums, the result unscaled exactly.  The 64- / 32-row tiles (M <= 64) run
 // exact f32 MFMA.  Partials as in the _sc entry points ((pointer, count), NULL = computed).
-static bool f16_ready() { return g_f32_form == kMathH3P; }
 
 int msl_dconv_fwd_f16(const float* x, const float* packed, const float* bias, float* y, int nbranch, int cin,
                       int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,

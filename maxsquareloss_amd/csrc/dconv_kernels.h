@@ -213,15 +213,7 @@ __device__ __forceinline__ f32x16 mfma_h3(const Split2h& a, const Split2h& b, f3
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.hi, c, 0, 0, 0);
 }
 
-// 2^k with k = clamp(141 - biased exponent of mx, -100, 100): mx * 2^k in [2^14, 2^15) (fp16's
-// largest finite value is 65504); a zero / fp32-subnormal maximum gives 2^100, inf / NaN 2^-100.
-// `inv` = 2^-k.  Powers of two: scaling and unscaling are exact.
-__device__ __forceinline__ float pow2_scale(float mx, float& inv) {
-  const int e = (int)((__float_as_uint(mx) >> 23) & 0xffu);
-  const int k = min(100, max(-100, 141 - e));
-  inv = __uint_as_float((unsigned)(127 - k) << 23);
-  return __uint_as_float((unsigned)(127 + k) << 23);
-}
+// pow2_scale: msl_internal.h
 
 // max over the n absmax partials of one tensor (kNPart from k_absmax, or one per channel from
 // the BN kernels that produced it), by every wave on its own (wave-uniform): float4 loads, four
@@ -1004,23 +996,14 @@ struct SkArgs {
   int nchunk, kchunk;
 };
 
-__device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
 // Tile t of the forward-form stream-K space -> (m-block, n-block), n fastest: consecutive tiles
 // share an m-block, so the 64 workers of one XCD (consecutive ranges) read one or two m-blocks'
 // weights and a contiguous pixel range - their L2 holds the operands.  Layer3 fwd: 66 vs 154 MB
 // fetched per launch with m fastest (FETCH_SIZE x 2), same time; 2048->512 pointwise 121 vs 133
-// us (profiles/r02_sk_tile_order.txt).  MSL_SK_MMAJOR restores m fastest for A/B builds.
+// us (profiles/r02_sk_tile_order.txt).  (SkView in msl_internal.h relies on this order.)
 __device__ __forceinline__ void sk_tile(int t, int tiles_m, int tiles_n, int& tm, int& tn) {
-#ifdef MSL_SK_MMAJOR
-  tm = t % tiles_m;
-  tn = t / tiles_m;
-#else
   tm = t / tiles_n;
   tn = t - tm * tiles_n;
-#endif
-}
-__device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
-  return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
 }
 
 // BD (r03, f16x3 / fp16, 1 x 4 waves, G = 1, STAGES = 4): the image operand skips LDS - each lane

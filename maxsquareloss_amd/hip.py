@@ -99,6 +99,17 @@ SIGNATURES = {
     "msl_maxpool_bwd": (c_int, [c_p, c_p] + [c_int] * 8 + [c_p, c_p]),
     "msl_subsample": (c_int, [c_p] + [c_int] * 6 + [c_p, c_p]),
     "msl_subsample_bwd": (c_int, [c_p] + [c_int] * 6 + [c_p, c_p]),
+    "msl_dconv_fwd_pend": (c_int, [c_p] * 3 + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p]),
+    "msl_dconv_dgrad_pend": (c_int, [c_p] * 3 + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p]),
+    "msl_pconv_fwd_pend": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p]),
+    "msl_pconv_dgrad_pend": (c_int, [c_p] * 3 + [c_int] * 5 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p]),
+    "msl_sk_finish": (c_int, [c_p, c_p, c_p]),
+    "msl_bn_fwd_pend": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_sz, c_p, c_p, c_p]),
+    "msl_bn_bwd_pend": (c_int, [c_p] * 11 + [c_int] * 6 + [c_p, c_sz, c_p, c_p, c_p]),
+    "msl_aspp_weight_layout": (c_int, [c_p, c_ll, c_int, c_int, c_int, c_p, c_p]),
+    "msl_aspp_weight_grad": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p]),
+    "msl_aspp_shift_add": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p]),
+    "msl_aspp_shift_gather": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p]),
     "msl_sgd_block_elems": (c_int, []),
     "msl_sgd_plan": (c_ll, [c_p, c_int, c_p, c_p, c_ll]),
     "msl_sgd_step": (c_int, [c_p, c_p, c_p, c_ll, c_f, c_f, c_f, c_f, c_f, c_p]),
@@ -106,6 +117,13 @@ SIGNATURES = {
 }
 
 ABI_VERSION = 2
+
+
+class SkPending(ctypes.Structure):
+    """msl_sk_pending (include/msl_hip.h): the unfinished output of a stream-K conv GEMM."""
+    _fields_ = [("part", c_p), ("pending", c_int), ("bm", c_int), ("bn", c_int), ("tiles_m", c_int),
+                ("tiles_n", c_int), ("ks", c_int), ("nw", c_int), ("t", c_int), ("tdp", c_int),
+                ("accum", c_int), ("m", c_int), ("p", c_int), ("maxp", c_int)]
 _lib = None
 
 

@@ -27,7 +27,10 @@ ws = [per_launch(write_csv, "WRITE_SIZE", n) for n in names]
 f, nf = sum(v for v, _ in fs), [n for _, n in fs]
 w, nw = sum(v for v, _ in ws), [n for _, n in ws]
 import os  # noqa: E402
-res = {"kernel": kernels, "form": form, "nimg": int(os.environ.get("NIMG", "2")), "launches": [nf, nw], "fetch_size_kib": f, "write_size_kib": w,
+# the map size and image count of the profiled op (scripts/prof_dominant.py: 65 x 129, a pair); bench.py
+# uses the figure only for exactly this kernel set, form and shape
+res = {"kernel": kernels, "form": form, "nimg": int(os.environ.get("NIMG", "2")), "h": int(os.environ.get("PH", "65")),
+       "w": int(os.environ.get("PW", "129")), "launches": [nf, nw], "fetch_size_kib": f, "write_size_kib": w,
        "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024),
        "note": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), gfx950 FETCH_SIZE correction; "
                "per-launch figures of the listed kernels summed"}
