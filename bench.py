@@ -103,7 +103,6 @@ def parse():
                     help="with --pair 0: the target forward runs on a side stream concurrently with the source backward")
     ap.add_argument("--async-wgrad", type=int, default=0,
                     help="1: in-place weight gradients on a side stream beside the data-gradient chain (ops.ASYNC_WGRAD)")
-    ap.add_argument("--variant", type=int, default=0, help="msl_conv_set_variant (kernel-form A/B experiments)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=2, help="0 disables the CPU baseline")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM traffic per launch of the dominant kernel (from a rocprofv3 --pmc run)")
@@ -125,9 +124,6 @@ def main():
     args, _, _ = init_args(build_parser().parse_args(argv))
     ops.set_bn_fused(a.bn_form == "fused")
     ops.ASYNC_WGRAD = bool(a.async_wgrad)
-    if a.variant:
-        from maxsquareloss_amd import hip
-        hip.check(hip.load().msl_conv_set_variant(a.variant), "msl_conv_set_variant")
     tr = UDATrainer(args, cuda=True)
     rank, dev = tr.rank, tr.device
     init_state = {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()} if rank == 0 else None
@@ -194,10 +190,8 @@ def main():
     flops = 2.0 * 256 * 256 * 9 * h3 * w3 * nimg
     achieved = flops / (kern_ms * 1e-3) / 1e12
     form = ops.f32_form() if a.conv_math == "fp32" else a.conv_math
-    # the op the probe timed: the GEMM alone when its stream-K pieces are summed by the BN kernel that
-    # follows it (ops.FOLD, conv -> BN fusion), else the GEMM + its piece-reduce launch
-    folded = ops._fold_math(a.conv_math) is not None
-    kernels = "k_igemm_fwd_sk2" if folded else "k_igemm_fwd_sk2,k_sk_reduce"
+    # the op the probe timed: the stream-K GEMM + its piece-reduce launch
+    kernels = "k_igemm_fwd_sk,k_sk_reduce"
     traffic, rec = None, None
     if os.path.exists(a.pmc):
         try:
@@ -219,11 +213,10 @@ def main():
                 "traffic_source": (os.path.relpath(a.pmc, ROOT) + ": committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                    "passes of this kernel (scripts/gpu_bench_prof.sh), not measured in this run; "
                                    "memory-side bytes incl. Infinity-Cache hits") if traffic is not None else None,
-                "kernel": f"dconv3x3 fwd layer3 d=2 over {nimg} image(s): {kernels} (" + (
-                    "the stream-K pieces of its split tiles are summed by the BN kernel that reads the map, "
-                    "msl_bn_fwd_pend" if folded else "the stream-K GEMM and its piece reduce") +
-                "; the weight planes are split at pack time, once per SGD step; f16x3: the input's absmax "
-                "partials come from the BN kernel that produced it)",
+                "kernel": f"dconv3x3 fwd layer3 d=2 over {nimg} image(s): one op call = the stream-K GEMM "
+                          "k_igemm_fwd_sk(2) + its piece reduce k_sk_reduce (the weight planes are split at pack "
+                          "time, once per SGD step; f16x3: the input's absmax partials come from the BN kernel "
+                          "that produced it)",
                 "form": form, "kernel_ms": round(kern_ms, 4), "launches": len(probes),
                 "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
                 # NOT a utilisation: fp32-equivalent TFLOP/s of the f16x3 / bf16x6 forms (3 / 6 MFMAs per
@@ -277,7 +270,7 @@ def main():
         "data": "synthetic (counter-generated uint8 images -> BGR-mean, uniform labels; random-init weights)",
         "config": {"workload": f"{'SYNTHIA' if C == 16 else 'GTA5'}->Cityscapes {args.target_mode} UDA step "
                                f"(solve_gta5.py), {W}x{H}, bs=1/GPU",
-                   "conv_math": a.conv_math, "bn_form": a.bn_form, "hipgraph": graphed, "pair": bool(a.pair), "overlap": bool(a.overlap), "async_wgrad": bool(a.async_wgrad), "variant": a.variant, "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
+                   "conv_math": a.conv_math, "bn_form": a.bn_form, "hipgraph": graphed, "pair": bool(a.pair), "overlap": bool(a.overlap), "async_wgrad": bool(a.async_wgrad), "f32_form": ops.f32_form() if a.conv_math == "fp32" else None,
                    "target_mode": args.target_mode, "multi": args.multi, "lambda_target": args.lambda_target,
                    "num_classes": C, "global_batch": 2 * world, "parallelism": f"dp{world}"},
         "roofline": roofline, "step_roofline": step_roofline, "cpu_baseline": cpu,

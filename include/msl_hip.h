@@ -72,21 +72,6 @@ int msl_conv_set_pack_form(int form);
  * workgroups, whole rounds of tiles run data-parallel and only the remainder is split stream-K
  * (default); 0 = pure stream-K (every tile range-split over 512 workgroups). */
 int msl_conv_set_sk_hybrid(int on);
-/* Kernel-variant switch for same-box A/B measurements of alternative kernel forms (process-wide,
- * read at launch; identical results up to fp32 summation order): 0 = the default forms; each bit a
- * deviation: bit 0 = the weight gradient's dY fragments prefetched three K-steps ahead (k_wgrad_x6
- * PIPE 1); bit 1 = the 3x3 / ASPP forward-form GEMMs on <= 64-row tiles run their K-steps
- * channel-block-major; bit 2 = the 3x3 f16x3 / fp16 forward-form GEMMs stage the image operand
- * through LDS (the r02 form) instead of loading it straight to registers; bit 3 = the stream-K
- * remainder after data-parallel rounds spread at one K-step per workgroup (the r02 split); bit 4 =
- * the f16x3 3x3 GEMMs with M <= 64 (ASPP forward, layer1) on exact-f32 32 / 64-row tiles; bit 5 =
- * those 64-row f16x3 GEMMs as chunked split-K in channel-block-major K order; bit 6 = the
- * fp16 weight-gradient GEMMs with the image values two stages ahead (PIPE 2); bit 7 flips which f16x3 /
- * fp16 forward-form GEMMs read an image pre-split into fp16 planes by one pass ahead of the GEMM
- * (default: the 3x3 GEMMs with M >= 512).
- * MSL_CONV_VARIANT in the environment sets it when the Python host loads the library.
- * MSL_ERR_ARG for a negative value. */
-int msl_conv_set_variant(int variant);
 
 /* ------------------------------------------------------------------------
  * Dilated 3x3 convolution, stride 1, padding = dilation, as an FP32-MFMA
@@ -244,43 +229,6 @@ int msl_pconv_wgrad_sc(const float* x, const float* dy, float* dw, int cin, int 
                        int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
                        int x_npart, const float* dy_part, int dy_npart);
 
-/* ------------------------------------------------------------------------
- * Conv -> BatchNorm fusion (the 1x1 / 3x3 Bottleneck convs and their BN,
- * deeplab_multi.py:12-46).  The forward-form GEMMs (forward and data gradient) split their
- * (tile, K-step) space over 512 persistent workgroups; a tile that two or more workgroups share is
- * left as pieces that a second launch sums (stream-K).  The _pend entry points below skip that
- * launch and describe the unfinished output instead; the consumer BN kernel sums the pieces while
- * it reads the map (msl_bn_fwd_pend: the conv output, written back once for the backward;
- * msl_bn_bwd_pend: the data gradient arriving at the BN output, never written) with the reduce's
- * exact order, so the results are bit-identical to conv + msl_bn_*.
- * fp16 = 0: the current fp32 form (f16x3 by default); 1: the fp16 MFMA math (msl_*_f16).
- * ---------------------------------------------------------------------- */
-typedef struct msl_sk_pending {
-  const float* part;  /* the pieces, inside the GEMM's workspace (keep it alive until consumed) */
-  int pending;        /* 0: the output is complete; 1: split tiles still need their pieces */
-  int bm, bn, tiles_m, tiles_n;
-  int ks, nw, t, tdp; /* stages per tile, stream-K workers, their iterations, data-parallel tiles */
-  int accum;          /* the GEMM accumulates into its output (old values in the split tiles) */
-  int m, p;           /* output rows and pixels */
-  int maxp;           /* most pieces any split tile has */
-} msl_sk_pending;
-/* The GEMM of msl_dconv_fwd_sc / msl_dconv_dgrad_sc (nbranch = 1, no bias), msl_pconv_fwd_sc and
- * msl_pconv_dgrad_acc_sc (or their _f16 forms), leaving split tiles pending in *pend when pend is not
- * NULL and the form allows it (else complete, pend->pending = 0).  Same workspaces. */
-int msl_dconv_fwd_pend(const float* x, const float* packed, float* y, int cin, int cout, int h, int w, int nimg,
-                       int dil, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
-                       const float* x_part, int x_npart, msl_sk_pending* pend);
-int msl_dconv_dgrad_pend(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int h, int w,
-                         int nimg, int dil, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
-                         const float* dy_part, int dy_npart, msl_sk_pending* pend);
-int msl_pconv_fwd_pend(const float* x, const float* packed, float* y, int cin, int cout, int p, int fp16,
-                       int* counters, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
-                       int x_npart, msl_sk_pending* pend);
-int msl_pconv_dgrad_pend(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                         int accumulate, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
-                         const float* dy_part, int dy_npart, msl_sk_pending* pend);
-/* Completes a pending output on its own (k_sk_reduce): for consumers other than the BN kernels. */
-int msl_sk_finish(const msl_sk_pending* pend, float* out, msl_stream_t stream);
 /* ------------------------------------------------------------------------
  * ASPP heads as a pointwise GEMM plus shifts (csrc/aspp.hip; Classifier_Module.forward,
  * deeplab_multi.py:51-66, 84-85, quirk Q1: branches 0 and 1 with their biases).  With nt = 9*nbranch
@@ -487,22 +435,6 @@ int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const fl
 /* 1 if msl_bn_fwd / msl_bn_bwd run the fused one-block-per-channel kernels for this shape (their
  * _am absmax output is then free; the split forms add a pass over the output). */
 int msl_bn_uses_fused(int c, int p, int training);
-/* Conv -> BN fusion (see msl_sk_pending).  msl_bn_fwd_am where x is the output of a _pend conv GEMM
- * with m = c rows of nimg*p pixels: the split tiles are summed as x is read and written back into
- * x (which must be writable; the backward reads it).  msl_bn_bwd_am_beta where dy is the output of a
- * _pend data-gradient GEMM (dy_pend, its split tiles summed as dy is read; dy itself is not
- * written).  A NULL pending (or pending = 0) is the plain call.  The pending forms need
- * msl_bn_uses_fused(c, p, training) and at most 1024 pixel tiles per row (else MSL_ERR_ARG: complete
- * the output with msl_sk_finish first). */
-int msl_bn_fwd_pend(float* x, const float* gamma, const float* beta, const float* residual, float* y,
-                    float* running_mean, float* running_var, long long* num_batches_tracked, float* save_mean,
-                    float* save_invstd, int c, int p, int nimg, int training, int update_running, float momentum,
-                    float eps, int relu, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax,
-                    const msl_sk_pending* x_pend);
-int msl_bn_bwd_pend(const float* dy, const float* x, const float* y, const float* gamma, const float* beta,
-                    const float* save_mean, const float* save_invstd, float* dx, float* dres, float* dgamma,
-                    float* dbeta, int c, int p, int nimg, int training, int relu, int accumulate_params, void* ws,
-                    size_t ws_bytes, msl_stream_t stream, float* absmax_dx, const msl_sk_pending* dy_pend);
 /* BN kernel form (process-wide): 1 = train-mode layers with p <= 16384 (or p <= 33792 and
  * c >= 128) run one fused statistics+apply launch per call (one block per channel, operands held in registers), 0 =
  * the split statistics / flat-apply launches everywhere.  Returns 0, or MSL_ERR_ARG. */

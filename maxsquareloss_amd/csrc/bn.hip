@@ -104,7 +104,6 @@ struct BnArgs {
   int C, NI, P, S, chunk, relu, training, update_running;  // C channels, NI images, P pixels per image
   float eps, momentum;
   float* absmax;  // [C] max |y| per channel (msl_bn_fwd_am: the next conv's f16x3 partials) or null
-  SkView fold;    // msl_bn_fwd_pend: x = fold.out, its split tiles summed here and written back
 };
 
 // Batch statistics of row r (channel r / NI of image r % NI) from the fp64 partial sums.
@@ -222,7 +221,6 @@ struct BnBwdArgs {
   double* part;
   int C, NI, P, S, chunk, relu, training, accumulate;
   float* absmax;  // [C] max |dx| per channel (msl_bn_bwd_am) or null
-  SkView fold;    // msl_bn_bwd_pend: dy = fold.out, its split tiles summed as it is read
 };
 
 template <bool VEC>
@@ -391,7 +389,7 @@ __global__ void __launch_bounds__(256) k_zero_rows(float* __restrict__ v, int n)
 // The maxima are zeroed by a kernel, not hipMemsetAsync: inside a captured hipGraph (utils/graph.py)
 // the memset node was not ordered against the atomicMax kernel that follows it - replays left stale
 // or garbage maxima (up to 1e38) in the partials, i.e. wrong f16x3 operand scales (r03 pair-mode
-// graph test; scripts/diag_graph_pair.py).  Kernel nodes keep the stream order.
+// graph test).  Kernel nodes keep the stream order.
 int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
   hipLaunchKernelGGL(k_zero_rows, dim3(cdiv(c, 256)), dim3(256), 0, st, absmax, c);
   MSL_CHECK_LAUNCH();
@@ -442,18 +440,10 @@ __device__ __forceinline__ void bn_st(__amdgpu_buffer_rsrc_t r, unsigned voff, i
 }
 constexpr int kBnTwoBlockEpt = 16;  // forms built for two blocks per CU (64 VGPRs)
 
-// FOLD (msl_bn_fwd_pend): x is the unfinished output of a stream-K conv GEMM (SkView); each element
-// of a split tile is summed from its pieces as it is loaded (sk_fold: k_sk_reduce's order) and
-// written back, so the backward reads the same x the unfused path leaves.
-constexpr int kFoldChunk = 3;  // elements whose fold loads are in flight together (per thread)
-
-template <int EPT, int FP = 0>
+template <int EPT>
 __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= kBnTwoBlockEpt ? 8 : 1))) k_bn_fwd_fused(BnArgs a) {
-  constexpr bool FOLD = FP > 0;
   __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
-  FoldTable ft;
-  if constexpr (FOLD) ft.build(a.fold, c);
   float am = 0.f;
   for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
   if (img) __syncthreads();               // red[] is reused
@@ -463,39 +453,12 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
   const unsigned vo = (unsigned)t * 4u;
   const __amdgpu_buffer_rsrc_t rx = bn_row(xc, P);
   float xv[EPT];
-  double shift;
-  if constexpr (FOLD) {
-    unsigned long long spl = 0;  // the elements of split tiles: written back after every load is issued
 #pragma unroll
-    for (int j0 = 0; j0 < EPT; j0 += kFoldChunk) {
-      FoldVal<FP> f[kFoldChunk];
-#pragma unroll
-      for (int q = 0; q < kFoldChunk; ++q) {
-        const int e = (j0 + q) * kBnFusedThreads + t;
-        if (j0 + q < EPT) f[q].issue(ft, a.fold, c, img * P + e, e < P);
-      }
-#pragma unroll
-      for (int q = 0; q < kFoldChunk; ++q)
-        if (j0 + q < EPT) {
-          xv[j0 + q] = f[q].value(a.fold.accum);
-          if (f[q].np) spl |= 1ull << (j0 + q);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < EPT; ++j)
-      if ((spl >> j) & 1) a.fold.out[base + j * kBnFusedThreads + t] = xv[j];
-    __shared__ float sh_shift;
-    if (t == 0) sh_shift = xv[0];
-    __syncthreads();
-    shift = (double)sh_shift;
-  } else {
-#pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      const int e = j * kBnFusedThreads + t;
-      xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
-    }
-    shift = (double)xc[0];
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
   }
+  const double shift = (double)xc[0];
   double s1 = 0.0, s2 = 0.0;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
@@ -556,15 +519,10 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
   }
 }
 
-// FOLD (msl_bn_bwd_pend): dy is the unfinished output of a stream-K data-gradient GEMM, summed as it
-// is loaded (FoldTable).
-template <int EPT, int FP = 0>
+template <int EPT>
 __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= kBnTwoBlockEpt ? 8 : 1))) k_bn_bwd_fused(BnBwdArgs a) {
-  constexpr bool FOLD = FP > 0;
   __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
-  FoldTable ft;
-  if constexpr (FOLD) ft.build(a.fold, c);
   float am = 0.f;
   float dg = 0.f, db = 0.f;  // the parameter gradients, image by image (thread 0)
   for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
@@ -575,29 +533,11 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
   const unsigned vo = (unsigned)t * 4u;
   const __amdgpu_buffer_rsrc_t rdy = bn_row(a.dy + base, P), rx = bn_row(a.x + base, P);
   float g[EPT], xv[EPT];
-  if constexpr (FOLD) {
 #pragma unroll
-    for (int j0 = 0; j0 < EPT; j0 += kFoldChunk) {
-      FoldVal<FP> f[kFoldChunk];
-#pragma unroll
-      for (int q = 0; q < kFoldChunk; ++q) {
-        const int e = (j0 + q) * kBnFusedThreads + t;
-        if (j0 + q < EPT) {
-          f[q].issue(ft, a.fold, c, img * P + e, e < P);
-          xv[j0 + q] = e < P ? bn_ld(rx, vo, j0 + q) : 0.f;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < kFoldChunk; ++q)
-        if (j0 + q < EPT) g[j0 + q] = f[q].value(a.fold.accum);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      const int e = j * kBnFusedThreads + t;
-      g[j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
-      xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
-    }
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    g[j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
+    xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
   }
   const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
   if (a.relu && a.y) {
@@ -706,28 +646,7 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
                   float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
                   int update_running, float momentum, float eps, int relu, void* ws,
                   size_t ws_bytes, msl_stream_t stream, float* absmax) {
-  return msl_bn_fwd_pend(const_cast<float*>(x), gamma, beta, residual, y, running_mean, running_var,
-                         num_batches_tracked, save_mean, save_invstd, c, p, nimg, training, update_running, momentum,
-                         eps, relu, ws, ws_bytes, stream, absmax, nullptr);
-}
-
-// a pending GEMM output that a BN kernel over c channels of nimg images of p pixels can fold
-static bool pend_matches(const msl_sk_pending* pd, int c, int p, int nimg) {
-  return pd->part && pd->m == c && pd->p == p * nimg && (pd->bm == 64 || pd->bm == 128) && pd->bn == kFoldBN &&
-         pd->nw > 0 && pd->t > 0 && pd->tiles_n <= kFoldMaxTilesN && pd->tiles_n * kFoldBN >= pd->p &&
-         (long long)c * p * nimg * 4 < (1LL << 31) && (long long)pd->nw * 2 * pd->bm * kFoldBN * 4 < (1LL << 31) &&
-         pd->maxp >= 2 && pd->maxp <= kFoldMaxPieces;
-}
-
-int msl_bn_fwd_pend(float* x, const float* gamma, const float* beta, const float* residual, float* y,
-                    float* running_mean, float* running_var, long long* num_batches_tracked, float* save_mean,
-                    float* save_invstd, int c, int p, int nimg, int training, int update_running, float momentum,
-                    float eps, int relu, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax,
-                    const msl_sk_pending* x_pend) {
   if (!x || !y || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
-    return MSL_ERR_ARG;
-  const bool fold = x_pend && x_pend->pending;
-  if (fold && !(training && bn_fused_enabled() && bn_fused_shape(c, p) && pend_matches(x_pend, c, p, nimg)))
     return MSL_ERR_ARG;
   if ((!training || update_running) && (!running_mean || !running_var)) return MSL_ERR_ARG;
   hipStream_t st = as_stream(stream);
@@ -767,17 +686,6 @@ int msl_bn_fwd_pend(float* x, const float* gamma, const float* beta, const float
   a.eps = eps;
   a.momentum = momentum;
   a.absmax = absmax;
-  if (fold) {
-    a.fold = sk_view(x_pend, x);
-    if (x_pend->maxp <= 2)
-      return bn_launch_fused(k_bn_fwd_fused<4, 2>, k_bn_fwd_fused<9, 2>, k_bn_fwd_fused<16, 2>, k_bn_fwd_fused<33, 2>,
-                             c, p, st, a);
-    if (x_pend->maxp == 3)
-      return bn_launch_fused(k_bn_fwd_fused<4, 3>, k_bn_fwd_fused<9, 3>, k_bn_fwd_fused<16, 3>, k_bn_fwd_fused<33, 3>,
-                             c, p, st, a);
-    return bn_launch_fused(k_bn_fwd_fused<4, 4>, k_bn_fwd_fused<9, 4>, k_bn_fwd_fused<16, 4>, k_bn_fwd_fused<33, 4>, c,
-                           p, st, a);
-  }
   if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>, c, p, st, a);
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec)
@@ -810,20 +718,9 @@ int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const fl
                        const float* save_mean, const float* save_invstd, float* dx, float* dres,
                        float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
                        int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
-  return msl_bn_bwd_pend(dy, x, y, gamma, beta, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, nimg, training,
-                         relu, accumulate_params, ws, ws_bytes, stream, absmax_dx, nullptr);
-}
-
-int msl_bn_bwd_pend(const float* dy, const float* x, const float* y, const float* gamma, const float* beta,
-                    const float* save_mean, const float* save_invstd, float* dx, float* dres, float* dgamma,
-                    float* dbeta, int c, int p, int nimg, int training, int relu, int accumulate_params, void* ws,
-                    size_t ws_bytes, msl_stream_t stream, float* absmax_dx, const msl_sk_pending* dy_pend) {
   if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
     return MSL_ERR_ARG;
   const bool fused = training && bn_fused_enabled() && bn_fused_shape(c, p);
-  const bool fold = dy_pend && dy_pend->pending;
-  if (fold && !(fused && pend_matches(dy_pend, c, p, nimg))) return MSL_ERR_ARG;
-
   // the mask recompute is the fused kernels' alone, up to 16 elements per lane
   if (relu && !y && !(fused && p <= kBnRemaskMaxEpt * kBnFusedThreads)) return MSL_ERR_ARG;
   if (absmax_dx && !dx) return MSL_ERR_ARG;
@@ -853,17 +750,6 @@ int msl_bn_bwd_pend(const float* dy, const float* x, const float* y, const float
   a.training = training;
   a.accumulate = accumulate_params;
   a.absmax = absmax_dx;
-  if (fold) {
-    a.fold = sk_view(dy_pend, const_cast<float*>(dy));
-    if (dy_pend->maxp <= 2)
-      return bn_launch_fused(k_bn_bwd_fused<4, 2>, k_bn_bwd_fused<9, 2>, k_bn_bwd_fused<16, 2>, k_bn_bwd_fused<33, 2>,
-                             c, p, st, a);
-    if (dy_pend->maxp == 3)
-      return bn_launch_fused(k_bn_bwd_fused<4, 3>, k_bn_bwd_fused<9, 3>, k_bn_bwd_fused<16, 3>, k_bn_bwd_fused<33, 3>,
-                             c, p, st, a);
-    return bn_launch_fused(k_bn_bwd_fused<4, 4>, k_bn_bwd_fused<9, 4>, k_bn_bwd_fused<16, 4>, k_bn_bwd_fused<33, 4>, c,
-                           p, st, a);
-  }
   if (fused)
     return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));

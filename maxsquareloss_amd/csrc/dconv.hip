@@ -271,13 +271,6 @@ static int g_sk_hybrid = 1;
 // 4e-8 vs 6e-8 relative to sum|terms|), kMathH3P the scaled two-way fp16 split (three fp16
 // MFMAs per slice; dconv_kernels.h Split2h).  Process-wide; packs are form-specific.
 static int g_f32_form = kMathH3P;
-// Kernel-variant switch for same-box A/B of alternative kernel forms (msl_conv_set_variant), each bit a
-// deviation from the default forms: bit 0: k_wgrad_x6 with the 3-ahead dY fragment ring; bit 1: the
-// tap-inner K order of the <= 64-row exact-f32 forward tiles; bit 2: the 3x3 f16x3 / fp16 forward
-// form stages B through LDS (the pre-r03 form) instead of loading it to registers (BD); bit 3: the
-// stream-K remainder after data-parallel rounds on one K-step per worker (the pre-r03 split).
-// Bits 0 and 1 measured no faster (profiles/r03_fwd_forms_ab.txt).  Process-wide, read at launch.
-static int g_variant = 0;
 constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
 
 struct FwdPlan {
@@ -327,7 +320,7 @@ static FwdPlan plan_fwd(int nbranch, int taps, int cimg, int M, int P, bool has_
 }
 
 // Weight gradient: stream-K over (tile, 64-pixel stage) (k_wgrad_sk + k_wsk_reduce).  Tiles by
-// shape (scripts/tune_dconv.hip wsk, profiles/): 128x128 at one workgroup per CU for the
+// shape (the r01 tuning harness, profiles/r01_tune_wsk*.txt): 128x128 at one workgroup per CU for the
 // 512-channel layer4 convs, 64x64 at two per CU below, 32-row tiles for the 19-class ASPP.
 struct WgradPlan {
   int bm, bn, nw, tiles_m, tiles_n, ntap, KS, slots;
@@ -373,7 +366,7 @@ static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, boo
     // x6, >= 128 channels: k_wgrad_x6 (dY split once, 16-pixel K-steps, two workgroups per CU),
     // chunked split-K when its items fill the resident slots (layer3 77.6 us, layer4 274,
     // layer2 38.8; stream-K 86.5 / 306 / 44.1; k_wgrad_sk 110 / 395 / 41.0 -
-    // scripts/tune_dconv.hip wx6, profiles/r02_wgrad_x6.txt), else stream-K over 512 workers
+    // profiles/r02_wgrad_x6.txt), else stream-K over 512 workers
     pl.bm = 128; pl.bn = 128; pl.nw = 512;
     pl.rx6 = true;
     pl.lda = pad_to(cout, kPackPad);
@@ -415,28 +408,22 @@ static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)
 // counters, flags or other state survive a call).
 // + (f16x3) the image's kNPart absmax partials at the end of the caller's workspace.
 constexpr size_t kPartBytes = kNPart * sizeof(float);
-// stream-K pieces, then (variant bit 7) the image operand's fp16 planes, then the partials at the end
+// stream-K pieces, then (the BP form) the image operand's fp16 planes, then the partials at the end
 static size_t fwd_piece_bytes(const FwdPlan& pl) {
   // (the <= 64-row f16x3 / fp16 3x3 tiles run 64 rows: room for those pieces whatever the form)
   return align_up((size_t)kSkNW * 2 * std::max(pl.bm, 64) * pl.bn * sizeof(float), 256);
 }
 static size_t img_planes_bytes(int cimg, int P) { return align_up((size_t)cdiv(cimg, kCB) * kCB * P * 4, 256); }
-static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P, int cimg) {
-  if (pl.sk) return fwd_piece_bytes(pl) + img_planes_bytes(cimg, P) + kPartBytes;
+// The f16x3 / fp16 forward-form GEMMs that read their image operand pre-split (k_split_img, BP form):
+// the 3x3 ones with M >= 512 (profiles/r03_bp_ab.txt)
+static bool bp_form(int taps, int M, bool small_f16) { return taps == 9 && M >= 512 && !small_f16; }
+static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P, int cimg, int taps) {
+  // the planes only where the BP form can run (the stem / pointwise calls reserved them too)
+  if (pl.sk) return fwd_piece_bytes(pl) + (bp_form(taps, M, false) ? img_planes_bytes(cimg, P) : 0) + kPartBytes;
   return (pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0) + kPartBytes;
 }
 static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials block from the end
   return reinterpret_cast<float*>((char*)ws + ((ws_bytes - (size_t)k * kPartBytes) & ~(size_t)15));
-}
-
-// most pieces any split tile of a stream-K schedule leaves (workers its iteration range touches)
-static int sk_max_pieces(const SkArgs& sk, long long tiles) {
-  int mx = 1;
-  for (long long tl = 0; tl < tiles - sk.tdp; ++tl) {
-    const int lo = sk_worker_of((int)(tl * sk.KS), sk.T, sk.NW), hi = sk_worker_of((int)((tl + 1) * sk.KS - 1), sk.T, sk.NW);
-    mx = std::max(mx, hi - lo + 1);
-  }
-  return mx;
 }
 
 // The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
@@ -445,7 +432,7 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
                       bool bp = false) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
     if constexpr ((BM == 128 || (BM == 64 && MT == kMathH3P)) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
-      if (bp) {  // the image operand pre-split by k_split_img (variant bit 7)
+      if (bp) {  // the image operand pre-split by k_split_img
         if (accum)
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0, st,
                              a, sk);
@@ -458,7 +445,7 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
       // the pointwise rows keep their two dwordx4 LDS-DMA pieces per wave and K-step (BD loses there:
       // 256 -> 1024 fwd 32.7 vs 31.0 us, 2048 -> 512 82.7 vs 75.1; layer3 3x3 fwd 52.4 vs 55.0,
       // layer4 172 vs 190; profiles/r03_fwd_forms_ab.txt)
-      if (!PW && !(g_variant & 4)) {
+      if (!PW) {
         if (accum)
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a, sk);
         else
@@ -483,12 +470,10 @@ template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int nimg, int dil0,
                            int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st,
-                           int accum = 0, const float* img_part = nullptr, int img_npart = 0,
-                           msl_sk_pending* pend = nullptr) {
+                           int accum = 0, const float* img_part = nullptr, int img_npart = 0) {
   const int P = nimg * h * w;  // nimg images of h x w stacked along the pixel axis
-  if (pend) pend->pending = 0;
   FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
-  // The x6 form runs one K-step per stage, three stages deep (scripts/tune_dconv.hip x6, layer3:
+  // The x6 form runs one K-step per stage, three stages deep (r01 tuning harness, layer3:
   // 87 us vs 115 with two K-steps per stage; f32 is indifferent); its 64- and 32-row tiles stay
   // on exact f32 MFMA (no gain measured there).
   // split forms (and the fp16 math, which reads the f16x3 packs' hi planes): 128-row tiles only
@@ -504,11 +489,10 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   // f16x3 / fp16 (r03): the 3x3 / ASPP GEMMs with M <= 64 (the 19-class ASPP forward, layer1's
   // 64-channel convs) on 64-row tiles of the same kernel (weights from the fp16 planes, the image
   // operand straight to registers) instead of exact-f32 32 / 64-row tiles: 3 fp16 MFMAs per 16-deep
-  // slice at 64 rows cost 2.7x less matrix time than 8 f32 MFMAs at 32 rows.  Variant bit 4 keeps
-  // the exact-f32 tiles.
+  // slice at 64 rows cost 2.7x less matrix time than 8 f32 MFMAs at 32 rows.
   // (r03: also the pointwise / stem GEMMs with M <= 64 - layer1's 256 -> 64 convs, the 64-channel data
   // gradients, the stem's 147 -> 64 - through the same form with one unshifted tap)
-  const bool small_f16 = MT == kMathH3P && pl.sk && pl.bm <= 64 && !(g_variant & 16);
+  const bool small_f16 = MT == kMathH3P && pl.sk && pl.bm <= 64;
   if (small_f16) {
     pl.G = 1;
     pl.bm = 64;
@@ -516,7 +500,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     pl.tiles_m = cdiv(M, 64);
     pl.kps = pl.ksteps;
   }
-  if (ws_bytes < fwd_ws_bytes(pl, M, P, cimg)) return MSL_ERR_WORKSPACE;
+  if (ws_bytes < fwd_ws_bytes(pl, M, P, cimg, taps)) return MSL_ERR_WORKSPACE;
   FwdArgs a{};
   a.Ax6 = nullptr;
   a.ascale = nullptr;
@@ -541,9 +525,6 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   a.kps = pl.kps;
   a.taps = taps;
   a.slab = (long long)M * P;
-  // the exact-f32 (<= 64-row) stream-K tiles of the 3x3 / ASPP convs: channel-block-major K order
-  // (FwdArgs::tapinner; variant bit 1 while it is measured)
-  a.tapinner = (pl.sk && taps == 9 && pl.bm <= 64 && (g_variant & 2)) ? 1 : 0;
   if (pl.sk) {
     if (!counters) return MSL_ERR_ARG;
     if ((long long)pl.tiles_m * pl.tiles_n > kMaxCounters) return MSL_ERR_SHAPE;
@@ -566,58 +547,15 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     // the remainder after data-parallel rounds (e.g. 16 tiles x 16 K-steps of a 256 -> 1024 pointwise
     // GEMM): at one or two K-steps per worker every worker writes a whole 64-KB piece for almost no
     // work; at least kSkMinIt K-steps each (512 -> 2048 fwd 75.9 vs 82.2 us, 2048 -> 512 dgrad 85.6 vs
-    // 90.0; variant bit 3 restores one per worker)
+    // 90.0)
     constexpr long long kSkMinIt = 8;
-    if (sk.tdp > 0 && !(g_variant & 8)) sk.NW = (int)std::max<long long>(1, std::min<long long>(sk.NW, T / kSkMinIt));
+    if (sk.tdp > 0) sk.NW = (int)std::max<long long>(1, std::min<long long>(sk.NW, T / kSkMinIt));
     sk.T = (int)T;
-    sk.nchunk = sk.kchunk = 0;
-    // the small-M f16x3 3x3 GEMMs (ASPP forward, layer1), variant bit 5: chunked split-K,
-    // channel-block-major K (a chunk's weights in each XCD's L2, the taps of one channel block back to
-    // back), chunks sized to fill one round of the 512 resident workgroups.  Measured, not adopted:
-    // ASPP d=6 forward 140.6 vs 131.8 us stream-K, layer1 20.3 vs 21.4 (profiles/r03_fwd_forms_ab.txt)
-    if (small_f16 && (g_variant & 32)) {
-      int nch = 0, kch = 0;
-      double best = 0.0;
-      for (int C = 1; C <= 64 && tiles * C <= 512; ++C) {
-        const int L = cdiv(sk.KS, C);
-        if (L < 16) break;
-        const int Ce = cdiv(sk.KS, L);
-        const double eff = (double)(tiles * Ce) / 512.0;
-        if (eff > best) { best = eff; nch = Ce; kch = L; }
-      }
-      if (nch > 1) {
-        sk.nchunk = nch;
-        sk.kchunk = kch;
-        sk.tdp = 0;
-        sk.NW = (int)(tiles * nch);
-        a.tapinner = 1;
-      }
-    }
     a.C = out;
     a.bias = bias;
-    const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);  // (chunked: NW = items <= 512)
+    const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
     const dim3 rgrid(pl.bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp));
-    bool reduce = T > 0;
-    // conv -> BN fusion (msl_*_pend): the consumer sums the pieces; the f16x3 / fp16 forms, range-split
-    // stream-K, no bias, at most kFoldMaxPieces pieces per tile (the consumer's unrolled sum)
-    const int maxp = (pend && reduce) ? sk_max_pieces(sk, tiles) : 0;
-    if (pend && reduce && F16 && (pl.bm == 128 || small_f16) && sk.nchunk == 0 && !bias && maxp <= kFoldMaxPieces) {
-      reduce = false;
-      pend->maxp = maxp;
-      pend->part = sk.part;
-      pend->pending = 1;
-      pend->bm = pl.bm;
-      pend->bn = kSkBN;
-      pend->tiles_m = sk.tiles_m;
-      pend->tiles_n = sk.tiles_n;
-      pend->ks = sk.KS;
-      pend->nw = sk.NW;
-      pend->t = sk.T;
-      pend->tdp = sk.tdp;
-      pend->accum = accum;
-      pend->m = M;
-      pend->p = P;
-    }
+    const bool reduce = T > 0;
     if (X6L && (pl.bm == 128 || small_f16)) {
       // the x6 kernel stages its weights from the bf16 planes that pack() split once, behind
       // the fp32 part of the same buffer (M > 64 <=> 128-row tiles; f16x3: every M)
@@ -639,8 +577,8 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // the image operand pre-split once for the whole GEMM (BP form, behind the pieces): pays on
         // the layer4 3x3 GEMMs (M = 512: the split pass is shared by 4 row blocks and 9 taps), fwd
         // 162 vs 174 us, dgrad 172 vs 185; loses where the pass is a large share (pointwise 39 vs
-        // 31 us, layer2 34 vs 31, ASPP 144 vs 135) - profiles/r03_bp_ab.txt.  Variant bit 7 flips it.
-        const bool bp = (taps == 9 && M >= 512 && !small_f16) != ((g_variant & 128) != 0);
+        // 31 us, layer2 34 vs 31, ASPP 144 vs 135) - profiles/r03_bp_ab.txt
+        const bool bp = bp_form(taps, M, small_f16);
         if (bp) {
           f16x8* planes = reinterpret_cast<f16x8*>((char*)ws + fwd_piece_bytes(pl));
           const long long n = (long long)a.ncb * 2 * P;
@@ -899,12 +837,7 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
       hipLaunchKernelGGL(k_split_rows<MT>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, ap, an, a.rowscale);
       MSL_CHECK_LAUNCH();
-      if (g_variant & 64)
-        hipLaunchKernelGGL((k_wgrad_x6<MT, 2>), grid, block, 0, st, a);
-      else if (g_variant & 1)
-        hipLaunchKernelGGL((k_wgrad_x6<MT, 1>), grid, block, 0, st, a);
-      else
-        hipLaunchKernelGGL((k_wgrad_x6<MT, 0>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((k_wgrad_x6<MT>), grid, block, 0, st, a);
     } else {
       hipLaunchKernelGGL(k_split_rows<kMathX6>, dim3(pl.lda / 64, cdiv(pl.KS, 4)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, (const float*)nullptr, 0);
@@ -942,8 +875,6 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   return MSL_OK;
 }
 
-static bool f16_ready() { return g_f32_form == kMathH3P; }  // the fp16 math reads the f16x3 packs
-
 template <typename... Args>
 static int fwd_f32(Args... args) {
   if (g_f32_form == kMathH3P) return launch_fwd_form<kMathH3P>(args...);
@@ -954,12 +885,6 @@ template <typename... Args>
 static int wgrad_f32(Args... args) {
   if (g_f32_form == kMathH3P) return launch_wgrad<kMathH3P>(args...);
   return g_f32_form == kMathX6 ? launch_wgrad<kMathX6>(args...) : launch_wgrad<kMathF32>(args...);
-}
-
-template <typename... Args>
-static int fwd_math(int fp16, Args... args) {
-  if (fp16) return f16_ready() ? launch_fwd_form<kMathH1P>(args...) : MSL_ERR_ARG;
-  return fwd_f32(args...);
 }
 
 }  // namespace msl
@@ -979,12 +904,6 @@ int msl_conv_set_f32_form(int form) {
 }
 
 int msl_conv_f32_form(void) { return g_f32_form; }
-
-int msl_conv_set_variant(int v) {
-  if (v < 0) return MSL_ERR_ARG;
-  g_variant = v;
-  return MSL_OK;
-}
 
 int msl_conv_set_sk_hybrid(int on) {
   if (on != 0 && on != 1) return MSL_ERR_ARG;
@@ -1060,8 +979,8 @@ size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w, int
   if (bad_dims(nbranch, cin, cout, h, w, nimg)) return 0;
   const int P = nimg * h * w;
   // large enough with or without a bias (the plan depends on it)
-  return std::max(fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, P, false), cout, P, cin),
-                  fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, P, true), cout, P, cin));
+  return std::max(fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, P, false), cout, P, cin, 9),
+                  fwd_ws_bytes(plan_fwd(nbranch, 9, cin, cout, P, true), cout, P, cin, 9));
 }
 
 int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
@@ -1077,7 +996,7 @@ int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float*
 size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg) {
   if (bad_dims(nbranch, cin, cout, h, w, nimg)) return 0;
   const int P = nimg * h * w;
-  return fwd_ws_bytes(plan_fwd(nbranch, 9, cout, cin, P, false), cin, P, cout);
+  return fwd_ws_bytes(plan_fwd(nbranch, 9, cout, cin, P, false), cin, P, cout, 9);
 }
 
 int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
@@ -1120,7 +1039,7 @@ int msl_pconv_pack(const float* w, int cin, int cout, int for_dgrad, float* pack
 
 size_t msl_pconv_fwd_workspace(int cin, int cout, int p) {
   if (bad_dims(1, cin, cout, 1, p)) return 0;
-  return fwd_ws_bytes(plan_fwd(1, 1, cin, cout, p, false), cout, p, cin);
+  return fwd_ws_bytes(plan_fwd(1, 1, cin, cout, p, false), cout, p, cin, 1);
 }
 
 int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
@@ -1132,7 +1051,7 @@ int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int co
 
 size_t msl_pconv_dgrad_workspace(int cin, int cout, int p) {
   if (bad_dims(1, cin, cout, 1, p)) return 0;
-  return fwd_ws_bytes(plan_fwd(1, 1, cout, cin, p, false), cin, p, cout);
+  return fwd_ws_bytes(plan_fwd(1, 1, cout, cin, p, false), cin, p, cout, 1);
 }
 
 int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
@@ -1232,69 +1151,6 @@ int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cou
                       as_stream(stream));
 }
 
-// ------------------------------------------------------------------ conv -> BN fusion (msl_sk_pending)
-int msl_dconv_fwd_pend(const float* x, const float* packed, float* y, int cin, int cout, int h, int w, int nimg,
-                       int dil, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
-                       const float* x_part, int x_npart, msl_sk_pending* pend) {
-  if (bad_parts(x_part, x_npart) || bad_dims(1, cin, cout, h, w, nimg) || !x || !packed || !y || dil < 1)
-    return MSL_ERR_ARG;
-  return fwd_math(fp16, x, cin, packed, cout, (const float*)nullptr, 0, y, 1, 9, h, w, nimg, dil, 0, counters, ws,
-                  ws_bytes, as_stream(stream), 0, x_part, x_npart, pend);
-}
-
-int msl_dconv_dgrad_pend(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int h, int w,
-                         int nimg, int dil, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
-                         const float* dy_part, int dy_npart, msl_sk_pending* pend) {
-  if (bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, h, w, nimg) || !dy || !packed_dgrad || !dx || dil < 1)
-    return MSL_ERR_ARG;
-  return fwd_math(fp16, dy, cout, packed_dgrad, cin, (const float*)nullptr, 0, dx, 1, 9, h, w, nimg, dil, 0, counters,
-                  ws, ws_bytes, as_stream(stream), 0, dy_part, dy_npart, pend);
-}
-
-int msl_pconv_fwd_pend(const float* x, const float* packed, float* y, int cin, int cout, int p, int fp16,
-                       int* counters, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
-                       int x_npart, msl_sk_pending* pend) {
-  if (bad_parts(x_part, x_npart) || bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return fwd_math(fp16, x, cin, packed, cout, (const float*)nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws,
-                  ws_bytes, as_stream(stream), 0, x_part, x_npart, pend);
-}
-
-int msl_pconv_dgrad_pend(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                         int accumulate, int fp16, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
-                         const float* dy_part, int dy_npart, msl_sk_pending* pend) {
-  if (bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx)
-    return MSL_ERR_ARG;
-  return fwd_math(fp16, dy, cout, packed_dgrad, cin, (const float*)nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws,
-                  ws_bytes, as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart, pend);
-}
-
-int msl_sk_finish(const msl_sk_pending* pend, float* out, msl_stream_t stream) {
-  if (!pend || !out) return MSL_ERR_ARG;
-  if (!pend->pending) return MSL_OK;
-  if (!pend->part || (pend->bm != 64 && pend->bm != 128) || pend->bn != kSkBN) return MSL_ERR_ARG;
-  FwdArgs a{};
-  a.C = out;
-  a.M = pend->m;
-  a.P = pend->p;
-  a.accum = pend->accum;
-  SkArgs sk{};
-  sk.part = const_cast<float*>(pend->part);
-  sk.tiles_m = pend->tiles_m;
-  sk.tiles_n = pend->tiles_n;
-  sk.KS = pend->ks;
-  sk.NW = pend->nw;
-  sk.T = pend->t;
-  sk.tdp = pend->tdp;
-  const long long tiles = (long long)pend->tiles_m * pend->tiles_n;
-  const dim3 rgrid(pend->bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp)), block(256);
-  hipStream_t st = as_stream(stream);
-  if (pend->bm == 64)
-    hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
-  else
-    hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
-  MSL_CHECK_LAUNCH();
-  return MSL_OK;
-}
 
 // ------------------------------------------------------------------ BF16-MFMA forms
 // Same operands, workspaces and results layout; products in bf16 (RNE from the fp32 operands),
@@ -1356,6 +1212,7 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
 // so packs must be made in the f16x3 fp32 form, the default), one v_mfma_f32_32x32x16_f16 per
 // 16-deep slice, fp32 sums, the result unscaled exactly.  The 64- / 32-row tiles (M <= 64) run
 // exact f32 MFMA.  Partials as in the _sc entry points ((pointer, count), NULL = computed).
+static bool f16_ready() { return g_f32_form == kMathH3P; }
 
 int msl_dconv_fwd_f16(const float* x, const float* packed, const float* bias, float* y, int nbranch, int cin,
                       int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,

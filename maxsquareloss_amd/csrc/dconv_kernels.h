@@ -1,5 +1,5 @@
 // Implicit-GEMM kernel templates for the dilated 3x3 conv (design notes in dconv.hip).
-// Shared by libmsl_hip.so (dconv.hip) and the standalone tuning harness (scripts/tune_dconv.hip).
+// Included by dconv.hip (libmsl_hip.so).
 #pragma once
 #include "msl_internal.h"
 
@@ -32,11 +32,6 @@ struct FwdArgs {
   const float* ascale;
   const float* bpart;
   int bnpart;  // partials in bpart
-  // tapinner = 1 (exact-f32 stream-K forms, r03): the K-steps run channel-block-major with the
-  // (branch, tap) index fastest, (cb, z) -> packed K-step z*ncb + cb, so the 9 (or 18) shifted reads
-  // of one 16-channel block follow each other and hit L2, instead of re-streaming the whole image
-  // once per tap (the 19-class ASPP forward moved 1.16 GB per launch for a 69 MB input, r02).
-  int tapinner;
 };
 
 struct WgradArgs {
@@ -85,11 +80,6 @@ __device__ __forceinline__ void mfma_stage_pipe(const float* __restrict__ As, co
   constexpr int KP = BK / 2;
   float av[2][TM], bv[2][TN];
   auto load = [&](int kp, int buf) {
-#ifdef MSL_SK_NOLDS  // tuning-harness experiment only: operands from registers, no LDS reads
-    for (int i = 0; i < TM; ++i) av[buf][i] = __int_as_float(lane + kp + i);
-    for (int j = 0; j < TN; ++j) bv[buf][j] = __int_as_float(lane * 3 + kp + j);
-    return;
-#endif
     const int kr = 2 * kp + kh;
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[buf][i] = As[kr * LDA_S + wm + i * 32 + l32];
@@ -149,7 +139,7 @@ __device__ __forceinline__ void mfma_stage_bf16(const float* __restrict__ As, co
 // accumulated in fp32, smallest first: lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi (a bf16 x
 // bf16 product is exact in fp32).  The dropped terms (mid*lo, lo*mid, lo*lo) and the residuals
 // sit at the 2^-24 level of fp32's own rounding, so the result is fp32-accurate (checked against
-// fp64: scripts/tune_dconv.hip x6).  Six 32x32x16 bf16 MFMAs (6 x 32 cycles) replace eight
+// fp64 by the r01 tuning harness).  Six 32x32x16 bf16 MFMAs (6 x 32 cycles) replace eight
 // 32x32x2 f32 MFMAs (8 x 64 cycles) for one 16-deep K slice.
 struct Split3 {
   bf16x8 hi, mid, lo;
@@ -213,7 +203,15 @@ __device__ __forceinline__ f32x16 mfma_h3(const Split2h& a, const Split2h& b, f3
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.hi, c, 0, 0, 0);
 }
 
-// pow2_scale: msl_internal.h
+// 2^k with k = clamp(141 - biased exponent of mx, -100, 100): mx * 2^k in [2^14, 2^15) (fp16's
+// largest finite value is 65504); a zero / fp32-subnormal maximum gives 2^100, inf / NaN 2^-100.
+// `inv` = 2^-k.  Powers of two: scaling and unscaling are exact.
+__device__ __forceinline__ float pow2_scale(float mx, float& inv) {
+  const int e = (int)((__float_as_uint(mx) >> 23) & 0xffu);
+  const int k = min(100, max(-100, 141 - e));
+  inv = __uint_as_float((unsigned)(127 - k) << 23);
+  return __uint_as_float((unsigned)(127 + k) << 23);
+}
 
 // max over the n absmax partials of one tensor (kNPart from k_absmax, or one per channel from
 // the BN kernels that produced it), by every wave on its own (wave-uniform): float4 loads, four
@@ -988,22 +986,20 @@ struct SkArgs {
   int tiles_m, tiles_n, KS, NW;
   int T;           // stream-K iterations: (tiles - tdp) * KS  (T * NW < 2^31, checked by the planner)
   int tdp;         // leading tiles that run data-parallel (a multiple of the grid size)
-  // chunked split-K (r03, nchunk > 0; tdp = 0): worker w = one (chunk c = w / tiles, tile t = w % tiles)
-  // item, K-steps [c*kchunk, (c+1)*kchunk) of tile t; NW = nchunk * tiles.  Chunk-major items give the
-  // workgroups of one XCD the same K chunk of every tile, so the weights of that chunk stay in its L2
-  // (the 19-class ASPP forward re-read its whole weight pack once per pixel tile).  Every item leaves a
-  // piece (slot 1 for chunk 0, slot 0 otherwise) that k_sk_reduce sums in chunk order.
-  int nchunk, kchunk;
 };
 
+__device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
 // Tile t of the forward-form stream-K space -> (m-block, n-block), n fastest: consecutive tiles
 // share an m-block, so the 64 workers of one XCD (consecutive ranges) read one or two m-blocks'
 // weights and a contiguous pixel range - their L2 holds the operands.  Layer3 fwd: 66 vs 154 MB
 // fetched per launch with m fastest (FETCH_SIZE x 2), same time; 2048->512 pointwise 121 vs 133
-// us (profiles/r02_sk_tile_order.txt).  (SkView in msl_internal.h relies on this order.)
+// us (profiles/r02_sk_tile_order.txt).
 __device__ __forceinline__ void sk_tile(int t, int tiles_m, int tiles_n, int& tm, int& tn) {
   tm = t / tiles_n;
   tn = t - tm * tiles_n;
+}
+__device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
+  return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
 }
 
 // BD (r03, f16x3 / fp16, 1 x 4 waves, G = 1, STAGES = 4): the image operand skips LDS - each lane
@@ -1037,11 +1033,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr int A_INST = APRE ? G * NQL * (BM / 64) : BK / A_ROWS_PER_INST;
   constexpr int A_INST_W = A_INST / 4;
   constexpr int NH = BN / 64;
-#ifdef MSL_SK_FAKEX4
-  constexpr int BG_INST_W = kCB * BN / 256 / 4;
-#else
   constexpr int BG_INST_W = BPRE ? 6 * NH / 4 : PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B DMAs per wave per K-step
-#endif
   static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
   static_assert(!BP || BD, "BP: the BD form with a pre-split image");
   constexpr int INST_W = A_INST_W + G * (BP ? (H1 ? 1 : 2) : BD ? 8 : BG_INST_W);
@@ -1065,14 +1057,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // after data-parallel rounds with fewer stream-K workers than workgroups, the block id, so those
   // workers spread over all XCDs instead of filling the first one
   const int sw = (sk.tdp > 0 && sk.NW < nb) ? b : w;
-  if (sk.nchunk > 0) {
-    if (w < sk.NW) {
-      const int ntl = sk.tiles_m * sk.tiles_n;
-      const int c = w / ntl, t = w - c * ntl;
-      it = t * sk.KS + c * sk.kchunk;
-      it_end = t * sk.KS + min(sk.KS, (c + 1) * sk.kchunk);
-    }
-  } else if (sw < sk.NW) {
+  if (sw < sk.NW) {
     it = sk.tdp * sk.KS + sk_start(sw, sk.T, sk.NW);
     it_end = sk.tdp * sk.KS + sk_start(sw + 1, sk.T, sk.NW);
   }
@@ -1144,15 +1129,9 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     const int pqd = pbd / a.W, pxd = pbd - pqd * a.W, pyd = pqd % a.H;
     {
       const int ks0 = k_a * G;
-      if (a.tapinner) {  // logical K-step = cb * nz + z
-        const int nz = a.ksteps / a.ncb;
-        c_cb = ks0 / nz;
-        c_tap = ks0 - c_cb * nz;
-      } else {
-        const int tq = ks0 / a.ncb;  // branch*taps + tap
-        c_cb = ks0 - tq * a.ncb;
-        c_tap = tq;
-      }
+      const int tq = ks0 / a.ncb;  // branch*taps + tap
+      c_cb = ks0 - tq * a.ncb;
+      c_tap = tq;
     }
     auto set_tap = [&](int tq) {
       const int br = tq / a.taps;
@@ -1174,9 +1153,6 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     set_tap(c_tap);
     float bdq[4][8];  // BD: the register ring of B values (K-step i in slot i % 4)
     auto issue = [&](int s, int slot, float (&bq)[8]) {
-#ifdef MSL_SK_NODMA  // tuning-harness experiment only: no operand traffic
-      return;
-#endif
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
       if constexpr (APRE) {
@@ -1186,26 +1162,8 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
           const int inst = wid * A_INST_W + i;
           const int g = inst / (NQL * (BM / 64)), r = inst % (NQL * (BM / 64));
           const int qh = r / (BM / 64), mb = (r % (BM / 64)) * 64;
-          int ks = s * G + g;
-          if (a.tapinner) {  // logical (cb, z), z fastest -> packed K-step z * ncb + cb
-            const int nz = a.ksteps / a.ncb;
-            const int cbk = ks / nz;
-            ks = (ks - cbk * nz) * a.ncb + cbk;
-          }
+          const int ks = s * G + g;
           dma_b128(rx, As + inst * 256, (unsigned)(((ks * NQ + qh) * a.lda + m0 + mb + lane) * 16));
-        }
-      } else if (a.tapinner) {
-        // logical K-step s*G + g = (cb, z), z fastest; instruction inst covers rows of K-step
-        // g = inst / (A_INST / G) of the stage, at packed K-step z*ncb + cb
-        const int nz = a.ksteps / a.ncb;
-#pragma unroll
-        for (int i = 0; i < A_INST_W; ++i) {
-          const int inst = wid * A_INST_W + i;
-          const int g = inst / (A_INST / G);
-          const int lk = s * G + g;
-          const int cbk = lk / nz, zk = lk - cbk * nz;
-          const unsigned a_base = (unsigned)((zk * a.ncb + cbk) * kCB * a.lda * 4) - (unsigned)(g * kCB * a.lda * 4);
-          dma_b128(ra, As + inst * 256, a_off[i] + a_base);
         }
       } else {
         const unsigned a_base = (unsigned)s * a_stage_bytes;
@@ -1248,12 +1206,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
             const unsigned rowb = (unsigned)((c_cb * 6 + qh) * a.P) * 16u;
             dma_b128(rbx, Bs + g * 24 * BN + (qh * BN + h * 64) * 4, vrow[h] + rowb);
           }
-        } else
-#ifdef MSL_SK_FAKEX4  // tuning-harness experiment only: dwordx4 B loads of unshifted rows (wrong results)
-        if constexpr (true) {
-#else
-        if constexpr (PW) {
-#endif
+        } else if constexpr (PW) {
           // lanes 0-31 -> row 2*inst, lanes 32-63 -> row 2*inst+1; 4 pixels per lane.  A chunk
           // that straddles P reads the next channel's first pixels: they only reach output
           // columns >= P, which are never stored.
@@ -1276,13 +1229,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
             dma_b32(rb, Bs + (g * kCB + r) * BN + h * 64, vrow[h] + cofs);
           }
         }
-        if (a.tapinner) {
-          if (++c_tap * a.ncb == a.ksteps) {
-            c_tap = 0;
-            ++c_cb;
-          }
-          set_tap(c_tap);
-        } else if (++c_cb == a.ncb) {
+        if (++c_cb == a.ncb) {
           c_cb = 0;
           if (++c_tap * a.ncb < a.ksteps) set_tap(c_tap);  // (past the last K-step: nothing to set)
         }
@@ -1385,11 +1332,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
           for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * iA * iB;
     }
     constexpr int PSZ = BM * BN;
-#ifdef MSL_SK_NOFIX  // tuning-harness experiment only: every piece stores as if it were the whole tile
-    if (false) {
-#else
     if (k_a > 0 || k_b < sk.KS) {
-#endif
       // A piece of a split tile: slot 0 = a piece that starts inside the tile (first segment of
       // the range), slot 1 = the tile's head piece (last segment of the range).  Stored row-major
       // [BM][BN] with plain stores (each half-wave writes 128 contiguous bytes per register) and
@@ -1499,10 +1442,8 @@ template <int BM, int BN>
 __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   constexpr int PSZ = BM * BN;
   const int tl = blockIdx.y, t = sk.tdp + tl;  // tile, and its index in the stream-K space
-  const bool chunked = sk.nchunk > 0;
-  const int ntl = sk.tiles_m * sk.tiles_n;
-  const int w_lo = chunked ? 0 : sk_worker_of(tl * sk.KS, sk.T, sk.NW);
-  const int w_hi = chunked ? sk.nchunk - 1 : sk_worker_of((tl + 1) * sk.KS - 1, sk.T, sk.NW);
+  const int w_lo = sk_worker_of(tl * sk.KS, sk.T, sk.NW);
+  const int w_hi = sk_worker_of((tl + 1) * sk.KS - 1, sk.T, sk.NW);
   if (w_lo == w_hi) return;
   int tm, tn;
     sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
@@ -1510,7 +1451,6 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   const float4* __restrict__ part = reinterpret_cast<const float4*>(sk.part);
   for (int g = blockIdx.x * 256 + threadIdx.x; g < PSZ / 4; g += gridDim.x * 256) {
     auto piece = [&](int wc) {
-      if (chunked) return part[(long long)((wc * ntl + tl) * 2 + (wc > 0 ? 0 : 1)) * (PSZ / 4) + g];
       const int slot = sk_start(wc, sk.T, sk.NW) > tl * sk.KS ? 0 : 1;
       return part[(long long)(wc * 2 + slot) * (PSZ / 4) + g];
     };
@@ -2265,10 +2205,7 @@ __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ sr
 // MT = kMathH3P (f16x3): dY (the pre-split operand) as two fp16 planes scaled by k_split_rows<H3>,
 // X scaled by its own pow2_scale (absmax partials bpart) and split into two fp16 planes; the
 // pieces are unscaled by both before they are stored.
-// PIPE = 1 (r03): the dY fragments come from a ring of four register sets, loaded three K-steps
-// ahead of their MFMAs instead of one (one K-step is only 12 MFMAs = ~0.17 us per wave, less than an
-// L2 round trip), the stage loop unrolled by two so every ring slot is a static register set.
-template <int MT = kMathX6, int PIPE = 0>
+template <int MT = kMathX6>
 __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
   constexpr bool H1 = MT == kMathH1P;  // fp16 math: the hi planes only
   constexpr bool H3 = MT == kMathH3P || H1;
@@ -2517,68 +2454,6 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __syncthreads();  // the previous segment's LDS reads are complete in every wave
-    if constexpr (PIPE == 2) {
-      // PIPE 2: the PIPE 1 dY ring, and the X values of stage s + 2 loaded at the start of stage s into
-      // the register set stage s's values left (two sets), so each load has two stages to land
-      u32x4 A2[TM][NP], A3[TM][NP];
-      float rb2[16];
-      unsigned rmb2 = 0;
-      loadB(rbv, rmb);
-      loadA(A0, k_a);
-      if (k_a + 1 < k_b) loadA(A1, k_a + 1);
-      if (k_a + 2 < k_b) loadA(A2, k_a + 2);
-      storeB(0, rbv, rmb);
-      if (nst > 2) loadB(rb2, rmb2);
-      __syncthreads();
-      auto stage = [&](int s, u32x4 (&Ra)[TM][NP], u32x4 (&Rb)[TM][NP], u32x4 (&Rl)[TM][NP], float (&rl)[16],
-                       unsigned& ml, const float (&rs)[16], unsigned ms) {
-        const int left = nst - 2 * s;
-        const int i = k_a + 2 * s;
-        if (left > 4) loadB(rl, ml);  // stage s + 2
-        const char* Bs = smem + (s & 1) * STAGEB;
-        if (i + 3 < k_b) loadA(Rl, i + 3);
-        compute(Bs, Ra);
-        if (left > 1) {
-          if (i + 4 < k_b) loadA(Ra, i + 4);
-          compute(Bs + KVB, Rb);
-        }
-        if (left > 2) storeB((s + 1) & 1, rs, ms);  // stage s + 1
-        __syncthreads();
-      };
-      for (int s = 0; 2 * s < nst; s += 2) {
-        stage(s, A0, A1, A3, rbv, rmb, rb2, rmb2);
-        if (2 * (s + 1) < nst) stage(s + 1, A2, A3, A1, rb2, rmb2, rbv, rmb);
-      }
-    } else if constexpr (PIPE == 1) {
-      u32x4 A2[TM][NP], A3[TM][NP];
-      loadB(rbv, rmb);
-      loadA(A0, k_a);
-      if (k_a + 1 < k_b) loadA(A1, k_a + 1);
-      if (k_a + 2 < k_b) loadA(A2, k_a + 2);
-      storeB(0, rbv, rmb);
-      __syncthreads();
-      // stage s: K-steps k_a + 2s (ring slot 2s % 4) and k_a + 2s + 1; each K-step i first issues the
-      // load of K-step i + 3 into the slot K-step i - 1 freed
-      auto stage = [&](int s, u32x4 (&Ra)[TM][NP], u32x4 (&Rb)[TM][NP], u32x4 (&Rl)[TM][NP]) {
-        const int left = nst - 2 * s;
-        const bool more = left > 2;
-        const int i = k_a + 2 * s;
-        if (more) loadB(rbv, rmb);
-        const char* Bs = smem + (s & 1) * STAGEB;
-        if (i + 3 < k_b) loadA(Rl, i + 3);
-        compute(Bs, Ra);
-        if (left > 1) {
-          if (i + 4 < k_b) loadA(Ra, i + 4);
-          compute(Bs + KVB, Rb);
-        }
-        if (more) storeB((s + 1) & 1, rbv, rmb);
-        __syncthreads();
-      };
-      for (int s = 0; 2 * s < nst; s += 2) {
-        stage(s, A0, A1, A3);
-        if (2 * (s + 1) < nst) stage(s + 1, A2, A3, A1);
-      }
-    } else {
     loadB(rbv, rmb);
     loadA(A0, k_a);
     storeB(0, rbv, rmb);
@@ -2599,7 +2474,6 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       }
       if (more) storeB((s + 1) & 1, rbv, rmb);
       __syncthreads();
-    }
     }
     if (H3 && !a.rowscale) {  // exact: both factors are powers of two (rowscale: in k_wsk_reduce)
 #pragma unroll

@@ -41,8 +41,8 @@ class DilatedConv3x3(nn.Conv2d):
                          dilation=dilation, bias=False)
         self._pack = ops.PackCache()
 
-    def forward(self, x, fold=0):
-        return ops.dconv3x3(x, self.weight, self.dilation[0], self._pack, fold)
+    def forward(self, x):
+        return ops.dconv3x3(x, self.weight, self.dilation[0], self._pack)
 
 
 # Bottleneck blocks with an identity residual let conv1's data-gradient GEMM sum in the residual's
@@ -58,10 +58,10 @@ class PointwiseConv(nn.Conv2d):
         super().__init__(in_channels, out_channels, kernel_size=1, stride=stride, bias=False)
         self._pack = ops.PackCache(pointwise=True)
 
-    def forward(self, x, residual_grad=None, presampled=False, fold=0):
+    def forward(self, x, residual_grad=None, presampled=False):
         if self.stride[0] != 1 and not presampled:
             x = ops.subsample(x, self.stride[0])
-        return ops.pconv(x, self.weight, self._pack, residual_grad, fold)
+        return ops.pconv(x, self.weight, self._pack, residual_grad)
 
 
 class StemConv(nn.Conv2d):
@@ -112,18 +112,13 @@ class Bottleneck(nn.Module):
         hold = ops.ResidualGrad() if fuse else None
         # a strided block (layer2.0): conv1 and the downsample read one shared x[:, :, ::s, ::s]
         xs = ops.subsample(x, self.stride) if self.stride != 1 else x
-        # conv -> BN fusion (ops.FOLD): every conv output goes straight to its BN, which sums the
-        # GEMM's stream-K pieces (fold bit 0); the data gradient of conv2 / conv3 (inputs: bn1 / bn2
-        # outputs, read by nothing else) and of conv1 in an identity block (input: the previous
-        # block's bn3 output, read by conv1 and the detached residual) reaches that BN's backward
-        # unfinished (bit 1).  The downsample's input is shared with conv1: no bit 1 for either.
-        out = ops.bn_act(self.bn1, self.conv1(xs, hold, presampled=True, fold=1 | (2 if fuse else 0)), relu=True)
-        out = ops.bn_act(self.bn2, self.conv2(out, fold=3), relu=True)
+        out = ops.bn_act(self.bn1, self.conv1(xs, hold, presampled=True), relu=True)
+        out = ops.bn_act(self.bn2, self.conv2(out), relu=True)
         residual = x.detach() if fuse else x
         if self.downsample is not None:
-            residual = ops.bn_act(self.downsample[1], self.downsample[0](xs, presampled=True, fold=1))
+            residual = ops.bn_act(self.downsample[1], self.downsample[0](xs, presampled=True))
         # bn3 + residual add + ReLU in one kernel (deeplab_multi.py:38-46)
-        return ops.bn_act(self.bn3, self.conv3(out, fold=3), residual=residual, relu=True, residual_grad=hold)
+        return ops.bn_act(self.bn3, self.conv3(out), residual=residual, relu=True, residual_grad=hold)
 
 
 class Classifier_Module(nn.Module):

@@ -28,7 +28,6 @@ SIGNATURES = {
     "msl_conv_set_f32_form": (c_int, [c_int]),
     "msl_conv_f32_form": (c_int, []),
     "msl_conv_set_sk_hybrid": (c_int, [c_int]),
-    "msl_conv_set_variant": (c_int, [c_int]),
     "msl_conv_set_pack_form": (c_int, [c_int]),
     "msl_dconv_fwd": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_dgrad_workspace": (c_sz, [c_int] * 6),
@@ -99,13 +98,6 @@ SIGNATURES = {
     "msl_maxpool_bwd": (c_int, [c_p, c_p] + [c_int] * 8 + [c_p, c_p]),
     "msl_subsample": (c_int, [c_p] + [c_int] * 6 + [c_p, c_p]),
     "msl_subsample_bwd": (c_int, [c_p] + [c_int] * 6 + [c_p, c_p]),
-    "msl_dconv_fwd_pend": (c_int, [c_p] * 3 + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p]),
-    "msl_dconv_dgrad_pend": (c_int, [c_p] * 3 + [c_int] * 7 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p]),
-    "msl_pconv_fwd_pend": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p]),
-    "msl_pconv_dgrad_pend": (c_int, [c_p] * 3 + [c_int] * 5 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p]),
-    "msl_sk_finish": (c_int, [c_p, c_p, c_p]),
-    "msl_bn_fwd_pend": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_sz, c_p, c_p, c_p]),
-    "msl_bn_bwd_pend": (c_int, [c_p] * 11 + [c_int] * 6 + [c_p, c_sz, c_p, c_p, c_p]),
     "msl_aspp_weight_layout": (c_int, [c_p, c_ll, c_int, c_int, c_int, c_p, c_p]),
     "msl_aspp_weight_grad": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p]),
     "msl_aspp_shift_add": (c_int, [c_p, c_p, c_p] + [c_int] * 7 + [c_p]),
@@ -117,13 +109,6 @@ SIGNATURES = {
 }
 
 ABI_VERSION = 2
-
-
-class SkPending(ctypes.Structure):
-    """msl_sk_pending (include/msl_hip.h): the unfinished output of a stream-K conv GEMM."""
-    _fields_ = [("part", c_p), ("pending", c_int), ("bm", c_int), ("bn", c_int), ("tiles_m", c_int),
-                ("tiles_n", c_int), ("ks", c_int), ("nw", c_int), ("t", c_int), ("tdp", c_int),
-                ("accum", c_int), ("m", c_int), ("p", c_int), ("maxp", c_int)]
 _lib = None
 
 
@@ -154,8 +139,6 @@ def load(require_gpu=True):
     if lib.msl_abi_version() != ABI_VERSION:
         raise MSLError("libmsl_hip.so ABI version mismatch; rebuild it")
     _lib = lib
-    if os.environ.get("MSL_CONV_VARIANT"):  # kernel-form experiments (msl_conv_set_variant) for a whole run
-        check(lib.msl_conv_set_variant(int(os.environ["MSL_CONV_VARIANT"])), "msl_conv_set_variant")
     return lib
 
 

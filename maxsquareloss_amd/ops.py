@@ -9,7 +9,6 @@ out [C][2][H][W], each image convolved, pooled and batch-normalised on its own (
 own bs=1 statistics) while every conv GEMM runs once over both (pair_join /
 pair_split; the trunk ops take either form, the losses one image).
 """
-import ctypes
 from contextlib import nullcontext as _nullctx
 
 import torch
@@ -133,61 +132,9 @@ def _split_gemm(m, k_other):
     return m > 64 or min(m, k_other) >= 128
 
 
-# --------------------------------------------------------------------------- conv -> BN fusion
-# SURVEY.md §8f row 1 (deeplab_multi.py:12-46): a Bottleneck conv's stream-K GEMM leaves the tiles
-# that two workgroups shared as pieces (csrc/dconv_kernels.h), and the BN kernel that reads the conv
-# output (forward) or the data gradient arriving at the BN output (backward) sums them as it reads,
-# in the reduce's own order (include/msl_hip.h msl_sk_pending): one launch and one pass over the map
-# fewer per edge, results bit-identical.
-# The model decides which edges fold (Bottleneck: every conv's output; the data gradients whose
-# tensor has the BN as its only consumer) by passing fold flags; False here turns it off.
-FOLD = True
-
-
-def _fold_math(math):
-    """The fp16 argument of the _pend / _pl entry points for a conv math, None without such forms."""
-    if not FOLD:
-        return None
-    if math == "fp16":
-        return 1
-    if math == "fp32" and _form_code() == F32_FORMS["f16x3"]:
-        return 0
-    return None
-
-
-def _attach_pend(t, pend, ws):
-    """Mark `t` as the unfinished output described by `pend` (its pieces live in `ws`)."""
-    if pend.pending:
-        t._msl_pend = (pend, ws, t._version)
-
-
-def _take_pend(t):
-    """The (pending, workspace) record of an unfinished conv output, removed from `t`; None if complete.
-    Raises if `t` was modified since (e.g. autograd summed a second gradient into it in place: the
-    model marked an edge as foldable whose tensor has another consumer)."""
-    rec = getattr(t, "_msl_pend", None)
-    if rec is None:
-        return None
-    del t._msl_pend
-    if rec[2] != t._version:
-        raise hip.MSLError("a pending stream-K conv output was modified before its BN consumed it "
-                           "(an edge marked foldable has a second consumer)")
-    return rec
-
-
-def finish_pending(t):
-    """Complete an unfinished conv output in place (msl_sk_finish) for a consumer that cannot fold."""
-    rec = _take_pend(t)
-    if rec is not None:
-        hip.check(hip.load().msl_sk_finish(ctypes.byref(rec[0]), t.data_ptr(), hip.stream_ptr()), "msl_sk_finish")
-    return t
-
-
 def _check_act(x, name, images=False):
     """x contiguous; with `images`, (1,C,H,W) or an image batch (1,C,N,H,W) ([C][N][H][W])."""
     ok = x.is_cuda and x.dtype == _f32 and x.size(0) == 1 and (x.dim() == 4 or (images and x.dim() == 5))
-    if getattr(x, "_msl_pend", None) is not None:  # an unfinished conv output reaching a non-folding op
-        finish_pending(x)
     if not ok:
         shapes = "(1,C,H,W) or (1,C,N,H,W)" if images else "(1,C,H,W)"
         raise hip.MSLError(f"{name}: expected a CUDA fp32 tensor of shape {shapes}, got "
@@ -428,7 +375,7 @@ class _DConv3x3(Function):
     """sum_b conv3x3(x, W_b, dilation d_b) (+ sum_b bias_b); nbranch in {1, 2}."""
 
     @staticmethod
-    def forward(ctx, x, w0, w1, b0, b1, dil0, dil1, cache, fold=0):
+    def forward(ctx, x, w0, w1, b0, b1, dil0, dil1, cache):
         x = _check_act(x, "dconv3x3", images=True)
         n = _nimg(x)
         weights = [w0] if w1 is None else [w0, w1]
@@ -451,18 +398,10 @@ class _DConv3x3(Function):
             ev0.record()
         math = CONV_MATH
         xpart = _parts(x, math, compute=_split_gemm(cout, cin))
-        fm = _fold_math(math) if (nb == 1 and bias is None) else None
-        if fold & 1 and fm is not None:  # the output goes to a BN that sums the stream-K pieces
-            pend = hip.SkPending()
-            hip.check(lib.msl_dconv_fwd_pend(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, h, w, n, dil0,
-                                             fm, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
-                                             hip.stream_ptr(), *_pp(xpart), ctypes.byref(pend)), "msl_dconv_fwd_pend")
-            _attach_pend(y, pend, ws)
-        else:
-            hip.check(_conv_call(lib, "msl_dconv_fwd", math,
-                                 (x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb, cin, cout, h, w,
-                                  n, dil0, dil1 if nb > 1 else 0, hip.counters(x.device).data_ptr(), ws.data_ptr(),
-                                  wsb, hip.stream_ptr()), (xpart,)), "msl_dconv_fwd")
+        hip.check(_conv_call(lib, "msl_dconv_fwd", math,
+                             (x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb, cin, cout, h, w, n,
+                              dil0, dil1 if nb > 1 else 0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                              hip.stream_ptr()), (xpart,)), "msl_dconv_fwd")
         if probe is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
@@ -470,7 +409,6 @@ class _DConv3x3(Function):
         ctx.save_for_backward(x, *weights)
         ctx.meta = (nb, cin, cout, h, w, n, dil0, dil1, b0 is not None, cache, math)
         ctx.xpart = xpart
-        ctx.fold_dx = bool(fold & 2) and fm is not None
         return y
 
     @staticmethod
@@ -489,18 +427,10 @@ class _DConv3x3(Function):
             dx = torch.empty_like(x)
             wsb = lib.msl_dconv_dgrad_workspace(nb, cin, cout, h, w, n)
             ws = hip.workspace(wsb, x.device)
-            if ctx.fold_dx:  # dx goes to the BN backward that produced x, which sums the pieces
-                pend = hip.SkPending()
-                hip.check(lib.msl_dconv_dgrad_pend(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, h, w,
-                                                   n, dil0, _fold_math(math), hip.counters(x.device).data_ptr(),
-                                                   ws.data_ptr(), wsb, s, *_pp(gpart), ctypes.byref(pend)),
-                          "msl_dconv_dgrad_pend")
-                _attach_pend(dx, pend, ws)
-            else:
-                hip.check(_conv_call(lib, "msl_dconv_dgrad", math,
-                                     (gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin, cout, h, w, n, dil0,
-                                      d1, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (gpart,)),
-                          "msl_dconv_dgrad")
+            hip.check(_conv_call(lib, "msl_dconv_dgrad", math,
+                                 (gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin, cout, h, w, n, dil0, d1,
+                                  hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (gpart,)),
+                      "msl_dconv_dgrad")
         sink = grad_sink(weights[0]) if (nb == 1 and not has_bias and ctx.needs_input_grad[1]) else None
         wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w, n)
         if sink is not None:
@@ -514,7 +444,7 @@ class _DConv3x3(Function):
             if side is not None:
                 _keep(side, x, gy, *(q[0] for q in (xpart, gpart) if q is not None))
             fg.notify(i)
-            return dx, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None
         ws = hip.workspace(wsb, x.device)
         dw_all = torch.empty((nb, cout, cin, 3, 3), dtype=_f32, device=x.device)
         db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
@@ -525,14 +455,12 @@ class _DConv3x3(Function):
         dw1 = dw_all[1] if nb > 1 else None
         db0 = db_all[0] if has_bias else None
         db1 = db_all[1] if (has_bias and nb > 1) else None
-        return dx, dw0, dw1, db0, db1, None, None, None, None
+        return dx, dw0, dw1, db0, db1, None, None, None
 
 
-def dconv3x3(x, weight, dilation, cache, fold=0):
-    """Stride-1, padding=dilation, bias-free 3x3 conv (Bottleneck.conv2, deeplab_multi.py:17-18).
-    fold: bit 0 = the output goes straight to a BN (ops.bn_act) that sums its stream-K pieces; bit 1 =
-    x is a BN output whose only consumer is this conv, so dx may reach that BN's backward unfinished."""
-    return _DConv3x3.apply(x, weight, None, None, None, int(dilation), 0, cache, int(fold))
+def dconv3x3(x, weight, dilation, cache):
+    """Stride-1, padding=dilation, bias-free 3x3 conv (Bottleneck.conv2, deeplab_multi.py:17-18)."""
+    return _DConv3x3.apply(x, weight, None, None, None, int(dilation), 0, cache)
 
 
 # --------------------------------------------------------------------------- ASPP heads: shift form
@@ -657,7 +585,7 @@ def aspp2(x, w0, b0, w1, b1, dil0, dil1, cache):
     """conv_d6(x) + conv_d12(x) with biases: the live part of Classifier_Module (deeplab_multi.py:62-66)."""
     if ASPP_FORM == "shift":
         return _ASPPShift.apply(x, w0, w1, b0, b1, int(dil0), int(dil1), cache)
-    return _DConv3x3.apply(x, w0, w1, b0, b1, int(dil0), int(dil1), cache, 0)
+    return _DConv3x3.apply(x, w0, w1, b0, b1, int(dil0), int(dil1), cache)
 
 
 # --------------------------------------------------------------------------- pointwise conv
@@ -671,7 +599,7 @@ class _PConv(Function):
     No library GEMM: every call is deterministic (fixed summation order)."""
 
     @staticmethod
-    def forward(ctx, x, weight, cache, hold=None, fold=0):
+    def forward(ctx, x, weight, cache, hold=None):
         x = _check_act(x, "pconv", images=True)
         cout, cin = weight.shape[0], weight.shape[1]
         if weight.shape[2:] != (1, 1) or x.size(1) != cin:
@@ -686,23 +614,14 @@ class _PConv(Function):
         math = CONV_MATH
         # f16x3: x's absmax partials once for the forward and the weight gradient
         xpart = _parts(x, math, compute=_split_gemm(cout, cin))
-        fm = _fold_math(math)
-        if fold & 1 and fm is not None:  # the output goes to a BN that sums the stream-K pieces
-            pend = hip.SkPending()
-            hip.check(lib.msl_pconv_fwd_pend(x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p, fm,
-                                             hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr(),
-                                             *_pp(xpart), ctypes.byref(pend)), "msl_pconv_fwd_pend")
-            _attach_pend(y, pend, ws)
-        else:
-            hip.check(_conv_call(lib, "msl_pconv_fwd", math,
-                                 (x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
-                                  hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()), (xpart,)),
-                      "msl_pconv_fwd")
+        hip.check(_conv_call(lib, "msl_pconv_fwd", math,
+                             (x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
+                              hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()), (xpart,)),
+                  "msl_pconv_fwd")
         ctx.save_for_backward(x, weight)
         ctx.meta = (cin, cout, p, cache, math)
         ctx.xpart = xpart
         ctx.hold = hold
-        ctx.fold_dx = bool(fold & 2) and fm is not None
         return y
 
     @staticmethod
@@ -733,18 +652,12 @@ class _PConv(Function):
                                                    cnt, ws.data_ptr(), wsb, s), "msl_pconv_dgrad")
                 if acc:  # the bf16 form has no accumulate epilogue
                     dx.add_(tgt)
-            elif ctx.fold_dx:  # dx goes to the BN backward that produced x, which sums the pieces
-                pend = hip.SkPending()
-                hip.check(lib.msl_pconv_dgrad_pend(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, acc,
-                                                   _fold_math(math), cnt, ws.data_ptr(), wsb, s, *_pp(gpart),
-                                                   ctypes.byref(pend)), "msl_pconv_dgrad_pend")
-                _attach_pend(dx, pend, ws)
             else:
                 fn = lib.msl_pconv_dgrad_f16 if math == "fp16" else lib.msl_pconv_dgrad_acc_sc
                 hip.check(fn(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, acc, cnt,
                              ws.data_ptr(), wsb, s, *_pp(gpart)), "msl_pconv_dgrad")
         if not ctx.needs_input_grad[1]:
-            return dx, None, None, None, None
+            return dx, None, None, None
         sink = grad_sink(weight)
         dst = sink[0] if sink is not None else torch.empty_like(weight)
         wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
@@ -757,16 +670,16 @@ class _PConv(Function):
         if side is not None:
             _keep(side, x, gy, *(q[0] for q in (ctx.xpart, gpart) if q is not None))
         if sink is None:
-            return dx, dst, None, None, None
+            return dx, dst, None, None
         sink[1].notify(sink[2])
-        return dx, None, None, None, None
+        return dx, None, None, None
 
 
-def pconv(x, weight, cache, residual_grad=None, fold=0):
+def pconv(x, weight, cache, residual_grad=None):
     """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99).
     `residual_grad` (a ResidualGrad also given to the block's bn_act): its gradient is added into
-    this conv's input gradient by the data-gradient GEMM.  `fold`: as dconv3x3's."""
-    return _PConv.apply(x, weight, cache, residual_grad, int(fold))
+    this conv's input gradient by the data-gradient GEMM."""
+    return _PConv.apply(x, weight, cache, residual_grad)
 
 
 conv1x1 = pconv
@@ -1252,7 +1165,6 @@ class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, training, momentum,
                 eps, relu, hold=None):
-        rec = _take_pend(x)  # an unfinished conv output (ops.FOLD): summed by the BN kernel below
         x = _check_act(x, "bn_act", images=True)
         n = _nimg(x)
         c, p = x.size(1), x.size(-2) * x.size(-1)  # p: pixels of one image
@@ -1270,17 +1182,13 @@ class _BNAct(Function):
         # f16x3: the per-channel absmax of y for the convs that read it (their operand scales), where
         # the fused kernel has it in registers; after a split-form BN (stem, 64-channel layer1) a
         # conv that needs it reduces it itself (its first consumer is often an exact-f32 GEMM)
-        fused = bool(lib.msl_bn_uses_fused(c, p, int(bool(training))))
-        am = torch.empty(c, dtype=_f32, device=x.device) if (_h3(CONV_MATH) and fused) else None
-        if rec is not None and not fused:  # the split BN forms read a finished map
-            hip.check(lib.msl_sk_finish(ctypes.byref(rec[0]), x.data_ptr(), hip.stream_ptr()), "msl_sk_finish")
-            rec = None
-        hip.check(lib.msl_bn_fwd_pend(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
-                                      hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
-                                      save_mean.data_ptr(), save_invstd.data_ptr(), c, p, n, int(bool(training)),
-                                      int(update), float(momentum), float(eps), int(bool(relu)), ws.data_ptr(), wsb,
-                                      hip.stream_ptr(), hip.ptr(am), None if rec is None else ctypes.byref(rec[0])),
-                  "msl_bn_fwd")
+        am = torch.empty(c, dtype=_f32, device=x.device) if (
+            _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(bool(training)))) else None
+        hip.check(lib.msl_bn_fwd_am(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
+                                    hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
+                                    save_mean.data_ptr(), save_invstd.data_ptr(), c, p, n, int(bool(training)),
+                                    int(update), float(momentum), float(eps), int(bool(relu)), ws.data_ptr(), wsb,
+                                    hip.stream_ptr(), hip.ptr(am)), "msl_bn_fwd")
         if am is not None:
             _tag_absmax(y, am)
         # ReLU without a residual under the fused kernels (p <= 16384): the backward recomputes the
@@ -1297,7 +1205,6 @@ class _BNAct(Function):
     def backward(ctx, gy):
         x, weight, y, save_mean, save_invstd = ctx.saved_tensors
         c, p, n, training, relu = ctx.meta
-        rec = _take_pend(gy)  # an unfinished data gradient (ops.FOLD): summed by the BN kernel below
         gy = gy.contiguous()
         lib = hip.load()
         nig = ctx.needs_input_grad
@@ -1315,17 +1222,13 @@ class _BNAct(Function):
         wsb = lib.msl_bn_workspace(c, p, n)
         ws = hip.workspace(wsb, x.device)
         # f16x3: the per-channel absmax of dx, the gradient the conv before this BN reads twice
-        fused = bool(lib.msl_bn_uses_fused(c, p, int(training)))
-        am = torch.empty(c, dtype=_f32, device=x.device) if (dx is not None and _h3(CONV_MATH) and fused) else None
-        if rec is not None and not fused:
-            hip.check(lib.msl_sk_finish(ctypes.byref(rec[0]), gy.data_ptr(), hip.stream_ptr()), "msl_sk_finish")
-            rec = None
-        hip.check(lib.msl_bn_bwd_pend(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight),
-                                      hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(),
-                                      hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n,
-                                      int(training), int(relu), int(direct), ws.data_ptr(), wsb,
-                                      hip.stream_ptr(), hip.ptr(am), None if rec is None else ctypes.byref(rec[0])),
-                  "msl_bn_bwd")
+        am = torch.empty(c, dtype=_f32, device=x.device) if (
+            dx is not None and _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(training))) else None
+        hip.check(lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight),
+                                         hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(),
+                                         hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n,
+                                         int(training), int(relu), int(direct), ws.data_ptr(), wsb,
+                                         hip.stream_ptr(), hip.ptr(am)), "msl_bn_bwd")
         if am is not None:
             _tag_absmax(dx, am)
         if direct:

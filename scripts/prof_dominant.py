@@ -28,12 +28,8 @@ cache = ops.PackCache()
 q = ops._parts(x)
 if q is not None:
     ops._tag_absmax(x, q[0])
-# as in the step (ops.FOLD): the GEMM leaves its stream-K pieces for the BN kernel that follows it, so the
-# op is the GEMM launch alone; MSL_PROBE_FOLD=0 times the GEMM + its piece reduce
-fold = int(os.environ.get("MSL_PROBE_FOLD", "1"))
 with torch.no_grad():
     for _ in range(n):
-        y = ops.dconv3x3(x, w, 2, cache, fold)
-    ops.finish_pending(y)
+        y = ops.dconv3x3(x, w, 2, cache)
 torch.cuda.synchronize()
 print("launches", n, "checksum", float(y.double().sum()))

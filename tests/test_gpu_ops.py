@@ -129,6 +129,30 @@ def test_aspp2_fwd_bwd(cin, c, h, w, f32_form):
         assert _rel(a.grad, b.grad) < 1e-5
 
 
+@pytest.mark.parametrize("cin,c,h,w,n,d0,d1", [(2048, 19, 65, 129, 2, 6, 12), (1024, 16, 96, 161, 2, 6, 12),
+                                              (256, 19, 9, 17, 1, 6, 12), (128, 5, 13, 7, 2, 2, 5)])
+def test_aspp_shift_form_matches_direct(cin, c, h, w, n, d0, d1, monkeypatch):
+    """The r04 shift form of the heads (one pointwise GEMM with 18*C rows, then shifts: csrc/aspp.hip)
+    against the two-branch implicit GEMM (ASPP_FORM = "direct") on pairs and single images, incl. maps
+    narrower / shorter than the dilation (every tap of some pixels falls outside its image)."""
+    g = torch.Generator().manual_seed(cin + c + h)
+    shape = (1, cin, n, h, w) if n > 1 else (1, cin, h, w)
+    x = torch.randn(shape, generator=g).to(DEV)
+    ws = [(torch.randn(c, cin, 3, 3, generator=g) * 0.01).to(DEV) for _ in range(2)]
+    bs = [torch.randn(c, generator=g).to(DEV) for _ in range(2)]
+    gy = torch.randn((1, c) + shape[2:], generator=g).to(DEV)
+    res = []
+    for form in ("direct", "shift"):
+        monkeypatch.setattr(ops, "ASPP_FORM", form)
+        leaves = [t.clone().requires_grad_() for t in (x, ws[0], bs[0], ws[1], bs[1])]
+        y = ops.aspp2(*leaves, d0, d1, ops.PackCache())
+        y.backward(gy)
+        torch.cuda.synchronize()
+        res.append([y.detach()] + [t.grad for t in leaves])
+    for i, (a, b) in enumerate(zip(*res)):
+        assert _rel(a, b) < 1e-5, i
+
+
 @pytest.mark.parametrize("c,hi,wi,ho,wo", [(19, 65, 129, 512, 1024), (19, 33, 65, 256, 512), (16, 81, 161, 640, 1280), (3, 5, 7, 11, 13)])
 def test_upsample(c, hi, wi, ho, wo):
     g = torch.Generator().manual_seed(hi)

@@ -9,11 +9,10 @@ Tolerances: one forward/backward of the same network from the same state, so the
 differ only by fp32 rounding of the loss arithmetic (torch softmax vs the fused kernel): losses
 1e-5 relative, the guidance CE with up to two pixels' share on top (a pixel whose max probability
 sits within rounding of the 0.2 threshold can land on either side of it); the IW class histogram (argmax of the two paths' probabilities - torch's softmax
-vs the kernel's) within 0.05 % of the pixels; the parameter gradients per tensor within 4x the
-distance between two runs of the fused path itself, or 1e-4 of the tensor's norm.  (MIOpen's
-stride-2 1x1 data gradients in layer2 block 0 are not bit-reproducible (~2e-7), and the bs=1 BN
-backward amplifies that into up to a few % of the early layers' BN-parameter gradients from one
-run to the next: scripts/diag_nondet.py; the first two passes warm MIOpen's solver choice up.)
+vs the kernel's) within 0.05 % of the pixels; the parameter gradients per tensor within 1e-4 of
+the tensor's norm: the rounding of the loss arithmetic carried through one backward.  The fused path
+itself is bit-reproducible (no library kernel is left on the step since r03: two runs give identical
+gradients, asserted here), so the bar needs no run-to-run allowance.
 """
 import pytest
 import torch
@@ -73,10 +72,7 @@ def _grads(model):
 def test_reference_train_target_through_drop_in_modules(mode):
     tr = _trainer(mode)
     xt = synthetic_image(H, W, 321).cuda()
-    for _ in range(2):  # warm MIOpen's solver choice up
-        tr.optimizer.zero_grad()
-        tr.train_target(tr.model(xt))
-    # the package's fused path, twice (its own run-to-run spread)
+    # the package's fused path, twice (bit-reproducible)
     tr.optimizer.zero_grad()
     tr.train_target(tr.model(xt))
     fused = (tr.loss_target.detach().clone(), tr.loss_target_2.detach().clone())
@@ -97,8 +93,9 @@ def test_reference_train_target_through_drop_in_modules(mode):
     assert abs(fused[1].item() - ref[1].item()) <= 1e-5 * abs(ref[1].item()) + 2 * ref[3], (mode, fused, ref)
     assert len(g_fused) == len(g_ref) == len(g_fused2)
     for i, (a, a2, b) in enumerate(zip(g_fused, g_fused2, g_ref)):
-        err, spread = (a - b).norm().item(), (a - a2).norm().item()
-        assert err <= max(4 * spread, 1e-4 * b.norm().item()), (mode, i, err, spread, b.norm().item())
+        assert torch.equal(a, a2), (mode, i)
+        err = (a - b).norm().item()
+        assert err <= 1e-4 * b.norm().item(), (mode, i, err, b.norm().item())
     if hist_fused is not None:
         d = (hist_fused.long() - tr.target_loss.last_hist.long()).abs().sum().item()
         assert d <= 2 * 0.0005 * H * W, (hist_fused, tr.target_loss.last_hist)
