@@ -279,7 +279,8 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
  * time, as the hi planes of the f16x3 packs, so the packs must be made in the f16x3 fp32 form
  * (msl_conv_set_f32_form(5), the default; MSL_ERR_ARG otherwise) - then one
  * v_mfma_f32_32x32x16_f16 per 16-deep K slice with fp32 accumulation, the result unscaled
- * exactly.  GEMMs with M <= 64 (64- / 32-row tiles) run exact f32 MFMA.  Operand partials as in
+ * exactly (M <= 64: 64-row fp16 tiles, r04; the weight gradients with fewer than 128 channels on either
+ * side keep exact f32 MFMA tiles).  Operand partials as in
  * the _sc entry points ((pointer, count), NULL = computed); msl_pconv_dgrad_f16 carries the
  * accumulate flag of msl_pconv_dgrad_acc.  Same workspaces and results layout.
  * ---------------------------------------------------------------------- */

@@ -431,7 +431,7 @@ template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk,
                       bool bp = false) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
-    if constexpr ((BM == 128 || (BM == 64 && MT == kMathH3P)) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
+    if constexpr ((BM == 128 || BM == 64) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
       if (bp) {  // the image operand pre-split by k_split_img
         if (accum)
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0, st,
@@ -492,7 +492,8 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   // slice at 64 rows cost 2.7x less matrix time than 8 f32 MFMAs at 32 rows.
   // (r03: also the pointwise / stem GEMMs with M <= 64 - layer1's 256 -> 64 convs, the 64-channel data
   // gradients, the stem's 147 -> 64 - through the same form with one unshifted tap)
-  const bool small_f16 = MT == kMathH3P && pl.sk && pl.bm <= 64;
+  // r04: the fp16 math too (its single fp16 plane split into half-wave A pieces, fwd_sk_body AHALF)
+  const bool small_f16 = F16 && pl.sk && pl.bm <= 64;
   if (small_f16) {
     pl.G = 1;
     pl.bm = 64;
@@ -596,10 +597,8 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // waves 1 x 4 (each 128 rows x 32 pixels): every wave splits only its own B columns
         // (2 x 2 waves split each column twice); step 40.5 vs 40.9 ms on one box
         // (profiles/r02_f16x3_waves.txt)
-        if constexpr (MT == kMathH3P) {
-          if (small_f16) launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp);
-        }
         if (small_f16) {
+          launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp);
         } else if (taps == 1 && dil0 == 0)
           launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
         else

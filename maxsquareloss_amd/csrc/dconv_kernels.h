@@ -1031,13 +1031,17 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr int STAGE = A_STAGE + (BD ? 0 : BPRE ? G * 24 * BN : BK * BN);
   constexpr int A_ROWS_PER_INST = 256 / BM;
   constexpr int A_INST = APRE ? G * NQL * (BM / 64) : BK / A_ROWS_PER_INST;
-  constexpr int A_INST_W = A_INST / 4;
+  // fp16 math on 64-row tiles (r04): a K-step's A is one plane's two 1-KB pieces; each wave issues
+  // half a piece (its lane half of the 64 rows), so every wave still issues one A instruction
+  constexpr bool AHALF = APRE && A_INST == 2;
+  constexpr int A_INST_W = AHALF ? 1 : A_INST / 4;
   constexpr int NH = BN / 64;
   constexpr int BG_INST_W = BPRE ? 6 * NH / 4 : PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B DMAs per wave per K-step
   static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
   static_assert(!BP || BD, "BP: the BD form with a pre-split image");
   constexpr int INST_W = A_INST_W + G * (BP ? (H1 ? 1 : 2) : BD ? 8 : BG_INST_W);
-  static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
+  static_assert(AHALF || A_INST % 4 == 0, "A instructions split evenly over waves");
+  static_assert(!AHALF || (G == 1 && BM == 64), "half-wave A pieces: one K-step of 64 rows per stage");
   static_assert((STAGES - 2) * INST_W < 64, "vmcnt range");
   // ONE __shared__ object: a second one (even a 4-byte flag) makes hipcc emit vmcnt(0) before the
   // first ds_read after every DMA issue, which drains the in-flight stage (cdna_hip_programming.md
@@ -1073,6 +1077,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       (int)min(0x7fffffffLL, (long long)a.ncb * (BP ? (H1 ? 2 : 4) : 6) * a.P * 16), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
   const unsigned chan_bytes = (unsigned)a.P * 4u;
+  const bool cfull = (a.cimg % kCB) == 0;  // every 16-channel block of the image operand is full
   // f16x3: B's scale from its absmax partials, A's from the pack; the result is unscaled by both
   float sB = 1.f, iA = 1.f, iB = 1.f;
   if constexpr (H3) {
@@ -1124,11 +1129,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     // offsets (OOB outside the image) are recomputed only when the tap changes.
     int c_cb, c_tap = -1;
     unsigned vrow[NH];
-    unsigned vbd = OOB;  // BD: this lane's shifted pixel byte offset (OOB outside the image)
+    unsigned vbd = OOB;   // BD: this lane's shifted pixel byte offset (OOB outside the image)
+    unsigned vbdh = OOB;  // BD, full channel blocks: + the lane's channel half (8 * (lane >> 5) rows)
     const int pbd = n0 + wn + (lane & 31);
     const int pqd = pbd / a.W, pxd = pbd - pqd * a.W, pyd = pqd % a.H;
     {
-      const int ks0 = k_a * G;
+      // wave-uniform: the cursor lives in scalar registers (it feeds the scalar channel offsets)
+      const int ks0 = __builtin_amdgcn_readfirstlane(k_a * G);
       const int tq = ks0 / a.ncb;  // branch*taps + tap
       c_cb = ks0 - tq * a.ncb;
       c_tap = tq;
@@ -1142,6 +1149,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       if constexpr (BD) {
         const bool v = pbd < a.P && (unsigned)(pyd + dh) < (unsigned)a.H && (unsigned)(pxd + dw) < (unsigned)a.W;
         vbd = v ? (unsigned)((pbd + shift) * (BP ? 16 : 4)) : OOB;
+        vbdh = v ? vbd + (unsigned)(8 * (lane >> 5)) * chan_bytes : OOB;
       } else {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
@@ -1155,7 +1163,12 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     auto issue = [&](int s, int slot, float (&bq)[8]) {
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
-      if constexpr (APRE) {
+      if constexpr (AHALF) {
+        // piece wid / 2 (= the k half of plane 0), rows 32 * (wid & 1) .. +31: the lanes of that half
+        const int qh = wid >> 1;
+        if ((lane >> 5) == (wid & 1))
+          dma_b128(rx, As + qh * 256, (unsigned)(((s * NQ + qh) * a.lda + m0 + lane) * 16));
+      } else if constexpr (APRE) {
         // piece inst = (g, plane*2 + half, 64-row block): planes row ((ks*NP+q)*2+h)*lda + m
 #pragma unroll
         for (int i = 0; i < A_INST_W; ++i) {
@@ -1189,13 +1202,24 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
             for (int j = 0; j < 4; ++j) bq[4 * q + j] = c.f[j];
           }
         } else if constexpr (BD) {
-          // channels cb16 + 8h + j of this lane's pixel; a channel past cimg reads 0 (OOB offset;
-          // OOB + c * P * 4 stays >= 2^31 since cimg * P * 4 < 2^31)
-          const int ci0 = cb16 + 8 * (lane >> 5);
+          // channels cb16 + 8h + j of this lane's pixel
+          if (cfull) {
+            // every channel block full (cimg % 16 == 0): the channel offset is wave-uniform, so it
+            // rides in the scalar soffset and the eight loads share one address VGPR (r04: the
+            // per-channel bound check cost ~32 VALU per K-step); an out-of-image pixel's voffset
+            // >= 2^31 is out of range whatever the soffset
+            const unsigned sb = (unsigned)__builtin_amdgcn_readfirstlane(cb16) * chan_bytes;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const unsigned off = ci0 + j < a.cimg ? vbd + (unsigned)(ci0 + j) * chan_bytes : OOB;
-            bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0));
+            for (int j = 0; j < 8; ++j)
+              bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vbdh, (int)(sb + j * chan_bytes), 0));
+          } else {
+            // a channel past cimg reads 0 (OOB offset; OOB + c * P * 4 stays >= 2^31 since cimg * P * 4 < 2^31)
+            const int ci0 = cb16 + 8 * (lane >> 5);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const unsigned off = ci0 + j < a.cimg ? vbd + (unsigned)(ci0 + j) * chan_bytes : OOB;
+              bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0));
+            }
           }
         } else if constexpr (BPRE) {
           // piece (plane*2 + k half, 64-pixel half): lane = pixel, 16 B = 8 channels of a plane

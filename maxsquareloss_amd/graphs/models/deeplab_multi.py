@@ -185,6 +185,17 @@ class ResNetMulti(nn.Module):
     def _make_pred_layer(self, block, inplanes, dilation_series, padding_series, num_classes):
         return block(inplanes, dilation_series, padding_series, num_classes)
 
+    # with keep_split, _heads leaves layer3's output in split_out: the point where a data-parallel step
+    # splits its backward in two (utils/graph.py: the gradients of layer4 and the heads are exchanged
+    # while the backward through layer3 .. the stem runs)
+    keep_split = False
+    split_out = None
+
+    def split_params(self):
+        """The trainable parameters whose gradients are final once the backward has reached layer3's
+        output: layer4 and both heads."""
+        return [p for m in (self.layer4, self.layer5, self.layer6) for p in m.parameters() if p.requires_grad]
+
     def _heads(self, x):
         """The trunk and both heads on (1,3,H,W) or an image batch (1,3,N,H,W): (layer6, layer5)
         low-resolution logits."""
@@ -192,6 +203,8 @@ class ResNetMulti(nn.Module):
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)
+        if self.keep_split:
+            self.split_out = x
         x1 = self.layer5(x)
         x2 = self.layer4(x)
         x2 = self.layer6(x2)

@@ -11,7 +11,9 @@ import os
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmsl_hip.so")
+# MSL_LIB_PATH: another build of the same library (same-box A/B of kernel changes, scripts/bench_ops.py)
+LIB_PATH = os.environ.get("MSL_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                          "libmsl_hip.so")
 
 c_int, c_ll, c_sz, c_f, c_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p
 

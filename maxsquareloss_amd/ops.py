@@ -731,10 +731,9 @@ class _StemConv(Function):
         y = _like(x, cout, ho, wo)
         wsb = lib.msl_pconv_fwd_workspace(kk, cout, p)
         ws = hip.workspace(wsb, x.device)
-        # the bf16 conv math keeps the stem (the raw image, values ~1e2) in fp32: 8 significant bits
-        # there cost 3-4 % of the target loss after one update; the fp16 math's 64-row GEMMs are exact
-        # fp32 anyway (msl_*_f16)
-        math = "fp32" if CONV_MATH == "bf16" else CONV_MATH
+        # the bf16 / fp16 conv maths keep the stem (the raw image, values ~1e2; 2.5 GFLOP per image) in
+        # the fp32 form: 8 significant bits there cost 3-4 % of the target loss after one update
+        math = "fp32" if CONV_MATH in ("bf16", "fp16") else CONV_MATH
         cpart = _parts(col, math, compute=_split_gemm(cout, kk))
         hip.check(_conv_call(lib, "msl_pconv_fwd", math,
                              (col.data_ptr(), packed.data_ptr(), y.data_ptr(), kk, cout, p,

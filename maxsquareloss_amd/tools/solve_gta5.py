@@ -125,6 +125,14 @@ class UDATrainer(Trainer):
             if self._graphed is None:
                 if self.reducer is None:
                     self._graphed = GraphedStep(self, self._uda_body)
+                elif self.pair and x_s.shape == x_t.shape and self._split_ok():
+                    # the backward captured in two segments split at layer3's output: the gradients of
+                    # layer4 and the heads are exchanged while the rest of the backward replays
+                    n_early = len(self.model.split_params())
+                    self._graphed = GraphedStep(
+                        self, self._uda_grads, update=self._uda_update,
+                        segments=[self._uda_grads_head, self._uda_grads_trunk],
+                        between=[lambda: self.reducer.reduce_early(n_early), self.reducer.reduce_rest])
                 else:
                     self._graphed = GraphedStep(self, self._uda_grads, exchange=self.reducer.reduce_all,
                                                 update=self._uda_update)
@@ -134,6 +142,13 @@ class UDATrainer(Trainer):
         self.current_iter += 1
 
     def _uda_grads(self, x_s, y_s, x_t):
+        if self.pair and x_s.shape != x_t.shape and not getattr(self, "_pair_warned", False):
+            #  --pair needs equal source and target crops; say so once instead of silently
+            # running the two-pass step (bench.py's pair-mode step time applies to equal crops only)
+            import warnings
+            warnings.warn(f"--pair: source {tuple(x_s.shape)} and target {tuple(x_t.shape)} crops differ; "
+                          "running the two-pass step", RuntimeWarning)
+            self._pair_warned = True
         if self.pair and x_s.shape == x_t.shape:
             # one image pair through the network, one backward pass for both objectives
             pred_s, pred_t = self.model.forward_pair(x_s, x_t)
@@ -175,6 +190,38 @@ class UDATrainer(Trainer):
             self.train_target(pred_t)
         main.wait_stream(side)
         ops.wgrad_join(self.device)  # the side-stream weight gradients (ops.ASYNC_WGRAD) rejoin
+
+    def _split_ok(self):
+        """Whether the parameters finished at layer3's output lead the flat gradient buffer (its
+        backward order), so reduce_early's buckets hold final gradients only."""
+        early = {id(p) for p in self.model.split_params()}
+        first = self.optimizer.grads.params[:len(early)]
+        return len(early) > 0 and {id(p) for p in first} == early
+
+    def _uda_grads_head(self, x_s, y_s, x_t):
+        """The pair's forward and the backward through the heads and layer4, stopping at layer3's
+        output (its gradient kept for _uda_grads_trunk): the first segment of a captured data-parallel
+        step (utils/graph.py).  The two segments run exactly the kernels of _uda_grads, in its order."""
+        m = self.model
+        m.keep_split = True
+        try:
+            pred_s, pred_t = m.forward_pair(x_s, x_t)
+        finally:
+            m.keep_split = False
+        x3, m.split_out = m.split_out, None
+        loss_s = self.source_loss(pred_s, y_s)
+        loss_t = self.target_loss_total(pred_t)
+        self.reducer.prepare_for_backward()
+        torch.autograd.backward([loss_s, loss_t], inputs=[x3] + m.split_params())
+        ops.wgrad_join(self.device)
+        self._split = x3
+
+    def _uda_grads_trunk(self):
+        """The rest of the backward: from layer3's output through layer3 .. the stem."""
+        x3, self._split = self._split, None
+        g, x3.grad = x3.grad, None
+        torch.autograd.backward([x3], [g])
+        ops.wgrad_join(self.device)
 
     def _uda_update(self):
         self.optimizer.step()

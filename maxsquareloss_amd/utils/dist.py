@@ -22,11 +22,14 @@ Dead parameters (Q1: ASPP branches d=18/24, or layer5 when --multi False)
 never fire a hook; they are discovered on the first iteration and excluded.
 
 Captured steps (utils/graph.py, --graph): the bucket countdown is host-driven, so a replayed graph
-cannot launch collectives from inside the backward.  There the reducer is `deferred` while the two
-forward/backward passes are captured (no hook launches anything), and between the replay of that
-graph and the replay of the SGD graph `reduce_all()` all-reduces every live bucket back to back on
-RCCL's stream (one exchange of 174 MB, ~1 ms over xGMI at 8 ranks, not overlapped) - the host
-enqueues three things per iteration instead of ~1,600 kernels.
+cannot launch collectives from inside the backward.  There the reducer is `deferred` while the
+iteration is captured (no hook launches anything) and the backward is captured as two graphs, split at
+layer3's output (r04): the first (forward + the backward through the heads and layer4) leaves the
+gradients of the first `n_early` parameters in backward order final, `reduce_early()` all-reduces the
+buckets made of those alone on RCCL's stream while the second graph (the backward through layer3 ..
+the stem) replays on the compute stream, and `reduce_rest()` launches the remaining buckets and joins
+the exchange before the SGD graph.  Without a split (two-pass mode) `reduce_all()` exchanges every
+bucket after the backward.
 """
 import numpy as np
 import torch
@@ -117,6 +120,28 @@ class GradReducer:
             w.wait()
         self.works = []
         self.armed = False
+
+    def reduce_early(self, n_early):
+        """Launch (asynchronously, on RCCL's stream) every live bucket made only of the first `n_early`
+        parameters in backward order - final after the first segment of a split backward."""
+        if self.live is None:
+            raise RuntimeError("GradReducer.reduce_early before the live set is known (run one eager step)")
+        self.works = []
+        self.next = 0
+        while self.next < len(self.bounds) and self.bounds[self.next][1] <= n_early:
+            if self.has_live[self.next]:
+                self._launch(self.next)
+            self.next += 1
+
+    def reduce_rest(self):
+        """Launch the buckets reduce_early left and make the current stream wait for every bucket."""
+        for b in range(self.next, len(self.bounds)):
+            if self.has_live[b]:
+                self._launch(b)
+        self.next = len(self.bounds)
+        for w in self.works:
+            w.wait()
+        self.works = []
 
     def reduce_all(self):
         """All-reduce every live bucket now (a replayed step: the backward ran inside a graph) and

@@ -17,22 +17,29 @@ iteration:
     parameter changed eagerly between replays (load_checkpoint, an in-place edit) shows as a new
     version, and the packs are then rebuilt eagerly before the next replay reads them;
   - loss scalars / meters are the captured tensors, rewritten in place by every replay.
-Data-parallel runs (a GradReducer, whose bucket countdown is host-driven) capture two graphs: the
-forward/backward passes (`body`, the reducer deferred) and the update (`update`: SGD, zero_grad,
-packs); each iteration replays the first, runs `exchange` (the reducer's all-reduce of every live
-bucket, eager, on RCCL's stream), then replays the second.  Those captures use the thread-local
-capture mode, so RCCL's / gloo's own threads may keep calling the HIP runtime meanwhile.
+Data-parallel runs (a GradReducer, whose bucket countdown is host-driven) capture the
+forward/backward passes (the reducer deferred) and the update (`update`: SGD, zero_grad, packs) as
+separate graphs.  The passes may be captured as several consecutive `segments` (r04, pair mode: the
+backward split at layer3's output) with a host call after each (`between`): each iteration replays
+segment 1, launches the exchange of the gradients it finished on RCCL's stream, replays segment 2
+meanwhile, launches the rest and joins it, then replays the update.  Those captures use the
+thread-local capture mode, so RCCL's / gloo's own threads may keep calling the HIP runtime meanwhile.
 """
 import torch
 
 
 class GraphedStep:
-    def __init__(self, trainer, body, ring=4, exchange=None, update=None):
+    def __init__(self, trainer, body, ring=4, exchange=None, update=None, segments=None, between=None):
         self.tr = trainer
         self.body = body
         self.exchange = exchange
         self.update = update
+        # the captured passes: segments[0](*inputs), segments[1](), ...; between[i]() runs after the
+        # replay of segment i (data parallel: the exchange)
+        self.segments = segments if segments is not None else [body]
+        self.between = between if between is not None else ([exchange] if exchange is not None else [])
         self.graph = None
+        self.graphs = []
         self.graph_update = None
         self.static = None
         self.device = trainer.device
@@ -73,9 +80,11 @@ class GraphedStep:
             self.tr.packer.run()
             self.eager_repacks += 1
         self._set_lr()
-        self.graph.replay()
-        if self.exchange is not None:
-            self.exchange()
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.between):
+                self.between[i]()
+        if self.graph_update is not None:
             self.graph_update.replay()
         self.replays += 1
         for p in opt._uniq:
@@ -87,7 +96,7 @@ class GraphedStep:
         self.static = [x.detach().clone() for x in inputs]
         s = self.stream
         s.wait_stream(torch.cuda.current_stream(self.device))
-        dp = self.exchange is not None
+        dp = self.update is not None  # data parallel: the update is a graph of its own
         red = self.tr.reducer if dp else None
         with torch.cuda.stream(s):
             if dp:  # iteration 0, eager, with the overlapped exchange (learns the live set)
@@ -108,7 +117,13 @@ class GraphedStep:
                 red.deferred = True
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, stream=s, capture_error_mode=mode):
-                self.body(*self.static)
+                self.segments[0](*self.static)
+            self.graphs = [self.graph]
+            for seg in self.segments[1:]:  # later segments read the first one's tensors: one memory pool
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.graph.pool(), stream=s, capture_error_mode=mode):
+                    seg()
+                self.graphs.append(g)
             if dp:
                 self.graph_update = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph_update, stream=s, capture_error_mode=mode):
@@ -126,3 +141,6 @@ class GraphedStep:
                     if isinstance(new, torch.Tensor) and new is not v and new.shape == v.shape:
                         new.copy_(v)
         torch.cuda.current_stream(self.device).wait_stream(s)
+        #  the packs the captured forward reads were built from these versions: an eager
+        # weight edit before the first replay must trigger the same repack as one between replays
+        self.versions = [p._version for p in opt._uniq]

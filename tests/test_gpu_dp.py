@@ -199,7 +199,13 @@ def _graph_worker(rank, world, port, q):
             tr = UDATrainer(args, cuda=True)
             tr.optimizer.zero_grad()
             losses = []
+            log = []
             for it in range(4):
+                if graph and it == 3:  # the host's order of segment replays and bucket launches
+                    gs, red = tr._graphed, tr.reducer
+                    for i, g in enumerate(gs.graphs):
+                        g.replay = (lambda f, i: lambda: (log.append(("replay", i)), f())[1])(g.replay, i)
+                    red._launch = (lambda f: lambda b: (log.append(("launch", b)), f(b))[1])(red._launch)
                 seed = 1000 * rank + it
                 tr.uda_step(synthetic_image(H, W, seed).cuda(), synthetic_labels(H, W, 19, seed).cuda(),
                             synthetic_image(H, W, 500 + seed).cuda())
@@ -207,6 +213,18 @@ def _graph_worker(rank, world, port, q):
                 losses.append((tr.loss_val.item(), tr.loss_target.item(), tr.loss_target_2.item()))
             if graph:
                 assert tr._graphed is not None and tr._graphed.replays == 3 and tr._graphed.graph_update is not None
+                # the backward replays as two segments split at layer3's output; the buckets of layer4
+                # and the heads (the leading parameters in backward order) launch between them, the
+                # rest after the second
+                assert len(tr._graphed.graphs) == 2, len(tr._graphed.graphs)
+                n_early = len(tr.model.split_params())
+                r1 = log.index(("replay", 1))
+                early = [b for k, b in log[:r1] if k == "launch"]
+                late = [b for k, b in log[r1:] if k == "launch"]
+                assert log[0] == ("replay", 0) and early and late, log
+                assert all(red.bounds[b][1] <= n_early for b in early), (early, n_early)
+                assert all(red.bounds[b][1] > n_early for b in late), (late, n_early)
+                assert early + late == [b for b in range(len(red.bounds)) if red.has_live[b]], log
             out[graph] = (losses, torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).cpu().numpy())
             del tr
         q.put((rank, "ok", out))
@@ -218,8 +236,9 @@ def _graph_worker(rank, world, port, q):
 
 
 def test_graphed_dp_step_matches_eager_dp():
-    """The captured data-parallel step (utils/graph.py: graph of the two forward/backward passes,
-    the reducer's all-reduce of every live bucket, graph of the SGD step) against the eager DP
+    """The captured data-parallel step (utils/graph.py: the forward/backward passes as two graphs
+    split at layer3's output with the exchange of the first one's gradients launched between their
+    replays, then the rest of the exchange, then the graph of the SGD step) against the eager DP
     step with the overlapped bucket countdown, 2 ranks (gloo) x 4 UDA iterations: every loss and
     every parameter bit-identical (the step has no library kernel and the 2-rank sum is exact in
     either order), and the two replicas' parameters identical after every run (one exchange per

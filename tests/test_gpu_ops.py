@@ -428,11 +428,13 @@ def _f16(t):
 
 @pytest.mark.parametrize("kind,cin,cout,h,w,d", [
     ("dconv", 256, 256, 17, 33, 2), ("dconv", 512, 512, 17, 33, 4), ("dconv", 64, 64, 33, 65, 1),
-    ("pconv", 256, 1024, 17, 33, 0), ("pconv", 1024, 256, 17, 33, 0)])
+    ("pconv", 256, 1024, 17, 33, 0), ("pconv", 1024, 256, 17, 33, 0), ("pconv", 256, 64, 33, 65, 0),
+    ("pconv", 64, 256, 33, 65, 0)])
 def test_conv_fp16_math(kind, cin, cout, h, w, d):
     """BASELINE config 5's fp16 MFMA path (msl_*_f16): products of fp16-rounded, per-tensor scaled
-    operands summed in fp32 on the 128-row tiles (M > 64; the weight gradient where both sides have
-    >= 128 channels), exact f32 MFMA below.  Reference: the same conv in fp64 on the operands as
+    operands summed in fp32 - the forward and data gradient on every M (r04: the M <= 64 GEMMs on the
+    64-row fp16 tiles too), the weight gradient where both sides have >= 128 channels, exact f32 MFMA
+    below.  Reference: the same conv in fp64 on the operands as
     the kernels see them, so the only admissible difference is the fp32 accumulation (1e-5 of
     max|ref|, as the fp32 kernels); operand scales far from 1 (weights 1e-2, gradients 1e-6)."""
     g = torch.Generator().manual_seed(cin + 13 * cout + d)
@@ -459,8 +461,7 @@ def test_conv_fp16_math(kind, cin, cout, h, w, d):
     def conv(xx, ww):
         return F.conv2d(xx, ww, padding=pad, dilation=dil)
 
-    rf, rd, rw = (_f16 if cout > 64 else exact), (_f16 if cin > 64 else exact), \
-        (_f16 if min(cin, cout) >= 128 else exact)
+    rf, rd, rw = _f16, _f16, (_f16 if min(cin, cout) >= 128 else exact)
     assert _rel(y, conv(rf(x), rf(wt))) < 1e-5
     xr = rd(x).requires_grad_()
     conv(xr, rd(wt)).backward(rd(gy))
