@@ -204,7 +204,12 @@ class ResNetMulti(nn.Module):
         x = self.layer2(x)
         x = self.layer3(x)
         if self.keep_split:
-            self.split_out = x
+            # the heads read a detached leaf: their backward stops there (backward(inputs=[x]) would
+            # run x's own node, layer3's last BN), and its .grad seeds the trunk's backward
+            xd = x.detach().requires_grad_()
+            if hasattr(x, "_msl_absmax"):
+                xd._msl_absmax = x._msl_absmax  # the BN's absmax tag (same version counter)
+            self.split_out, x = (x, xd), xd
         x1 = self.layer5(x)
         x2 = self.layer4(x)
         x2 = self.layer6(x2)

@@ -208,18 +208,18 @@ class UDATrainer(Trainer):
             pred_s, pred_t = m.forward_pair(x_s, x_t)
         finally:
             m.keep_split = False
-        x3, m.split_out = m.split_out, None
+        split, m.split_out = m.split_out, None
         loss_s = self.source_loss(pred_s, y_s)
         loss_t = self.target_loss_total(pred_t)
         self.reducer.prepare_for_backward()
-        torch.autograd.backward([loss_s, loss_t], inputs=[x3] + m.split_params())
+        torch.autograd.backward([loss_s, loss_t])  # ends at the heads' detached input (its .grad)
         ops.wgrad_join(self.device)
-        self._split = x3
+        self._split = split
 
     def _uda_grads_trunk(self):
         """The rest of the backward: from layer3's output through layer3 .. the stem."""
-        x3, self._split = self._split, None
-        g, x3.grad = x3.grad, None
+        (x3, xd), self._split = self._split, None
+        g, xd.grad = xd.grad, None
         torch.autograd.backward([x3], [g])
         ops.wgrad_join(self.device)
 
