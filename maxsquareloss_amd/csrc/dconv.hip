@@ -445,7 +445,8 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
       // the pointwise rows keep their two dwordx4 LDS-DMA pieces per wave and K-step (BD loses there:
       // 256 -> 1024 fwd 32.7 vs 31.0 us, 2048 -> 512 82.7 vs 75.1; layer3 3x3 fwd 52.4 vs 55.0,
       // layer4 172 vs 190; profiles/r03_fwd_forms_ab.txt)
-      if (!PW) {
+      // (full 16-channel blocks only: the stem's 147-row im2col operand keeps the LDS form)
+      if (!PW && a.cimg % kCB == 0) {
         if (accum)
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a, sk);
         else

@@ -575,6 +575,63 @@ __device__ __forceinline__ void mfma_stage_hdp(const float* __restrict__ As, int
   mid();
 }
 
+// The BD form with its first A fragments one K-step ahead (r04): bd_prep reads the plane K-step i+1's
+// first MFMAs use (f16x3: the lo plane; fp16: the only one) from its LDS slot while K-step i's MFMAs run;
+// bd_compute reads the other plane (in flight behind the first TM MFMAs), splits the B values and
+// issues the MFMAs in mfma_stage_hd's order (lo.hi, hi.lo, hi.hi per accumulator: bit-identical sums).
+template <int TM>
+struct BdFrag {
+  f16x8 a0[TM];
+};
+
+template <int TM, int BM, bool HI_ONLY>
+__device__ __forceinline__ void bd_prep(const float* __restrict__ As, int wm, int lane, BdFrag<TM>& f) {
+  const int l32 = lane & 31, h = lane >> 5;
+  const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) f.a0[i] = Ab[(HI_ONLY ? h : 2 + h) * BM + wm + i * 32 + l32];
+}
+
+template <int TM, int BM, bool HI_ONLY, bool PRE>
+__device__ __forceinline__ void bd_compute(const float* __restrict__ As, int wm, int lane, const BdFrag<TM>& f,
+                                           f32x16 (&acc)[TM][1], float sB, const float (&braw)[8]) {
+  const int l32 = lane & 31, h = lane >> 5;
+  const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
+  f16x8 ahi[TM];
+  if constexpr (!HI_ONLY) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) ahi[i] = Ab[h * BM + wm + i * 32 + l32];
+  }
+  Split2h bv;
+  if constexpr (PRE) {
+    union { float f[4]; f16x8 h; } bh, bl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh.f[j] = braw[j];
+      bl.f[j] = braw[4 + j];
+    }
+    bv.hi = bh.h;
+    bv.lo = bl.h;
+  } else if constexpr (HI_ONLY) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bv.hi[j] = (_Float16)(braw[j] * sB);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split2h_set(bv, j, braw[j] * sB);
+  }
+  if constexpr (HI_ONLY) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a0[i], bv.hi, acc[i][0], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a0[i], bv.hi, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[i], bv.lo, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[i], bv.hi, acc[i][0], 0, 0, 0);
+  }
+}
+
 // Forward form: C[m][p] = sum_k A[k][m] * B[k][p], BK = G * 16 (G tap-groups per K-step).
 template <int BM, int BN, int BK, int WM, int WN>
 __global__ void __launch_bounds__(256) k_igemm_fwd(FwdArgs a) {
@@ -1077,7 +1134,6 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       (int)min(0x7fffffffLL, (long long)a.ncb * (BP ? (H1 ? 2 : 4) : 6) * a.P * 16), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
   const unsigned chan_bytes = (unsigned)a.P * 4u;
-  const bool cfull = (a.cimg % kCB) == 0;  // every 16-channel block of the image operand is full
   // f16x3: B's scale from its absmax partials, A's from the pack; the result is unscaled by both
   float sB = 1.f, iA = 1.f, iB = 1.f;
   if constexpr (H3) {
@@ -1202,25 +1258,16 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
             for (int j = 0; j < 4; ++j) bq[4 * q + j] = c.f[j];
           }
         } else if constexpr (BD) {
-          // channels cb16 + 8h + j of this lane's pixel
-          if (cfull) {
-            // every channel block full (cimg % 16 == 0): the channel offset is wave-uniform, so it
-            // rides in the scalar soffset and the eight loads share one address VGPR (r04: the
-            // per-channel bound check cost ~32 VALU per K-step); an out-of-image pixel's voffset
-            // >= 2^31 is out of range whatever the soffset
-            const unsigned sb = (unsigned)__builtin_amdgcn_readfirstlane(cb16) * chan_bytes;
+          // channels cb16 + 8h + j of this lane's pixel.  The BD form runs only with every 16-channel
+          // block full (cimg % 16 == 0, launch_sk): the channel offset is wave-uniform, so it rides in
+          // the scalar soffset and the eight loads share one address VGPR (r04: a per-channel bound
+          // check cost ~32 VALU per K-step, and a second load path made the compiler's wait counts
+          // drain the queue); an out-of-image pixel's voffset >= 2^31 is out of range whatever the
+          // soffset
+          const unsigned sb = (unsigned)__builtin_amdgcn_readfirstlane(cb16) * chan_bytes;
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-              bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vbdh, (int)(sb + j * chan_bytes), 0));
-          } else {
-            // a channel past cimg reads 0 (OOB offset; OOB + c * P * 4 stays >= 2^31 since cimg * P * 4 < 2^31)
-            const int ci0 = cb16 + 8 * (lane >> 5);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const unsigned off = ci0 + j < a.cimg ? vbd + (unsigned)(ci0 + j) * chan_bytes : OOB;
-              bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0));
-            }
-          }
+          for (int j = 0; j < 8; ++j)
+            bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vbdh, (int)(sb + j * chan_bytes), 0));
         } else if constexpr (BPRE) {
           // piece (plane*2 + k half, 64-pixel half): lane = pixel, 16 B = 8 channels of a plane
 #pragma unroll
@@ -1267,68 +1314,51 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __builtin_amdgcn_s_barrier();  // the previous segment's LDS reads are complete in every wave
     if constexpr (BD) {
-      if (0 < nst) issue(k_a, 0, bdq[0]);
-      if (1 < nst) issue(k_a + 1, 1, bdq[1]);
-      if (2 < nst) issue(k_a + 2, 2, bdq[2]);
-      // K-step i: wait until its A piece and B values landed (the younger stages may stay in flight),
-      // barrier (the A slot refilled next was read by every wave at i - 1), issue K-step i + 3 into
-      // the ring slot K-step i - 1 freed, compute
-      auto step = [&](int i, float (&cur)[8], float (&nxt)[8]) {
-        const int younger = min(STAGES - 2, nst - 1 - i);
-        if (younger >= 2) wait_vmcnt<2 * INST_W>();
-        else if (younger == 1) wait_vmcnt<INST_W>();
-        else wait_vmcnt<0>();
+      // Every K-step issues a stage, also past the segment's end (K-steps >= nst: loads that land in a
+      // ring slot and an LDS slot no later K-step reads, zero-filled out of range), so exactly two
+      // stages are always younger than the one computed: one wait count, and the register ring's
+      // loads are followed by the same number of loads on every path.  (With the issues conditional,
+      // the compiler's wait-count analysis saw paths with no younger loads and drained the queue -
+      // vmcnt(0) - before the split of every first and fourth K-step, r04.)
+      issue(k_a, 0, bdq[0]);
+      issue(k_a + 1, 1, bdq[1]);
+      issue(k_a + 2, 2, bdq[2]);
+      // K-step i: wait until stage i + 1 landed (only stage i + 2 younger), barrier (stage i + 1 is
+      // complete in every wave's LDS pieces, and every wave has read slot i - 1's fragments, at step
+      // i - 2), issue stage i + 3 into that slot and ring entry, read + split K-step i + 1's fragments,
+      // and issue K-step i's MFMAs from the fragments read the step before
+      BdFrag<TM> fr[2];
+      wait_vmcnt<INST_W>();
+      __builtin_amdgcn_s_barrier();
+      bd_prep<TM, BM, H1>(smem, wm, lane, fr[0]);
+      auto step = [&](int i, BdFrag<TM>& fc, BdFrag<TM>& fn, float (&nxt)[8], const float (&cur)[8]) {
+        wait_vmcnt<INST_W>();
         __builtin_amdgcn_s_barrier();
-        const float* As = smem + (i % STAGES) * STAGE;
-        const bool more = i + STAGES - 1 < nst;
-        auto mid = [&] {
-          if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt);
-        };
-        if constexpr (BP)
-          mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
-        else
-          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
+        issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt);
+        bd_compute<TM, BM, H1, BP>(smem + (i % STAGES) * STAGE, wm, lane, fc, acc, sB, cur);
+        bd_prep<TM, BM, H1>(smem + ((i + 1) % STAGES) * STAGE, wm, lane, fn);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       };
-      for (int i = 0; i < nst; i += 4) {
-        step(i, bdq[0], bdq[3]);
-        if (i + 1 < nst) step(i + 1, bdq[1], bdq[0]);
-        if (i + 2 < nst) step(i + 2, bdq[2], bdq[1]);
-        if (i + 3 < nst) step(i + 3, bdq[3], bdq[2]);
+      int i = 0;
+      for (; i + 4 <= nst; i += 4) {
+        step(i, fr[0], fr[1], bdq[3], bdq[0]);
+        step(i + 1, fr[1], fr[0], bdq[0], bdq[1]);
+        step(i + 2, fr[0], fr[1], bdq[1], bdq[2]);
+        step(i + 3, fr[1], fr[0], bdq[2], bdq[3]);
       }
+      if (i < nst) step(i, fr[0], fr[1], bdq[3], bdq[0]);
+      if (i + 1 < nst) step(i + 1, fr[1], fr[0], bdq[0], bdq[1]);
+      if (i + 2 < nst) step(i + 2, fr[0], fr[1], bdq[1], bdq[2]);
+      wait_vmcnt<0>();  // the stages issued past the end land before the slots are reused
     } else {
+      // as in the BD form: a stage issued every K-step, past the end too, so one wait count
 #pragma unroll
-    for (int k = 0; k < STAGES - 1; ++k)
-      if (k < nst) issue(k_a + k, k, bdq[0]);
+    for (int k = 0; k < STAGES - 1; ++k) issue(k_a + k, k, bdq[0]);
     for (int i = 0; i < nst; ++i) {
-      const int younger = min(STAGES - 2, nst - 1 - i);
-      if constexpr (STAGES >= 6) {
-        if (younger >= 4) wait_vmcnt<4 * INST_W>();
-        else if (younger == 3) wait_vmcnt<3 * INST_W>();
-        else if (younger == 2) wait_vmcnt<2 * INST_W>();
-        else if (younger == 1) wait_vmcnt<INST_W>();
-        else wait_vmcnt<0>();
-      } else if constexpr (STAGES == 5) {
-        if (younger >= 3) wait_vmcnt<3 * INST_W>();
-        else if (younger == 2) wait_vmcnt<2 * INST_W>();
-        else if (younger == 1) wait_vmcnt<INST_W>();
-        else wait_vmcnt<0>();
-      } else if constexpr (STAGES >= 4) {
-        if (younger >= 2) wait_vmcnt<2 * INST_W>();
-        else if (younger == 1) wait_vmcnt<INST_W>();
-        else wait_vmcnt<0>();
-      } else if constexpr (STAGES == 3) {
-        if (younger == 1) wait_vmcnt<INST_W>();
-        else wait_vmcnt<0>();
-      } else {
-        wait_vmcnt<0>();
-      }
+      wait_vmcnt<(STAGES - 2) * INST_W>();
       __builtin_amdgcn_s_barrier();
       const float* As = smem + (i % STAGES) * STAGE;
-      const bool more = i + STAGES - 1 < nst;
-      auto mid = [&] {
-        if (more) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, bdq[0]);
-      };
+      auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, bdq[0]); };
       if constexpr (MT == kMathBf16)
         mfma_stage_bf16<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (MT == kMathX6)
@@ -1345,6 +1375,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         mfma_stage_pipe<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    wait_vmcnt<0>();  // the stages issued past the end land before the slots are reused
     }
 
     if constexpr (H3) {  // exact: both factors are powers of two
@@ -2333,37 +2364,58 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       }
     }
     float rbv[16];
-    unsigned rmb = 0;
-    // loads the stage's two K-steps (a missing second one is all-masked) into rv; the border mask is
-    // kept in mbo and applied when the values are split (storeB), so nothing waits for the loads here
-    auto loadB = [&](float (&rv)[16], unsigned& mbo) {
+    unsigned rmb = 0, rsh = 0;
+    // loads the stage's two K-steps (a missing second one is all-masked) into rv: exactly one 16-B load
+    // per row, so every stage issues the same number of loads on every path (the compiler's wait
+    // counts then keep the loads in flight across the MFMAs, r04).  The border mask is kept in mbo and
+    // applied when the values are split (storeB), so nothing waits for the loads here; a run that
+    // starts 1-3 pixels before X (row 0, negative shift) is loaded from X's start and shifted into
+    // place there (sho: the shift per row, one byte each); one further before is masked whole.
+    auto loadB = [&](float (&rv)[16], unsigned& mbo, unsigned& sho) {
       const int ks0 = ld_ks;
       const unsigned m32 = kmask() | (kmask() << 16);
       const unsigned mb = (m32 >> (4 * cc)) & 0xfu;
       mbo = mb;
+      sho = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int nr = (tid >> 3) + 32 * i;
         const long long e = (long long)(n0 + nr) * a.P + ks0 * kWx6BK + 4 * cc + shift;
-        union { u32x4 u; float f[4]; } c;
-        if (n0 + nr < a.N && e >= 0) {
-          c.u = __builtin_amdgcn_raw_buffer_load_b128(rB, (unsigned)e * 4u, 0, 0);
-        } else {  // row past N, or a run starting before X (row 0, negative shift): per element
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const unsigned off = (n0 + nr < a.N && e + j >= 0) ? (unsigned)(e + j) * 4u : OOB;
-            c.f[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rB, off, 0, 0));
+        unsigned off = OOB;
+        if (n0 + nr < a.N) {
+          if (e >= 0) {
+            off = (unsigned)e * 4u;
+          } else if (e > -4) {
+            off = 0u;
+            sho |= (unsigned)(-e) << (8 * i);
           }
         }
+        union { u32x4 u; float f[4]; } c;
+        c.u = __builtin_amdgcn_raw_buffer_load_b128(rB, off, 0, 0);
 #pragma unroll
         for (int j = 0; j < 4; ++j) rv[4 * i + j] = c.f[j];
       }
     };
-    auto storeB = [&](int buf, const float (&rv0)[16], unsigned mbv) {  // split once, NP 8-B plane quarters
+    auto storeB = [&](int buf, const float (&rv0)[16], unsigned mbv, unsigned shv) {  // split once, NP 8-B plane quarters
       char* base = smem + buf * STAGEB + wofs;
       float rbv[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) rbv[q] = (mbv >> (q & 3)) & 1u ? rv0[q] : 0.f;
+      for (int q = 0; q < 16; ++q) rbv[q] = rv0[q];
+      if (shv) {  // rows loaded from X's start: element j of the run is element j - sh of the load
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const unsigned sh = (shv >> (8 * i)) & 0xffu;
+#pragma unroll
+          for (int j = 3; j >= 0; --j) {
+            float v = 0.f;
+#pragma unroll
+            for (int k = 0; k < j; ++k) v = (unsigned)(j - k) == sh ? rv0[4 * i + k] : v;
+            rbv[4 * i + j] = sh == 0 ? rv0[4 * i + j] : v;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rbv[q] = (mbv >> (q & 3)) & 1u ? rbv[q] : 0.f;
       if constexpr (H1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -2478,25 +2530,26 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __syncthreads();  // the previous segment's LDS reads are complete in every wave
-    loadB(rbv, rmb);
+    loadB(rbv, rmb, rsh);
     loadA(A0, k_a);
-    storeB(0, rbv, rmb);
+    storeB(0, rbv, rmb, rsh);
     __syncthreads();
+    // Every stage issues the same loads, past the segment's end too (A out of range reads 0, B past
+    // the end is masked to 0, an odd segment's last K-step computes with zero B), so each wait
+    // leaves the younger loads in flight: A for the next K-step and the next stage's B stay in
+    // flight during the MFMAs.  (With the loads conditional, the compiler drained the queue -
+    // vmcnt(0) - before every stage's first MFMA, waiting for the B loads just issued, r04.)
     int ks = k_a;  // the K-step computed next
     for (int s = 0; 2 * s < nst; ++s) {
-      const int left = nst - 2 * s;
-      const bool more = left > 2;  // a next stage
-      if (more) loadB(rbv, rmb);   // in flight during this stage's MFMAs
       const char* Bs = smem + (s & 1) * STAGEB;
-      if (ks + 1 < k_b) loadA(A1, ks + 1);
+      loadA(A1, ks + 1);
+      loadB(rbv, rmb, rsh);  // the next stage: in flight during this stage's MFMAs
+      __builtin_amdgcn_sched_barrier(0);  // (left to itself the compiler sinks a B load past the MFMAs)
       compute(Bs, A0);
-      ++ks;
-      if (left > 1) {
-        if (ks + 1 < k_b) loadA(A0, ks + 1);
-        compute(Bs + KVB, A1);
-        ++ks;
-      }
-      if (more) storeB((s + 1) & 1, rbv, rmb);
+      loadA(A0, ks + 2);
+      compute(Bs + KVB, A1);
+      ks += 2;
+      storeB((s + 1) & 1, rbv, rmb, rsh);
       __syncthreads();
     }
     if (H3 && !a.rowscale) {  // exact: both factors are powers of two (rowscale: in k_wsk_reduce)

@@ -1,12 +1,11 @@
 """Per-op timing of the conv GEMMs at the step's 1024x512 shapes (GPU), for same-box A/B of kernel forms.
 
-    python scripts/bench_ops.py [--variant K ...] [--reps N] [--check]
+    python scripts/bench_ops.py [--reps N] [--check] [--only NAME] [--nimg 2]
 
 Each op call (the C-ABI entry point as ops.py issues it, incl. its reduce and split launches) is timed
-with HIP events over `reps` back-to-back calls after warm-up, on f16x3 (the default fp32 form).  With
---variant, the library's experiment switch (msl_conv_set_variant) is set to each value in turn and
-every op is re-timed, so variants compare on one box within one process.  --check also compares each
-variant's outputs against fp64 (per-element error relative to the sum of |terms|).
+with HIP events over `reps` back-to-back calls after warm-up, on f16x3 (the default fp32 form).  Two
+builds compare on one box by running this once per library (MSL_LIB_PATH, scripts/gpu_ab.sh).
+--check also compares the outputs against fp64 (per-element error relative to the sum of |terms|).
 """
 import argparse
 import json
@@ -107,7 +106,6 @@ SHAPES = [("aspp6 2048->19", 2048, 19, 3, 6), ("layer1 3x3", 64, 64, 3, 1), ("la
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variant", type=int, nargs="*", default=[0])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--only", default=None, help="substring of the shape names to run")
@@ -116,17 +114,14 @@ def main():
     a = ap.parse_args()
     lib = hip.load()
     ops_list = [conv_ops(*s, h=a.hw[0], w=a.hw[1], nimg=a.nimg) for s in SHAPES if a.only is None or a.only in s[0]]
-    for v in a.variant:
-        if hasattr(lib, "msl_conv_set_variant"):
-            hip.check(lib.msl_conv_set_variant(v), "msl_conv_set_variant")
-        for name, fwd, dgr, wgr, flops, check in ops_list:
-            t = [timed(f, a.reps) for f in (fwd, dgr, wgr)]
-            rec = {"variant": v, "hw": a.hw, "nimg": a.nimg, "op": name, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
-                   "wgrad_us": round(t[2], 1), "fwd_tf": round(flops / t[0] / 1e6, 1),
-                   "wgrad_tf": round(flops / t[2] / 1e6, 1)}
-            if a.check:
-                rec["err_fwd_dgrad_wgrad"] = [float(f"{e:.2e}") for e in check()]
-            print(json.dumps(rec), flush=True)
+    for name, fwd, dgr, wgr, flops, check in ops_list:
+        t = [timed(f, a.reps) for f in (fwd, dgr, wgr)]
+        rec = {"hw": a.hw, "nimg": a.nimg, "op": name, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
+               "wgrad_us": round(t[2], 1), "fwd_tf": round(flops / t[0] / 1e6, 1),
+               "wgrad_tf": round(flops / t[2] / 1e6, 1)}
+        if a.check:
+            rec["err_fwd_dgrad_wgrad"] = [float(f"{e:.2e}") for e in check()]
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
