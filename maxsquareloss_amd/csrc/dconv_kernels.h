@@ -47,7 +47,7 @@ struct WgradArgs {
 // All of the stage's operand reads are issued before the first MFMA, so the LDS latency of
 // k-pair kk+1.. overlaps the MFMAs of k-pair kk (the compiler emits counted lgkmcnt waits).
 template <int BK, int TM, int TN, int LDA_S, int LDB_S>
-__device__ __forceinline__ void mfma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void mfma_stage(const float* As, const float* Bs,
                                            int wm, int wn, int lane, f32x16 (&acc)[TM][TN]) {
   const int l32 = lane & 31, kh = lane >> 5;
   constexpr int KP = BK / 2;
@@ -74,7 +74,7 @@ __device__ __forceinline__ void mfma_stage(const float* __restrict__ As, const f
 // exposes the LDS latency once per k-pair), and `mid` - the next stage's DMA issue - is placed
 // after the first k-pair so its address arithmetic overlaps the MFMA pipe.
 template <int BK, int TM, int TN, int LDA_S, int LDB_S, typename F>
-__device__ __forceinline__ void mfma_stage_pipe(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void mfma_stage_pipe(const float* As, const float* Bs,
                                                 int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
   const int l32 = lane & 31, kh = lane >> 5;
   constexpr int KP = BK / 2;
@@ -110,7 +110,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // floats per half-wave), rounded to bf16 (RNE, v_cvt_pk_bf16_f32) in registers; fp32
 // accumulation.  `mid` runs after the first 16-deep group.
 template <int BK, int TM, int TN, int LDA_S, int LDB_S, typename F>
-__device__ __forceinline__ void mfma_stage_bf16(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void mfma_stage_bf16(const float* As, const float* Bs,
                                                 int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
   const int l32 = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -290,7 +290,7 @@ __device__ __forceinline__ f32x16 frag_mma(const typename MathFrag<MT>::type& a,
 
 // One LDS stage of fp32 operands through mfma_x6 (same operand reads as mfma_stage_bf16).
 template <int BK, int TM, int TN, int LDA_S, int LDB_S, typename F>
-__device__ __forceinline__ void mfma_stage_x6(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void mfma_stage_x6(const float* As, const float* Bs,
                                               int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
   const int l32 = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(256) k_split_act(const float* __restrict__ x, 
 
 // x6 stage with both operands read as pre-split bf16 planes: no split work in the loop.
 template <int G, int TM, int TN, int BM, int BN, typename F>
-__device__ __forceinline__ void mfma_stage_x6pp(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void mfma_stage_x6pp(const float* As, const float* Bs,
                                                 int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
   const int l32 = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -397,7 +397,7 @@ __device__ __forceinline__ void mfma_stage_x6pp(const float* __restrict__ As, co
 // x6 stage with the A fragments read as pre-split bf16 planes (one LDS stage = G K-steps of
 // [plane][half][BM][8] bf16, 24*BM floats each) and the B fragments split as they are read.
 template <int G, int TM, int TN, int BM, int LDB_S, typename F>
-__device__ __forceinline__ void mfma_stage_x6p(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void mfma_stage_x6p(const float* As, const float* Bs,
                                                int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
   const int l32 = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -428,7 +428,7 @@ __device__ __forceinline__ void mfma_stage_x6p(const float* __restrict__ As, con
 // f16x3 stage: A fragments from the pre-split fp16 planes (one LDS stage = G K-steps of
 // [plane][half][BM][8] fp16, 16*BM floats each), B fragments scaled by sB and split as they are read.
 template <int G, int TM, int TN, int BM, int LDB_S, typename F>
-__device__ __forceinline__ void mfma_stage_h3p(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void mfma_stage_h3p(const float* As, const float* Bs,
                                                int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid,
                                                float sB) {
   const int l32 = lane & 31, h = lane >> 5;
@@ -475,7 +475,7 @@ __device__ __forceinline__ void mfma_stage_h3p(const float* __restrict__ As, con
 // fp16 stage: A fragments from the pack's hi plane (G K-steps of [half][BM][8] fp16, 8*BM floats
 // each), B fragments scaled by sB and rounded to fp16 as they are read.
 template <int G, int TM, int TN, int BM, int LDB_S, typename F>
-__device__ __forceinline__ void mfma_stage_h1p(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void mfma_stage_h1p(const float* As, const float* Bs,
                                                int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid,
                                                float sB) {
   const int l32 = lane & 31, h = lane >> 5;
@@ -508,7 +508,7 @@ __device__ __forceinline__ void mfma_stage_h1p(const float* __restrict__ As, con
 // K-steps ahead; A fragments from the LDS ring as in mfma_stage_h3p.  One K-step, one 32-pixel column
 // per wave (1 x 4 waves).
 template <int TM, int BM, bool HI_ONLY, typename F>
-__device__ __forceinline__ void mfma_stage_hd(const float* __restrict__ As, int wm, int lane, f32x16 (&acc)[TM][1],
+__device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane, f32x16 (&acc)[TM][1],
                                               F&& mid, float sB, const float (&braw)[8]) {
   const int l32 = lane & 31, h = lane >> 5;
   const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
@@ -543,7 +543,7 @@ __device__ __forceinline__ void mfma_stage_hd(const float* __restrict__ As, int 
 // The BD stage with the image operand pre-split (k_split_img): braw holds the lane's hi plane (floats
 // 0..3 as 16 B) and lo plane (4..7), already scaled; no split work in the loop.
 template <int TM, int BM, bool HI_ONLY, typename F>
-__device__ __forceinline__ void mfma_stage_hdp(const float* __restrict__ As, int wm, int lane, f32x16 (&acc)[TM][1],
+__device__ __forceinline__ void mfma_stage_hdp(const float* As, int wm, int lane, f32x16 (&acc)[TM][1],
                                                F&& mid, const float (&braw)[8]) {
   const int l32 = lane & 31, h = lane >> 5;
   const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
@@ -573,63 +573,6 @@ __device__ __forceinline__ void mfma_stage_hdp(const float* __restrict__ As, int
     for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bh.h, acc[i][0], 0, 0, 0);
   }
   mid();
-}
-
-// The BD form with its first A fragments one K-step ahead (r04): bd_prep reads the plane K-step i+1's
-// first MFMAs use (f16x3: the lo plane; fp16: the only one) from its LDS slot while K-step i's MFMAs run;
-// bd_compute reads the other plane (in flight behind the first TM MFMAs), splits the B values and
-// issues the MFMAs in mfma_stage_hd's order (lo.hi, hi.lo, hi.hi per accumulator: bit-identical sums).
-template <int TM>
-struct BdFrag {
-  f16x8 a0[TM];
-};
-
-template <int TM, int BM, bool HI_ONLY>
-__device__ __forceinline__ void bd_prep(const float* __restrict__ As, int wm, int lane, BdFrag<TM>& f) {
-  const int l32 = lane & 31, h = lane >> 5;
-  const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
-#pragma unroll
-  for (int i = 0; i < TM; ++i) f.a0[i] = Ab[(HI_ONLY ? h : 2 + h) * BM + wm + i * 32 + l32];
-}
-
-template <int TM, int BM, bool HI_ONLY, bool PRE>
-__device__ __forceinline__ void bd_compute(const float* __restrict__ As, int wm, int lane, const BdFrag<TM>& f,
-                                           f32x16 (&acc)[TM][1], float sB, const float (&braw)[8]) {
-  const int l32 = lane & 31, h = lane >> 5;
-  const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
-  f16x8 ahi[TM];
-  if constexpr (!HI_ONLY) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) ahi[i] = Ab[h * BM + wm + i * 32 + l32];
-  }
-  Split2h bv;
-  if constexpr (PRE) {
-    union { float f[4]; f16x8 h; } bh, bl;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bh.f[j] = braw[j];
-      bl.f[j] = braw[4 + j];
-    }
-    bv.hi = bh.h;
-    bv.lo = bl.h;
-  } else if constexpr (HI_ONLY) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bv.hi[j] = (_Float16)(braw[j] * sB);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) split2h_set(bv, j, braw[j] * sB);
-  }
-  if constexpr (HI_ONLY) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a0[i], bv.hi, acc[i][0], 0, 0, 0);
-  } else {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a0[i], bv.hi, acc[i][0], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[i], bv.lo, acc[i][0], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[i], bv.hi, acc[i][0], 0, 0, 0);
-  }
 }
 
 // Forward form: C[m][p] = sum_k A[k][m] * B[k][p], BK = G * 16 (G tap-groups per K-step).
@@ -860,6 +803,17 @@ __device__ __forceinline__ void dma_b32(__amdgpu_buffer_rsrc_t r, float* lds_row
 }
 __device__ __forceinline__ void dma_b128(__amdgpu_buffer_rsrc_t r, float* lds_row, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_row, 16, voff, 0, 0, 0);
+}
+
+// The LDS base for the reads after a raw s_barrier: routed through an empty asm so the reads depend on
+// it and stay below the barrier (r04: the compiler does not see the LDS-DMA builtins as stores to the
+// array, treats its reads as movable, and may hoist a K-step's fragment reads above the barrier and the
+// counted waits - a race with the other waves' DMA pieces of that stage).
+typedef __attribute__((address_space(3))) float lds_f32;
+__device__ __forceinline__ const float* lds_after_barrier(float* smem) {
+  lds_f32* q = (lds_f32*)smem;
+  asm volatile("" : "+v"(q));
+  return (const float*)q;
 }
 
 template <int N>
@@ -1319,7 +1273,8 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // stages are always younger than the one computed: one wait count, and the register ring's
       // loads are followed by the same number of loads on every path.  (With the issues conditional,
       // the compiler's wait-count analysis saw paths with no younger loads and drained the queue -
-      // vmcnt(0) - before the split of every first and fourth K-step, r04.)
+      // vmcnt(0) - before the split of every first and fourth K-step; r04.  Those drains had also
+      // hidden the LDS-DMA ordering race described at the wait below.)
       issue(k_a, 0, bdq[0]);
       issue(k_a + 1, 1, bdq[1]);
       issue(k_a + 2, 2, bdq[2]);
@@ -1327,28 +1282,34 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // complete in every wave's LDS pieces, and every wave has read slot i - 1's fragments, at step
       // i - 2), issue stage i + 3 into that slot and ring entry, read + split K-step i + 1's fragments,
       // and issue K-step i's MFMAs from the fragments read the step before
-      BdFrag<TM> fr[2];
-      wait_vmcnt<INST_W>();
-      __builtin_amdgcn_s_barrier();
-      bd_prep<TM, BM, H1>(smem, wm, lane, fr[0]);
-      auto step = [&](int i, BdFrag<TM>& fc, BdFrag<TM>& fn, float (&nxt)[8], const float (&cur)[8]) {
-        wait_vmcnt<INST_W>();
+      // K-step i: wait until its A pieces landed, barrier (the A slot refilled next was read by every
+      // wave at i - 1), issue K-step i + 3 into the ring entry and slot K-step i - 1 freed, compute.
+      // The count leaves only the two younger stages' LDS-DMA pieces in flight, not their B loads:
+      // an LDS-DMA may land after register loads issued behind it (r04: with the B loads counted too -
+      // vmcnt(2 * INST_W) - a wave now and then read a stage's A slot before another wave's DMA piece
+      // had landed; scripts/dbg_det.py, profiles/r04_bd_wait_race.txt).  The B registers are waited
+      // for by the compiler at their use.
+      auto step = [&](int i, float (&cur)[8], float (&nxt)[8]) {
+        wait_vmcnt<2 * A_INST_W>();
         __builtin_amdgcn_s_barrier();
-        issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt);
-        bd_compute<TM, BM, H1, BP>(smem + (i % STAGES) * STAGE, wm, lane, fc, acc, sB, cur);
-        bd_prep<TM, BM, H1>(smem + ((i + 1) % STAGES) * STAGE, wm, lane, fn);
+        const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
+        auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt); };
+        if constexpr (BP)
+          mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
+        else
+          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       };
       int i = 0;
       for (; i + 4 <= nst; i += 4) {
-        step(i, fr[0], fr[1], bdq[3], bdq[0]);
-        step(i + 1, fr[1], fr[0], bdq[0], bdq[1]);
-        step(i + 2, fr[0], fr[1], bdq[1], bdq[2]);
-        step(i + 3, fr[1], fr[0], bdq[2], bdq[3]);
+        step(i, bdq[0], bdq[3]);
+        step(i + 1, bdq[1], bdq[0]);
+        step(i + 2, bdq[2], bdq[1]);
+        step(i + 3, bdq[3], bdq[2]);
       }
-      if (i < nst) step(i, fr[0], fr[1], bdq[3], bdq[0]);
-      if (i + 1 < nst) step(i + 1, fr[1], fr[0], bdq[0], bdq[1]);
-      if (i + 2 < nst) step(i + 2, fr[0], fr[1], bdq[1], bdq[2]);
+      if (i < nst) step(i, bdq[0], bdq[3]);
+      if (i + 1 < nst) step(i + 1, bdq[1], bdq[0]);
+      if (i + 2 < nst) step(i + 2, bdq[2], bdq[1]);
       wait_vmcnt<0>();  // the stages issued past the end land before the slots are reused
     } else {
       // as in the BD form: a stage issued every K-step, past the end too, so one wait count
@@ -1357,7 +1318,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     for (int i = 0; i < nst; ++i) {
       wait_vmcnt<(STAGES - 2) * INST_W>();
       __builtin_amdgcn_s_barrier();
-      const float* As = smem + (i % STAGES) * STAGE;
+      const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
       auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, bdq[0]); };
       if constexpr (MT == kMathBf16)
         mfma_stage_bf16<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
@@ -1550,7 +1511,7 @@ constexpr int kRgRL = 192;                        // staged floats per channel r
 constexpr int kRgMaxDil = (kRgRL - 3 - 128) / 2;  // 30: o_c + BN + 2d <= kRgRL
 
 template <int MT, int TM, int TN, int BM, typename F>
-__device__ __forceinline__ void rg_stage(const float* __restrict__ As, const float* __restrict__ Bs,
+__device__ __forceinline__ void rg_stage(const float* As, const float* Bs,
                                          int wm, int wn, int lane, int d, const int (&ob)[8],
                                          const bool (&vt)[TN][3], f32x16 (&acc)[TM][TN], F&& mid) {
   const int l32 = lane & 31, kh = lane >> 5;
@@ -1929,7 +1890,7 @@ __global__ void __launch_bounds__(256) k_wgrad_sk(WskArgs a) {
       }
       __builtin_amdgcn_s_barrier();
       if (i + STAGES - 1 < nst) issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES);
-      const float* As = smem + (i % STAGES) * STAGE;
+      const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
       const float* Bs = As + A_STAGE;
       typedef float f32x2 __attribute__((ext_vector_type(2)));
       if constexpr (MT != kMathF32) {
