@@ -334,3 +334,61 @@ def test_loss_bwd_chunk_lds_bound(hi, wi, ho, wo):
         lo = int(np.searchsorted(i0, ixa - 1, side="left"))
         hi_ = wo if ixb >= wi else int(np.searchsorted(i0, ixb, side="left"))
         assert hi_ - lo <= wmax, (j, hi_ - lo, wmax)
+
+
+def _split_worker(rank, world, port, q):
+    """The split exchange of a captured DP step (utils/graph.py segments; solve_gta5.uda_step): after
+    the first backward segment reduce_early launches only the buckets made of the parameters that
+    segment finished, reduce_rest the others after the second segment."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    from maxsquareloss_amd.utils.dist import GradReducer
+    from maxsquareloss_amd.utils.optim import SGD
+    net = _SinkNet()
+    plist = [p for p in net.parameters()]
+    opt = SGD([{"params": plist, "lr": 0.1}], lr=0.1, momentum=0.9, weight_decay=5e-4)
+    red = GradReducer(opt, bucket_cap_mb=0.0002)
+    g = torch.Generator().manual_seed(7 + rank)
+    x = torch.randn(4, 8, generator=g)
+    opt.zero_grad()
+    red.prepare_for_backward()
+    net(x).sum().backward()
+    red.finish()                                  # first step: learns the live set
+    log, real = [], red._launch
+    red._launch = lambda b: (log.append(("launch", b)), real(b))[1]
+    opt.zero_grad()
+    red.deferred = True                           # as under a graph capture: no hooks armed
+    red.prepare_for_backward()
+    net(x).sum().backward()
+    n_early = red.bounds[0][1]                    # the parameters of the first bucket (backward order)
+    log.append(("segment", 1))
+    red.reduce_early(n_early)
+    log.append(("segment", 2))
+    red.reduce_rest()
+    red.deferred = False
+    q.put((rank, log, list(red.bounds), [bool(h) for h in red.has_live],
+           opt.grads.flat.detach().numpy().copy(), n_early))
+    dist.destroy_process_group()
+
+
+def test_dp_bucket_launches_interleave_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    log, bounds, has_live, flat0, n_early = got[0]
+    seg2 = log.index(("segment", 2))
+    early = [b for k, b in log[:seg2] if k == "launch"]
+    late = [b for k, b in log[seg2:] if k == "launch"]
+    assert log[0] == ("segment", 1)                       # nothing launched inside the backward
+    assert early and late, (log, bounds, has_live)
+    assert all(bounds[b][1] <= n_early for b in early) and all(bounds[b][1] > n_early for b in late)
+    assert sorted(early + late) == [b for b in range(len(bounds)) if has_live[b]]
+    assert np.array_equal(flat0, got[1][3])              # both ranks hold the same reduced buffer
