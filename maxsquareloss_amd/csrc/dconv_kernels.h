@@ -2152,69 +2152,87 @@ __global__ void __launch_bounds__(256) k_wsk_reduce_wide(WskArgs a) {
 constexpr int kWx6BK = 16;
 
 // planes[((ks*3 + q)*2 + h)*lda + m][j] = term q of src[m][ks*16 + 8h + j] (0 past P or M).
-// Block = 64 rows x 4 K-steps (64 pixels).  Each wave loads 16 rows, one dword per lane and row
-// (lane = pixel: one coalesced 256-B run per load, 16 loads in flight per lane), splits them and
-// stores the bf16 terms to LDS as [plane][row][pixel] rows padded to 144 B; the block then writes
-// every (K-step, plane, half) as 64 consecutive rows of 16-B vectors (ds_read_b128 at a 144-B
-// stride: conflict-free).  The r01 form (32 rows, 8 scalar loads per thread at a 32-B stride
-// across lanes) ran 8.3 us on a 256 x 8385 dY.  grid = (lda / 64, ceil(KS / 4)).
+// Block = 32 rows x 16 K-steps (256 pixels).  Each wave loads 8 rows, 16 B per lane and row (4 pixels:
+// one coalesced 1-KB run per row and load; the r03 form's dword loads moved 256 B per instruction and ran
+// at 3.3 TB/s), splits them and stores the 16-bit terms to LDS as [plane][row][pixel] rows padded to
+// 528 B; the block then writes every (K-step, plane, half) as 32 consecutive rows of 16-B vectors
+// (ds_read_b128 at a 528-B stride: conflict-free).  grid = (lda / 32, ceil(KS / 16)).
 // MT = kMathH3P: two fp16 planes of src * s, s = pow2_scale of src's absmax partials `part`.
 template <int MT = kMathX6>
 __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ src, int M, int P, int KS, int lda,
                                                      bf16x8* __restrict__ planes, const float* __restrict__ part,
                                                      int npart, int rowscale = 0) {
-  constexpr int R = 64, LDP = 72;  // rows per block, LDS row stride in 16-bit terms (64 pixels + 8)
+  constexpr int R = 32, PX = 256, LDP = PX + 8;  // rows, pixels per block; LDS row stride in 16-bit terms
+  constexpr int KB = PX / kWx6BK;                // K-steps per block
   constexpr bool F16 = MT == kMathH3P || MT == kMathH1P;
   constexpr int NP = MT == kMathH1P ? 1 : F16 ? 2 : 3;
   __shared__ __attribute__((aligned(16))) unsigned short tile[NP * R * LDP];
+  typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int m0 = blockIdx.x * R, ks0 = blockIdx.y * 4;
-  const int p = ks0 * kWx6BK + lane;
-  const bool pin = p < P;
+  const int m0 = blockIdx.x * R, ks0 = blockIdx.y * KB;
+  const int p = ks0 * kWx6BK + 4 * lane;  // this lane's four pixels
   float sc = 1.f, inv;
   if constexpr (F16) {
     if (!rowscale) sc = pow2_scale(partials_max(part, npart, lane), inv);
   }
-  float v[R / 4];
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)src, (short)0, (int)min(0x7fffffffLL, (long long)M * P * 4), 0x00020000);
+  float v[R / 4][4];
 #pragma unroll
   for (int i = 0; i < R / 4; ++i) {
     const int m = m0 + wv + 4 * i;
-    v[i] = (pin && m < M) ? src[(long long)m * P + p] : 0.f;
-    if constexpr (F16) {  // the row's own scale (its maximum: one partial per row)
-      if (rowscale) v[i] *= m < M ? pow2_scale(part[m], inv) : 1.f;
-      else v[i] *= sc;
+    union { u32x4 u; float f[4]; } c;
+    if (p + 3 < P) {
+      c.u = __builtin_amdgcn_raw_buffer_load_b128(rs, m < M ? (unsigned)(m * P + p) * 4u : 0x80000000u, 0, 0);
+    } else {  // the block's last pixels: element by element, 0 past P
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        c.f[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rs, (m < M && p + j < P) ? (unsigned)(m * P + p + j) * 4u : 0x80000000u, 0, 0));
     }
+    float s = sc;
+    if constexpr (F16) {  // the row's own scale (its maximum: one partial per row)
+      if (rowscale) s = m < M ? pow2_scale(part[m], inv) : 1.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[i][j] = F16 ? c.f[j] * s : c.f[j];
   }
 #pragma unroll
   for (int i = 0; i < R / 4; ++i) {
     const int r = wv + 4 * i;
-    if constexpr (MT == kMathH1P) {
-      tile[r * LDP + lane] = __builtin_bit_cast(unsigned short, (_Float16)v[i]);
-    } else if constexpr (MT == kMathH3P) {
-      const float x = v[i];
-      const _Float16 h = (_Float16)x;
-      const _Float16 l = (_Float16)(x - (float)h);
-      tile[(0 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, h);
-      tile[((NP - 1) * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, l);
-    } else {
-      const __bf16 h = (__bf16)v[i];
-      const float rem = v[i] - (float)h;
-      const __bf16 md = (__bf16)rem;
-      tile[(0 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, h);
-      tile[(1 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, md);
-      tile[(2 * R + r) * LDP + lane] = __builtin_bit_cast(unsigned short, (__bf16)(rem - (float)md));
+    u16x4 t0, t1, t2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = v[i][j];
+      if constexpr (MT == kMathH1P) {
+        t0[j] = __builtin_bit_cast(unsigned short, (_Float16)x);
+      } else if constexpr (MT == kMathH3P) {
+        const _Float16 h = (_Float16)x;
+        t0[j] = __builtin_bit_cast(unsigned short, h);
+        t1[j] = __builtin_bit_cast(unsigned short, (_Float16)(x - (float)h));
+      } else {
+        const __bf16 h = (__bf16)x;
+        const float rem = x - (float)h;
+        const __bf16 md = (__bf16)rem;
+        t0[j] = __builtin_bit_cast(unsigned short, h);
+        t1[j] = __builtin_bit_cast(unsigned short, md);
+        t2[j] = __builtin_bit_cast(unsigned short, (__bf16)(rem - (float)md));
+      }
     }
+    *reinterpret_cast<u16x4*>(&tile[(0 * R + r) * LDP + 4 * lane]) = t0;
+    if constexpr (NP > 1) *reinterpret_cast<u16x4*>(&tile[(1 * R + r) * LDP + 4 * lane]) = t1;
+    if constexpr (NP > 2) *reinterpret_cast<u16x4*>(&tile[(2 * R + r) * LDP + 4 * lane]) = t2;
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 2 * NP; ++i) {  // 4 K-steps x NP planes x 2 halves x 64 rows: 2*NP vectors per thread
+  for (int i = 0; i < KB * NP * 2 * R / 256; ++i) {  // (K-step, plane, half, row) vectors: 2*NP per K-step
     const int idx = tid + 256 * i;
-    const int r = idx & 63, u = idx >> 6;  // u = (ksl*NP + q)*2 + h
+    const int r = idx & (R - 1), u = idx / R;  // u = (ksl*NP + q)*2 + h
     const int h = u & 1, q = (u >> 1) % NP, ksl = u / (2 * NP);
     const int ks = ks0 + ksl;
     if (ks < KS)
       planes[(long long)((ks * NP + q) * 2 + h) * lda + m0 + r] =
-          *reinterpret_cast<const bf16x8*>(&tile[(q * R + r) * LDP + ksl * 16 + h * 8]);
+          *reinterpret_cast<const bf16x8*>(&tile[(q * R + r) * LDP + ksl * kWx6BK + h * 8]);
   }
 }
 
