@@ -502,6 +502,14 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     pl.tiles_m = cdiv(M, 64);
     pl.kps = pl.ksteps;
   }
+  // fp16 pointwise GEMMs (r04): two K-steps per LDS stage, three stages (72 KB, two workgroups per
+  // CU): one barrier per 8 MFMAs per wave instead of 4 (f16x3's two planes would need 96 KB)
+  const bool pw2 = MT == kMathH1P && pl.sk && pl.bm == 128 && taps == 1 && dil0 == 0 && pl.ksteps % 2 == 0;
+  if (pw2) {
+    pl.G = 2;
+    pl.bk = 2 * kCB;
+    pl.kps = pl.ksteps / 2;
+  }
   if (ws_bytes < fwd_ws_bytes(pl, M, P, cimg, taps)) return MSL_ERR_WORKSPACE;
   FwdArgs a{};
   a.Ax6 = nullptr;
@@ -600,8 +608,16 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // (profiles/r02_f16x3_waves.txt)
         if (small_f16) {
           launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp);
-        } else if (taps == 1 && dil0 == 0)
-          launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
+        } else if (taps == 1 && dil0 == 0) {
+          if constexpr (MT == kMathH1P) {
+            if (pw2)
+              launch_sk<128, 2, 3, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
+            else
+              launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
+          } else {
+            launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
+          }
+        }
         else
           launch_sk<128, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp);
       } else {
