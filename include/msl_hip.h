@@ -16,10 +16,13 @@
  *     query, and no call leaves state that a later call reads.
  *   - Process-wide configuration: four switches select kernel FORMS, not
  *     results' meaning - msl_conv_set_f32_form, msl_conv_set_pack_form,
- *     msl_conv_set_sk_hybrid and msl_bn_set_fused.  They are plain globals read on the host at launch
- *     time: set them once at start-up, before work is enqueued; changing one
- *     while another host thread enqueues calls is a data race, and a captured
- *     hipGraph keeps the forms that were current at capture.
+ *     msl_conv_set_sk_hybrid and msl_bn_set_fused.  They are process-wide
+ *     atomics (not thread_local: PyTorch's autograd engine launches the
+ *     backward from its own per-device thread, which must see the forms the
+ *     main thread chose), read once per call on the host at launch time.
+ *     Set them at start-up, before work is enqueued: a concurrent set is
+ *     well defined but takes effect at an arbitrary call boundary, and a
+ *     captured hipGraph keeps the forms that were current at capture.
  *   - Work is enqueued on the given hipStream_t (passed as msl_stream_t) and
  *     is stream-ordered; no entry point synchronises the host, so every call
  *     is safe to capture in a hipGraph.

@@ -17,6 +17,7 @@
 // channels it touches).  Backward: per-channel reduce (sum g, sum g*xhat with g = dy masked by
 // y > 0 when ReLU) + flat apply (dx, d residual, dgamma, dbeta).  HBM-bound: fwd reads x twice,
 // writes y (+ reads the residual); bwd reads dy, x, y twice, writes dx (+ dres).
+#include <atomic>
 #include "msl_internal.h"
 
 namespace msl {
@@ -399,7 +400,7 @@ int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
 }
 constexpr int kBnRemaskMaxEpt = 16;  // msl_bn_bwd_am_beta's y = NULL: p <= 16 * 1024
 constexpr int kBnFusedMaxP = 33 * kBnFusedThreads;  // layer1 at 1024x512: 257x129 = 33153 px
-static int g_bn_fused = 1;  // msl_bn_set_fused
+static std::atomic<int> g_bn_fused{1};  // msl_bn_set_fused; process-wide + atomic as dconv.hip's forms
 static bool bn_fused_enabled() { return g_bn_fused != 0; }
 // beyond 16 elements per lane only with >= 128 channels: at 64 blocks (layer1's 64-channel
 // maps) the split kernels' wider grids win the backward (profiles/r01_bn_forms.txt)

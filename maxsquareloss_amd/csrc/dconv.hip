@@ -22,6 +22,7 @@
 // read is a conflict-free ds_read_b32 of 32 consecutive floats), double
 // buffered, one barrier per K-step.  Small GEMMs are split along K into fp32
 // slabs that a reduce kernel sums deterministically (fixed order).
+#include <atomic>
 #include "dconv_kernels.h"
 
 namespace msl {
@@ -263,14 +264,17 @@ __global__ void __launch_bounds__(256) k_pack_split_many(const msl_pack_job* __r
 // the tile count.  The split-K tile kernel remains for an odd K-step count with M <= 32.
 constexpr int kSkBN = 128, kSkNW = 512;
 // Forward-form schedule (msl_conv_set_sk_hybrid): 1 = data-parallel rounds + stream-K remainder
-// when the tiles outnumber the workers (SkArgs), 0 = pure stream-K.  Process-wide.
-static int g_sk_hybrid = 1;
+// when the tiles outnumber the workers (SkArgs), 0 = pure stream-K.  Process-wide, not per thread:
+// PyTorch's autograd engine issues the backward launches from its own per-device worker thread,
+// so a thread-local form set on the main thread would not reach them.  Atomic, so a setter racing
+// a launching thread is well defined (each launch reads a switch once).
+static std::atomic<int> g_sk_hybrid{1};
 // Matrix-core form of the fp32 entry points (msl_conv_set_f32_form): kMathF32 runs
 // v_mfma_f32_32x32x2_f32 (an exact fmaf chain), kMathX6 the three-way bf16 split on the BF16
 // matrix cores (fp32-accurate, dconv_kernels.h; layer3 fwd 78 vs 102 us in the step, err vs fp64
 // 4e-8 vs 6e-8 relative to sum|terms|), kMathH3P the scaled two-way fp16 split (three fp16
-// MFMAs per slice; dconv_kernels.h Split2h).  Process-wide; packs are form-specific.
-static int g_f32_form = kMathH3P;
+// MFMAs per slice; dconv_kernels.h Split2h).  Process-wide and atomic like g_sk_hybrid; packs are form-specific.
+static std::atomic<int> g_f32_form{kMathH3P};
 constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
 
 struct FwdPlan {
@@ -687,7 +691,7 @@ static long long packed_elems(int nbranch, int taps, int cin, int cout, int for_
   return pack_tail_offset(packed_f32_elems(nbranch, taps, cin, cout, for_dgrad)) + kPackTail;
 }
 
-static int g_pack_form = 1;  // msl_conv_set_pack_form: 1 = k_pack_split, 0 = k_pack + k_split_pack
+static std::atomic<int> g_pack_form{1};  // msl_conv_set_pack_form: 1 = k_pack_split, 0 = k_pack + k_split_pack
 
 static int pack(const float* w, long long branch_stride, int nbranch, int taps, int cin, int cout,
                 int for_dgrad, float* packed, hipStream_t st) {
@@ -893,14 +897,16 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
 
 template <typename... Args>
 static int fwd_f32(Args... args) {
-  if (g_f32_form == kMathH3P) return launch_fwd_form<kMathH3P>(args...);
-  return g_f32_form == kMathX6 ? launch_fwd_form<kMathX6>(args...) : launch_fwd_form<kMathF32>(args...);
+  const int form = g_f32_form.load(std::memory_order_relaxed);
+  if (form == kMathH3P) return launch_fwd_form<kMathH3P>(args...);
+  return form == kMathX6 ? launch_fwd_form<kMathX6>(args...) : launch_fwd_form<kMathF32>(args...);
 }
 
 template <typename... Args>
 static int wgrad_f32(Args... args) {
-  if (g_f32_form == kMathH3P) return launch_wgrad<kMathH3P>(args...);
-  return g_f32_form == kMathX6 ? launch_wgrad<kMathX6>(args...) : launch_wgrad<kMathF32>(args...);
+  const int form = g_f32_form.load(std::memory_order_relaxed);
+  if (form == kMathH3P) return launch_wgrad<kMathH3P>(args...);
+  return form == kMathX6 ? launch_wgrad<kMathX6>(args...) : launch_wgrad<kMathF32>(args...);
 }
 
 }  // namespace msl
