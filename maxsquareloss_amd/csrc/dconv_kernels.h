@@ -997,17 +997,26 @@ struct SkArgs {
   int tiles_m, tiles_n, KS, NW;
   int T;           // stream-K iterations: (tiles - tdp) * KS  (T * NW < 2^31, checked by the planner)
   int tdp;         // leading tiles that run data-parallel (a multiple of the grid size)
+  int gm;          // m-blocks per tile group (sk_tile): 1 = n fastest
 };
 
 __device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
-// Tile t of the forward-form stream-K space -> (m-block, n-block), n fastest: consecutive tiles
-// share an m-block, so the 64 workers of one XCD (consecutive ranges) read one or two m-blocks'
-// weights and a contiguous pixel range - their L2 holds the operands.  Layer3 fwd: 66 vs 154 MB
-// fetched per launch with m fastest (FETCH_SIZE x 2), same time; 2048->512 pointwise 121 vs 133
-// us (profiles/r02_sk_tile_order.txt).
-__device__ __forceinline__ void sk_tile(int t, int tiles_m, int tiles_n, int& tm, int& tn) {
-  tm = t / tiles_n;
-  tn = t - tm * tiles_n;
+// Tile t of the forward-form stream-K space -> (m-block, n-block).  gm <= 1: n fastest - consecutive
+// tiles share an m-block, so the 64 workers of one XCD (consecutive ranges) read one or two m-blocks'
+// weights and a contiguous pixel range (r02 layer3 fwd: 66 vs 154 MB fetched per launch with m
+// fastest; profiles/r02_sk_tile_order.txt).  gm > 1: groups of gm m-blocks, m fastest inside a
+// group - the gm tiles of one pixel block run on neighbouring workers, so the image block is
+// fetched once (r04: the pointwise and layer4 GEMMs, dconv.hip launch_fwd_form).
+__device__ __forceinline__ void sk_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  if (gm <= 1) {
+    tm = t / tiles_n;
+    tn = t - tm * tiles_n;
+    return;
+  }
+  const int g = t / (gm * tiles_n), r = t - g * gm * tiles_n;
+  const int m_in = min(gm, tiles_m - g * gm);  // m-blocks in this (possibly last, short) group
+  tn = r / m_in;
+  tm = g * gm + (r - tn * m_in);
 }
 __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
   return (int)((unsigned)((i + 1) * NW - 1) / (unsigned)T);
@@ -1113,7 +1122,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     }
     const int nst = k_b - k_a;
     int tm, tn;
-    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
+    sk_tile(t, sk.tiles_m, sk.tiles_n, sk.gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     // per-lane constants of this tile: A byte offsets (stage 0), pixel coordinates
     unsigned a_off[A_INST_W];
@@ -1462,7 +1471,7 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
   const int w_hi = sk_worker_of((tl + 1) * sk.KS - 1, sk.T, sk.NW);
   if (w_lo == w_hi) return;
   int tm, tn;
-    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
+    sk_tile(t, sk.tiles_m, sk.tiles_n, sk.gm, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const float4* __restrict__ part = reinterpret_cast<const float4*>(sk.part);
   for (int g = blockIdx.x * 256 + threadIdx.x; g < PSZ / 4; g += gridDim.x * 256) {
@@ -1627,7 +1636,7 @@ __global__ void __launch_bounds__(256) k_conv_rg(FwdArgs a, SkArgs sk) {
     const int nst = k_b - k_a;
     it += nst;
     int tm, tn;
-    sk_tile(t, sk.tiles_m, sk.tiles_n, tm, tn);
+    sk_tile(t, sk.tiles_m, sk.tiles_n, sk.gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     // A: instruction wid*A_INST_W + i loads rows of tap block a_tx[i] (wave-uniform)
     unsigned a_off[A_INST_W];
