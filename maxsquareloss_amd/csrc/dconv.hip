@@ -548,12 +548,6 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     sk.tiles_m = pl.tiles_m;
     sk.tiles_n = pl.tiles_n;
     sk.KS = pl.kps;
-    // Tile order (r04): m fastest (every m-block of a pixel block on neighbouring workers of one XCD,
-    // so the image block is fetched once and its re-reads hit that L2) for the pointwise GEMMs, whose
-    // weights fit the L2 anyway, and for the 3x3 GEMMs with >= 4 m-blocks (layer4); n fastest for
-    // layer3's two m-blocks.  Same box: 256 -> 1024 fwd 42.7 vs 49.8 us, 2048 -> 512 dgrad 127 vs 141,
-    // layer4 fwd 214 vs 226, layer3 fwd 77 vs 79 n-fastest; step -0.3 ms (profiles/r04_tile_order_ab.txt)
-    sk.gm = (taps == 1 || pl.tiles_m >= 4) ? pl.tiles_m : 1;
     const long long tiles = (long long)pl.tiles_m * pl.tiles_n;
     if (tiles * sk.KS * kSkNW >= (1LL << 31) || (long long)cimg * P >= (1LL << 29) ||
         (long long)pl.ksteps * kCB * a.lda >= (1LL << 29))
@@ -562,6 +556,14 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     // rest (SkArgs); fewer: pure stream-K.  Every stream-K worker must own at least one iteration:
     // the piece count of a tile is the number of workgroups its iteration range touches.
     sk.tdp = (g_sk_hybrid && tiles >= kSkNW) ? (int)(tiles / kSkNW * kSkNW) : 0;
+    // Tile order (r04): m fastest when whole rounds of tiles run data-parallel (hybrid): one XCD's
+    // workers then hold every m-block of a few pixel blocks, so each image block is fetched once and
+    // re-read from that L2 (same box: 256 -> 1024 fwd 42.7 vs 49.8 us, 2048 -> 512 dgrad 127 vs 141,
+    // layer4 fwd 214 vs 226; profiles/r04_tile_order_ab.txt).  n fastest for pure stream-K: a worker's
+    // range there is under one tile, the m-blocks of a pixel block run at staggered K offsets and get no
+    // L2 reuse, and the shared weights of n fastest win (ASPP fwd, M = 342 over 128 K-steps: 134 vs
+    // 101 us m fastest; layer3 fwd 79 vs 77.7; profiles/r04_aspp_tile_order.txt).
+    sk.gm = sk.tdp > 0 ? pl.tiles_m : 1;
     const long long T = (tiles - sk.tdp) * sk.KS;
     sk.NW = (int)std::min<long long>(kSkNW, T);
     // the remainder after data-parallel rounds (e.g. 16 tiles x 16 K-steps of a 256 -> 1024 pointwise
