@@ -435,28 +435,41 @@ template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk,
                       bool bp = false) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
-    if constexpr ((BM == 128 || BM == 64) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
-      if (bp) {  // the image operand pre-split by k_split_img
-        if (accum)
-          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0, st,
-                             a, sk);
-        else
+    if constexpr (!PW && (BM == 128 || BM == 64) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
+      // (accumulating BD / BP forms at 64 rows only: the pointwise M <= 64 data gradients; no 3x3 call
+      // accumulates, and the 128-row accumulating 3x3 forms are not instantiated)
+      if (bp) {  // the image operand pre-split by k_split_img (never for the pointwise kernels: no BP / BD form)
+        if constexpr (BM == 64) {
+          if (accum) {
+            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0,
+                               st, a, sk);
+            return;
+          }
+        }
+        if (!accum) {
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true, true>), grid, block, 0,
                              st, a, sk);
-        return;
+          return;
+        }
       }
       // the image operand straight to registers (BD form) for the shifted 3x3 rows (dword pieces);
       // the pointwise rows keep their two dwordx4 LDS-DMA pieces per wave and K-step (BD loses there:
       // 256 -> 1024 fwd 32.7 vs 31.0 us, 2048 -> 512 82.7 vs 75.1; layer3 3x3 fwd 52.4 vs 55.0,
       // layer4 172 vs 190; profiles/r03_fwd_forms_ab.txt)
       // (full 16-channel blocks only: the stem's 147-row im2col operand keeps the LDS form)
-      if (!PW && a.cimg % kCB == 0) {
-        if (accum)
-          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a, sk);
-        else
+      if (a.cimg % kCB == 0) {
+        if constexpr (BM == 64) {
+          if (accum) {
+            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a,
+                               sk);
+            return;
+          }
+        }
+        if (!accum) {
           hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true>), grid, block, 0, st, a,
                              sk);
-        return;
+          return;
+        }
       }
     }
     if (accum)

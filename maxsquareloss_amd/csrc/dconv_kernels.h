@@ -1507,263 +1507,6 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Row-grouped stream-K forward form (3x3 convs, 64- or 128-row tiles).  One K-step = (branch, tap
-// row ty, 16-channel block) x the row's three taps = 48 k, k = tx*16 + c inside the step; the A
-// rows are the three 16-row blocks of taps 3ty..3ty+2 in the tap-major pack.  The B operand of a
-// K-step is the union of the three taps' pixel windows, [s, s + BN + 2d) with
-// s = n0 + (ty-1)*d*W - d, staged once per channel row as 16-B chunks that start at the aligned
-// element floor4(ci*P + s): 12 dwordx4 DMA instructions per K-step instead of the 96 dword
-// instructions k_igemm_fwd_sk issues for the same 48 k.  Row c is read at o_c + tx*d + n,
-// o_c = (ci*P + s) & 3; image borders and the row wrap of the linear pixel index are
-// per-(pixel, tap) masks applied to the B reads (the staged window also holds neighbours).
-constexpr int kRgRL = 192;                        // staged floats per channel row (48 chunks)
-constexpr int kRgMaxDil = (kRgRL - 3 - 128) / 2;  // 30: o_c + BN + 2d <= kRgRL
-
-template <int MT, int TM, int TN, int BM, typename F>
-__device__ __forceinline__ void rg_stage(const float* As, const float* Bs,
-                                         int wm, int wn, int lane, int d, const int (&ob)[8],
-                                         const bool (&vt)[TN][3], f32x16 (&acc)[TM][TN], F&& mid) {
-  const int l32 = lane & 31, kh = lane >> 5;
-  if constexpr (MT == kMathF32) {
-    // k-pair kp: half-wave kh takes k = 2kp + kh = tap kp / 8, channel row 2 (kp % 8) + kh
-    const float* Bl = Bs + kh * kRgRL + wn + l32;
-    float av[2][TM], bv[2][TN];
-    auto load = [&](int kp, int buf) {
-      const int tx = kp >> 3, q = kp & 7;
-      const int kr = 2 * kp + kh;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) av[buf][i] = As[kr * BM + wm + i * 32 + l32];
-      const float* src = Bl + 2 * q * kRgRL + ob[q] + tx * d;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const float v = src[j * 32];
-        bv[buf][j] = vt[j][tx] ? v : 0.f;
-      }
-    };
-    load(0, 0);
-#pragma unroll
-    for (int kp = 0; kp < 24; ++kp) {
-      const int cur = kp & 1;
-      if (kp + 1 < 24) load(kp + 1, cur ^ 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
-      if (kp == 0) mid();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-    // one 16-deep K slice per tap: lane (r, h) takes channel rows 8h .. 8h+7
-    typedef typename MathFrag<MT>::type Frag;
-    const float* Bl = Bs + 8 * kh * kRgRL + wn + l32;
-#pragma unroll
-    for (int tx = 0; tx < 3; ++tx) {
-      Frag av[TM], bv[TN];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int kr = tx * 16 + 8 * kh + q;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) frag_set<MT>(av[i], q, As[kr * BM + wm + i * 32 + l32]);
-        const float* src = Bl + q * kRgRL + ob[q] + tx * d;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const float v = src[j * 32];
-          frag_set<MT>(bv[j], q, vt[j][tx] ? v : 0.f);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = frag_mma<MT>(av[i], bv[j], acc[i][j]);
-      if (tx == 0) mid();
-    }
-  }
-}
-
-template <int BM, int BN, int WM, int WN, int MT>
-__global__ void __launch_bounds__(256) k_conv_rg(FwdArgs a, SkArgs sk) {
-  constexpr int BK = 3 * kCB;
-  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && BN == 128 && BM >= 64, "tiles");
-  constexpr int A_STAGE = BK * BM;
-  constexpr int B_INST = kCB * kRgRL / 256;  // dwordx4 wave-instructions per staged B image
-  constexpr int STAGE = A_STAGE + B_INST * 256;
-  constexpr int A_ROWS_PER_INST = 256 / BM;
-  constexpr int A_INST_W = BK / A_ROWS_PER_INST / 4;
-  constexpr int B_INST_W = B_INST / 4;
-  constexpr int CH = kRgRL / 4;  // chunks per staged row
-  static_assert(B_INST % 4 == 0 && (BK / A_ROWS_PER_INST) % 4 == 0, "DMA split over 4 waves");
-  static_assert(kCB % A_ROWS_PER_INST == 0, "an A instruction stays inside one tap block");
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];  // the only LDS object
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
-  const int kh = lane >> 5;
-  const int nb = gridDim.x, b = blockIdx.x;
-  const int w = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);  // XCD-aware worker id
-  const int it_begin = sk_start(w, sk.T, sk.NW), it_end = sk_start(w + 1, sk.T, sk.NW);
-
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.A, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * kCB * a.lda * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
-  constexpr unsigned OOB = 0x80000000u;
-
-  // B chunk loads: instruction wid + 4t covers flat chunks f = (wid + 4t)*64 + lane of the
-  // stage's [16][kRgRL] image (channel row f / CH, chunk f % CH)
-  int b_row[B_INST_W], b_col[B_INST_W];
-#pragma unroll
-  for (int t = 0; t < B_INST_W; ++t) {
-    const int f = (wid + 4 * t) * 64 + lane;
-    b_row[t] = f / CH;
-    b_col[t] = (f - b_row[t] * CH) * 4;
-  }
-  // channel rows this lane reads (f32: 2q + kh; bf16 forms: 8kh + q), times P
-  int rowP[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) rowP[q] = (MT == kMathF32 ? 2 * q + kh : 8 * kh + q) * a.P;
-  const int per_b = 3 * a.ncb;
-  const unsigned blk_bytes = (unsigned)(kCB * a.lda * 4);  // one 16-row K block of the pack
-
-  f32x16 acc[TM][TN];
-  for (int it = it_begin; it < it_end;) {
-    const int t = (unsigned)it / (unsigned)sk.KS;
-    const int k_a = it - t * sk.KS;
-    const int k_b = min(sk.KS, k_a + (it_end - it));
-    const int nst = k_b - k_a;
-    it += nst;
-    int tm, tn;
-    sk_tile(t, sk.tiles_m, sk.tiles_n, sk.gm, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-    // A: instruction wid*A_INST_W + i loads rows of tap block a_tx[i] (wave-uniform)
-    unsigned a_off[A_INST_W];
-    int a_tx[A_INST_W];
-#pragma unroll
-    for (int i = 0; i < A_INST_W; ++i) {
-      const int inst = wid * A_INST_W + i;
-      const int row = inst * A_ROWS_PER_INST + lane / (BM / 4);  // 0 .. 47
-      a_tx[i] = (inst * A_ROWS_PER_INST) / kCB;
-      a_off[i] = (unsigned)(((row % kCB) * a.lda + m0 + (lane % (BM / 4)) * 4) * 4);
-    }
-    int py[TN], px[TN];
-    bool pin[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int p = n0 + wn + j * 32 + (lane & 31);
-      pin[j] = p < a.P;
-      const int pq = p / a.W;
-      px[j] = p - pq * a.W;
-      py[j] = pq % a.H;
-    }
-    // K-step ks -> branch, tap row, channel block, dilation, window start
-    auto decode = [&](int ks, int& br, int& ty, int& cb, int& d, int& s) {
-      br = ks / per_b;
-      const int r2 = ks - br * per_b;
-      ty = r2 / a.ncb;
-      cb = r2 - ty * a.ncb;
-      d = br ? a.dil1 : a.dil0;
-      s = n0 + (ty - 1) * d * a.W - d;
-    };
-    auto issue = [&](int ks, int slot) {
-      float* As = smem + slot * STAGE;
-      float* Bs = As + A_STAGE;
-      int br, ty, cb, d, s;
-      decode(ks, br, ty, cb, d, s);
-      const int blk0 = (br * 9 + 3 * ty) * a.ncb + cb;  // tap-major block of (br, 3ty, cb)
-#pragma unroll
-      for (int i = 0; i < A_INST_W; ++i)
-        dma_b128(ra, As + (wid * A_INST_W + i) * 256,
-                 a_off[i] + (unsigned)(blk0 + a_tx[i] * a.ncb) * blk_bytes);
-#pragma unroll
-      for (int t2 = 0; t2 < B_INST_W; ++t2) {
-        const int ci = cb * kCB + b_row[t2];
-        const int e = ((ci * a.P + s) & ~3) + b_col[t2];  // negative -> out of range -> zeros
-        dma_b128(rb, Bs + (wid + 4 * t2) * 256, ci < a.cimg ? (unsigned)e * 4u : OOB);
-      }
-    };
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    __builtin_amdgcn_s_barrier();  // the previous segment's LDS reads are complete in every wave
-    issue(k_a, 0);
-    for (int i = 0; i < nst; ++i) {
-      wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      const float* As = smem + (i & 1) * STAGE;
-      int br, ty, cb, d, s;
-      decode(k_a + i, br, ty, cb, d, s);
-      const int S = cb * kCB * a.P + s;
-      int ob[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) ob[q] = (rowP[q] + S) & 3;
-      bool vt[TN][3];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const bool vy = pin[j] && (unsigned)(py[j] + (ty - 1) * d) < (unsigned)a.H;
-#pragma unroll
-        for (int tx = 0; tx < 3; ++tx) vt[j][tx] = vy && (unsigned)(px[j] + (tx - 1) * d) < (unsigned)a.W;
-      }
-      auto mid = [&] {
-        if (i + 1 < nst) issue(k_a + i + 1, (i + 1) & 1);
-      };
-      rg_stage<MT, TM, TN, BM>(As, As + A_STAGE, wm, wn, lane, d, ob, vt, acc, mid);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-
-    constexpr int PSZ = BM * BN;
-    if (k_a > 0 || k_b < sk.KS) {
-      // piece of a split tile, row-major [BM][BN], summed by k_sk_reduce (as k_igemm_fwd_sk)
-      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)sk.part, (short)0, (int)min(0x7fffffffLL, (long long)sk.NW * 2 * PSZ * 4), 0x00020000);
-      const unsigned pbase = (unsigned)((w * 2 + (k_a > 0 ? 0 : 1)) * PSZ * 4);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int nl = wn + j * 32 + (lane & 31);
-          const int ml = wm + i * 32 + 4 * kh;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ro = (r & 3) + 8 * (r >> 2);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rp,
-                                                  pbase + (unsigned)(((ml + ro) * BN + nl) * 4), 0, 0);
-          }
-        }
-      continue;
-    }
-    // sole worker of the tile: final output (+ the summed branch biases)
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.C, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn + j * 32 + (lane & 31);
-        const int mrow = m0 + wm + i * 32 + 4 * kh;
-        const unsigned voff = n < a.P ? (unsigned)((mrow * a.P + n) * 4) : OOB;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ro = (r & 3) + 8 * (r >> 2);
-          float v = acc[i][j][r];
-          if (a.bias && mrow + ro < a.M) {
-            float bsum = a.bias[mrow + ro];
-            for (int b2 = 1; b2 < a.nbias; ++b2) bsum += a.bias[b2 * a.M + mrow + ro];
-            v += bsum;
-          }
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc,
-                                                mrow + ro < a.M ? voff + ro * a.P * 4 : OOB, 0, 0);
-        }
-      }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // Stream-K weight gradient.  dW[br][m][n][tap] = sum_p dY[m][p] * X[n][p + shift(br, tap)]:
 // one GEMM tile (BM output channels x BN input channels) per (branch, tap, m-block, n-block),
 // K = pixels in 64-pixel stages.  The (tile, stage) space is cut into NW equal worker ranges
