@@ -392,3 +392,31 @@ def test_dp_bucket_launches_interleave_gloo():
     assert all(bounds[b][1] <= n_early for b in early) and all(bounds[b][1] > n_early for b in late)
     assert sorted(early + late) == [b for b in range(len(bounds)) if has_live[b]]
     assert np.array_equal(flat0, got[1][3])              # both ranks hold the same reduced buffer
+
+
+def _sk_tile(t, tiles_m, tiles_n, gm):
+    """Host restatement of csrc/dconv_kernels.h sk_tile (r04 tile order): gm <= 1 n fastest, else
+    groups of gm m-blocks with m fastest inside a group (the last group may be short)."""
+    if gm <= 1:
+        return t // tiles_n, t % tiles_n
+    g, r = divmod(t, gm * tiles_n)
+    m_in = min(gm, tiles_m - g * gm)
+    tn = r // m_in
+    return g * gm + (r - tn * m_in), tn
+
+
+@pytest.mark.parametrize("tiles_m,tiles_n,gm", [(2, 132, 1), (8, 132, 8), (16, 132, 16), (3, 132, 3),
+                                                (4, 132, 4), (5, 7, 2), (7, 3, 4), (1, 9, 1), (1, 9, 5)])
+def test_sk_tile_order_is_a_bijection(tiles_m, tiles_n, gm):
+    """Every stream-K tile index maps to a distinct (m-block, n-block) in range - a non-bijective order
+    would leave output tiles unwritten - and with gm = tiles_m (the hybrid launches, dconv.hip
+    launch_fwd_form) the m-blocks of one pixel block are consecutive tile indices."""
+    seen = set()
+    for t in range(tiles_m * tiles_n):
+        tm, tn = _sk_tile(t, tiles_m, tiles_n, gm)
+        assert 0 <= tm < tiles_m and 0 <= tn < tiles_n
+        seen.add((tm, tn))
+    assert len(seen) == tiles_m * tiles_n
+    if gm == tiles_m:
+        for t in range(tiles_m * tiles_n):
+            assert _sk_tile(t, tiles_m, tiles_n, gm) == (t % tiles_m, t // tiles_m)
