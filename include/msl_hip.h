@@ -304,6 +304,13 @@ int msl_pconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, i
 int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int cout, int p, int accumulate,
                         void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
                         const float* dy_part, int dy_npart);
+/* 1 if the weight gradient of this conv (taps 9: msl_dconv_wgrad*, h x w maps of nimg images;
+ * taps 1: msl_pconv_wgrad* with p = nimg*h*w) runs the split kernel - whose fp16 form rounds both
+ * operands to fp16 (one power-of-two scale per row) - and 0 if it runs an fp32-accurate tile
+ * kernel (fewer than 128 channels on a side, or too few tiles to fill the chip).  A plan query,
+ * no work: the fp16-operand emulation of the tests (oracle conv_f16) asks it.  MSL_ERR_ARG on bad
+ * dimensions. */
+int msl_conv_wgrad_split(int nbranch, int taps, int cin, int cout, int h, int w, int nimg);
 
 /* ------------------------------------------------------------------------
  * Bilinear upsample, align_corners=True (F.interpolate at deeplab_multi.py:124,

@@ -1116,6 +1116,14 @@ int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, i
 
 static bool bad_parts(const float* p, int n) { return p && n < 1; }
 
+int msl_conv_wgrad_split(int nbranch, int taps, int cin, int cout, int h, int w, int nimg) {
+  if (bad_dims(nbranch, cin, cout, h, w, nimg) || (taps != 1 && taps != 9)) return MSL_ERR_ARG;
+  const int P = nimg * h * w;
+  const int wr = taps == 1 ? P : w;  // a pointwise call passes one flat row (msl_pconv_wgrad*)
+  if (wgrad_swaps(nbranch, taps, cin, cout) && plan_wgrad(nbranch, taps, cout, cin, P, true, wr).rx6) return 1;
+  return plan_wgrad(nbranch, taps, cin, cout, P, true, wr).rx6 ? 1 : 0;
+}
+
 int msl_absmax_partials(const float* x, int rows, int row_len, float* part, msl_stream_t stream) {
   if (!x || !part || rows < 1 || row_len < 1) return MSL_ERR_ARG;
   return absmax_rows(x, rows, row_len, part, as_stream(stream));

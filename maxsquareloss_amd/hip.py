@@ -58,6 +58,7 @@ SIGNATURES = {
     "msl_pconv_fwd_f16": (c_int, [c_p] * 3 + [c_int] * 3 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_dgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_wgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_conv_wgrad_split": (c_int, [c_int] * 7),
     "msl_dconv_fwd_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_wgrad_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_sz, c_p]),

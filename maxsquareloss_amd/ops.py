@@ -300,7 +300,7 @@ class PackBatch:
 
     def _jobs(self):
         out = []
-        for c in self.caches:
+        for c in self.caches + [c._shift.pc for c in self.caches if c._shift is not None]:
             for d in (0, 1):
                 if c.used[d] and c.buf[d] is not None and c.meta[d] is not None:
                     out.append((c, d))
@@ -338,6 +338,9 @@ class PackBatch:
         return tables
 
     def run(self):
+        for c in self.caches:  # the ASPP heads' shift-form layouts first (ops._ShiftPack): their packs follow
+            if c._shift is not None and c._shift.meta is not None:
+                c._shift.refresh()
         jobs, keys = [], []
         for c, d in self._jobs():
             k = c.key_of(c.meta[d][0])
@@ -477,8 +480,17 @@ class _ShiftPack:
         self.key = None
         self.wp = None
         self.pc = PackCache(pointwise=True)
+        self.meta = None  # (weights, cin, c) of the last get(): PackBatch refreshes the layout from them
 
     def get(self, weights, cin, c, for_dgrad):
+        self.meta = (list(weights), cin, c)
+        self.refresh()
+        return self.pc.get([self.wp], cin, 9 * len(weights) * c, for_dgrad)
+
+    def refresh(self):
+        """Rebuild W' if a branch weight changed since (its version bump then makes the packs behind it
+        stale: PackBatch.run packs them with the step's other packs)."""
+        weights, cin, c = self.meta
         key = tuple((w.data_ptr(), w._version) for w in weights)
         nb = len(weights)
         if self.key != key:
@@ -491,9 +503,8 @@ class _ShiftPack:
                 raise hip.MSLError("aspp2: misaligned branch weights")
             hip.check(lib.msl_aspp_weight_layout(wc[0].data_ptr(), stride, nb, c, cin, self.wp.data_ptr(),
                                                  hip.stream_ptr()), "msl_aspp_weight_layout")
-            torch.autograd.graph.increment_version(self.wp)  # the packs below key on it
+            torch.autograd.graph.increment_version(self.wp)  # the packs behind it key on it
             self.key = key
-        return self.pc.get([self.wp], cin, 9 * nb * c, for_dgrad)
 
 
 class _ASPPShift(Function):

@@ -110,32 +110,85 @@ def optim_param_lists(names):
     return g0, g1
 
 
+# --------------------------------------------------------------------------- fp16-operand convs
+def round_f16(t, dim=None):
+    """t rounded to fp16 as the fp16 MFMA path rounds its operands: scaled by a power of two that
+    puts the absolute maximum (of the tensor, or of each slice along `dim`) into [2^14, 2^15),
+    rounded to nearest-even fp16, unscaled - every step exact except the rounding itself."""
+    a = t.detach().abs()
+    if dim is None:
+        m = a.max()
+    else:
+        m = a.transpose(0, dim).reshape(t.shape[dim], -1).max(1)[0]
+        m = m.view([-1 if i == dim else 1 for i in range(t.dim())])
+    m = torch.where(m > 0, m, torch.ones_like(m))
+    sc = torch.ldexp(torch.ones_like(m), 15 - torch.frexp(m).exponent)
+    return ((t * sc).half().to(t.dtype)) / sc
+
+
+class _ConvF16(torch.autograd.Function):
+    """F.conv2d with the operands of every product rounded to fp16 (round_f16), products summed in
+    the working precision: the emulation of BASELINE config 5's fp16 MFMA convs.
+      forward        x (one scale per tensor) * W (one scale per tensor)
+      data gradient  dy (per tensor) * W
+      weight grad    dy (one scale per output channel) * x (one per input channel) when
+                     `wgrad_rounds(cin, cout, h, w)` says so, else exact - as the kernels choose."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding, dilation, wgrad_rounds):
+        ctx.save_for_backward(x, w)
+        ctx.conf = (stride, padding, dilation, b is not None, wgrad_rounds)
+        return F.conv2d(round_f16(x), round_f16(w), b, stride, padding, dilation)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        stride, padding, dilation, has_b, wgrad_rounds = ctx.conf
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.nn.grad.conv2d_input(x.shape, round_f16(w), round_f16(gy), stride, padding, dilation)
+        if ctx.needs_input_grad[1]:
+            rnd = wgrad_rounds(w.shape[1], w.shape[0], w.shape[2], gy.shape[2], gy.shape[3])
+            xr, gr = (round_f16(x, 1), round_f16(gy, 1)) if rnd else (x, gy)
+            gw = torch.nn.grad.conv2d_weight(xr, w.shape, gr, stride, padding, dilation)
+        if has_b and ctx.needs_input_grad[2]:
+            gb = gy.sum((0, 2, 3))
+        return gx, gw, gb, None, None, None, None
+
+
+def conv_f16(wgrad_rounds):
+    """A conv2d(x, w, b, stride, padding, dilation) in the fp16-operand emulation (_ConvF16)."""
+    def conv(x, w, b=None, stride=1, padding=0, dilation=1):
+        return _ConvF16.apply(x, w, b, stride, padding, dilation, wgrad_rounds)
+    return conv
+
+
 # --------------------------------------------------------------------------- forward
 def _bn(x, params, buffers, name, training):
     return F.batch_norm(x, buffers[name + ".running_mean"], buffers[name + ".running_var"],
                         params[name + ".weight"], params[name + ".bias"], training, 0.1, 1e-5)
 
 
-def _bottleneck(x, params, buffers, pre, stride, dil, has_down, training):
-    out = F.conv2d(x, params[pre + "conv1.weight"], stride=stride)
+def _bottleneck(x, params, buffers, pre, stride, dil, has_down, training, conv=F.conv2d):
+    out = conv(x, params[pre + "conv1.weight"], stride=stride)
     out = F.relu(_bn(out, params, buffers, pre + "bn1", training))
-    out = F.conv2d(out, params[pre + "conv2.weight"], padding=dil, dilation=dil)
+    out = conv(out, params[pre + "conv2.weight"], padding=dil, dilation=dil)
     out = F.relu(_bn(out, params, buffers, pre + "bn2", training))
-    out = F.conv2d(out, params[pre + "conv3.weight"])
+    out = conv(out, params[pre + "conv3.weight"])
     out = _bn(out, params, buffers, pre + "bn3", training)
     res = x
     if has_down:
-        res = F.conv2d(x, params[pre + "downsample.0.weight"], stride=stride)
+        res = conv(x, params[pre + "downsample.0.weight"], stride=stride)
         res = _bn(res, params, buffers, pre + "downsample.1", training)
     return F.relu(out + res)
 
 
-def _aspp(x, params, head):
+def _aspp(x, params, head, conv=F.conv2d):
     # Classifier_Module.forward returns after the first loop iteration (deeplab_multi.py:63-66)
-    out = F.conv2d(x, params[f"{head}.conv2d_list.0.weight"], params[f"{head}.conv2d_list.0.bias"],
-                   padding=ASPP_DIL[0], dilation=ASPP_DIL[0])
-    return out + F.conv2d(x, params[f"{head}.conv2d_list.1.weight"], params[f"{head}.conv2d_list.1.bias"],
-                          padding=ASPP_DIL[1], dilation=ASPP_DIL[1])
+    out = conv(x, params[f"{head}.conv2d_list.0.weight"], params[f"{head}.conv2d_list.0.bias"],
+               padding=ASPP_DIL[0], dilation=ASPP_DIL[0])
+    return out + conv(x, params[f"{head}.conv2d_list.1.weight"], params[f"{head}.conv2d_list.1.bias"],
+                      padding=ASPP_DIL[1], dilation=ASPP_DIL[1])
 
 
 def features(params, buffers, x, training=True):
@@ -150,26 +203,27 @@ def features(params, buffers, x, training=True):
     return low
 
 
-def forward_low(params, buffers, x, training=True):
-    """(x2_low, x1_low): the ASPP outputs before upsampling."""
+def forward_low(params, buffers, x, training=True, conv=F.conv2d):
+    """(x2_low, x1_low): the ASPP outputs before upsampling.  `conv` runs every conv but the stem
+    (conv_f16: the fp16 path, whose stem stays fp32)."""
     x = F.conv2d(x, params["conv1.weight"], stride=2, padding=3)
     x = F.relu(_bn(x, params, buffers, "bn1", training))
     x = F.max_pool2d(x, 3, 2, 1, ceil_mode=True)
     for li in range(3):
         for b in range(LAYERS[li]):
             x = _bottleneck(x, params, buffers, f"layer{li + 1}.{b}.", STRIDES[li] if b == 0 else 1,
-                            DILATIONS[li], b == 0, training)
-    x1 = _aspp(x, params, "layer5")
+                            DILATIONS[li], b == 0, training, conv)
+    x1 = _aspp(x, params, "layer5", conv)
     for b in range(LAYERS[3]):
-        x = _bottleneck(x, params, buffers, f"layer4.{b}.", 1, DILATIONS[3], b == 0, training)
-    x2 = _aspp(x, params, "layer6")
+        x = _bottleneck(x, params, buffers, f"layer4.{b}.", 1, DILATIONS[3], b == 0, training, conv)
+    x2 = _aspp(x, params, "layer6", conv)
     return x2, x1
 
 
-def forward(params, buffers, x, training=True):
+def forward(params, buffers, x, training=True, conv=F.conv2d):
     """ResNetMulti.forward (deeplab_multi.py:113-130) -> (x2, x1) upsampled to the input size."""
     hw = x.shape[2:]
-    x2, x1 = forward_low(params, buffers, x, training)
+    x2, x1 = forward_low(params, buffers, x, training, conv)
     up = lambda t: F.interpolate(t, size=hw, mode="bilinear", align_corners=True)  # noqa: E731
     return up(x2), up(x1)
 
@@ -260,9 +314,13 @@ class SGDMult:
 class Model:
     """Parameters + BN buffers as plain tensors (state_dict naming of DeeplabMulti)."""
 
-    def __init__(self, state_dict, num_classes=19, dtype=torch.float32):
+    def __init__(self, state_dict, num_classes=19, dtype=torch.float32, f16_wgrad=None):
+        """f16_wgrad: None = the reference's arithmetic; a predicate (cin, cout, k, h, w) -> bool =
+        the fp16-operand emulation of config 5's conv path (conv_f16), the predicate telling which
+        weight gradients round their operands."""
         self.num_classes = num_classes
         self.dtype = dtype
+        self.conv = F.conv2d if f16_wgrad is None else conv_f16(f16_wgrad)
         names = [n for n, _, _ in param_specs(num_classes)]
         self.names = names
         self.params = {n: state_dict[n].detach().clone().to(dtype) for n in names}
@@ -272,7 +330,7 @@ class Model:
                         for k, v in state_dict.items() if k not in self.params}
 
     def __call__(self, x, training=True):
-        return forward(self.params, self.buffers, x.to(self.dtype), training)
+        return forward(self.params, self.buffers, x.to(self.dtype), training, self.conv)
 
     def state_dict(self):
         sd = {n: p.detach() for n, p in self.params.items()}

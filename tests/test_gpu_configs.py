@@ -8,19 +8,22 @@ BASELINE.json configs, bs=1, counter-generated init, synthetic 
 (configs[0], train_source at 512x256, is tests/test_gpu_parity.py::test_source_step_cfg0_matches_goldens.)
 
 Bars:
-  - fp32 configs (one iteration): the source CE and the target loss within 1e-3 relative of the fp32
-    oracle; the guidance CE within 1e-3 plus the slack of the pixels that sit within rounding of its
+  - fp32 configs (one iteration): the logits x2 / x1 of both images of the iteration's pair
+    (ResNetMulti.forward, deeplab_multi.py:113-130) within 1e-3 normwise of the oracle's at the
+    config's full size; the source CE and the target loss within 1e-3 relative of the fp32 oracle;
+    the guidance CE within 1e-3 plus the slack of the pixels that sit within rounding of its
     threshold / argmax decisions (test_gpu_model._guidance_slack); the IW class histogram within
     0.1 % of the pixels (argmax flips of random-init logits with near-equal classes, Q11); the SGD
     update per tensor within 3x the fp32 oracle's own distance to an fp64 oracle (the bs=1 network
     amplifies fp32 rounding through ~100 BN layers: the stem's weight gradient moves by a few % between
     two fp32 summation orders - tests/test_gpu_model.py), and the whole update within 2x in norm;
   - configs[4] (fp16 operands, fp32 sums; "parity is loss curve vs fp32 CPU within tolerance",
-    SURVEY.md §8d): two iterations, each loss within 1e-2 of the fp32 oracle at iteration 0 and
-    3e-2 at iteration 1 (the oracle re-synced to the GPU's weights in between, so the bar measures
-    one iteration's fp16 rounding; the IW histogram and the update are not held: fp16 operand
-    rounding (2^-11) moves 0.4 % of the random-init argmaxes and, amplified by the bs=1 BN layers,
-    the early layers' gradients).
+    SURVEY.md §8d) against the oracle's fp16-operand emulation (oracle conv_f16: every conv but the
+    stem multiplies operands rounded to fp16 exactly as the kernels round them - the rounding is
+    the only arithmetic difference the fp16 path is allowed, so the emulation holds it to fp32-level
+    bars): the logits within 1e-3 normwise, two iterations (the oracle re-synced to the GPU state
+    between them) with every loss within 1e-3 (+ the guidance slack) and the IW histogram within
+    0.1 % of the pixels; the fp32 oracle's distance is printed beside it.
 The measured values are printed (pytest -s / -rA) so the margins are visible in the log.
 """
 import numpy as np
@@ -30,7 +33,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 from oracle import msl_oracle as orc  # noqa: E402
-from maxsquareloss_amd import ops  # noqa: E402
+from maxsquareloss_amd import hip, ops  # noqa: E402
 from maxsquareloss_amd.tools.solve_gta5 import UDATrainer, build_parser  # noqa: E402
 from maxsquareloss_amd.tools.train_source import init_args  # noqa: E402
 from maxsquareloss_amd.utils.synthetic import synthetic_image, synthetic_labels  # noqa: E402
@@ -42,6 +45,23 @@ CONFIGS = {
     "cfg4_synthia16_1280x760_fp16": dict(w=1280, h=760, C=16, mode="IW_maxsquare", multi=True, lt=0.1,
                                          math="fp16"),
 }
+
+
+def f16_wgrad_policy(num_classes, nimg=2):
+    """The oracle's fp16 emulation predicate (oracle.Model f16_wgrad): whether the GPU's weight gradient
+    of a conv (cin, cout, k, h, w) rounds its operands - asked of the library's own plan
+    (msl_conv_wgrad_split) at the trainer's shapes: image pairs (nimg 2), the ASPP heads in the shift
+    form (one pointwise GEMM with 18 * C rows)."""
+    lib = hip.load(require_gpu=False)
+
+    def rounds(cin, cout, k, h, w):
+        if k == 3 and cout == num_classes and ops.ASPP_FORM == "shift":
+            r = lib.msl_conv_wgrad_split(1, 1, cin, 18 * num_classes, h, w, nimg)
+        else:
+            r = lib.msl_conv_wgrad_split(1, 9 if k == 3 else 1, cin, cout, h, w, nimg)
+        assert r in (0, 1), (cin, cout, k, h, w, r)
+        return bool(r)
+    return rounds
 
 
 def _resync(tr, model, opt):
@@ -56,54 +76,100 @@ def _resync(tr, model, opt):
             opt.buf[n] = st["momentum_buffer"].detach().cpu().clone()
 
 
+def _normwise(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max()).item()
+
+
+def _pair_logits_vs_oracle(tr, model, xs, xt, name):
+    """The trainer's own pair forward (forward_pair, train mode) against the oracle's per-image
+    forward: worst normwise distance of x2 / x1 over both images.  BN running statistics are put
+    back on both sides (the step that follows updates them once)."""
+    bufs = {n: b.detach().clone() for n, b in tr.model.named_buffers()}
+    with torch.no_grad():
+        pairs = tr.model.forward_pair(xs.cuda(), xt.cuda())
+        torch.cuda.synchronize()
+        for n, b in tr.model.named_buffers():
+            b.copy_(bufs[n])
+        worst = 0.0
+        for img, (g2, g1) in zip((xs, xt), pairs):
+            r2, r1 = orc.forward(model.params, {k: v.clone() for k, v in model.buffers.items()}, img, conv=model.conv)
+            for tag, g, r in (("x2", g2, r2), ("x1", g1, r1)):
+                e = _normwise(g, r)
+                print(f"{name} logits {tag}: max|gpu - oracle| / max|oracle| = {e:.2e}")
+                worst = max(worst, e)
+    return worst
+
+
+def _trainer(c):
+    h, w, C = c["h"], c["w"], c["C"]
+    argv = ["--crop_size", f"{w},{h}", "--target_crop_size", f"{w},{h}", "--imagenet_pretrained", "False",
+            "--save_dir", "", "--num_classes", str(C), "--target_mode", c["mode"], "--multi", str(c["multi"]),
+            "--lambda_target", str(c["lt"]), "--conv_math", c["math"], "--iter_max", "200000"]
+    args, _, _ = init_args(build_parser().parse_args(argv))
+    tr = UDATrainer(args, cuda=True)
+    cfg = dict(lr=args.lr, iter_max=200000, lambda_seg=args.lambda_seg, IW_ratio=args.IW_ratio,
+               threshold=args.threshold, target_mode=c["mode"], multi=args.multi, lambda_target=c["lt"])
+    return tr, args, cfg
+
+
+def _hist_flips(tr, out):
+    hg = tr.target_loss.last_hist.cpu().numpy().astype(np.int64)
+    assert hg.sum() == out["hist"].sum()
+    return int(np.abs(hg - out["hist"]).sum()) // 2
+
+
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_config_full_size(name):
     from test_gpu_model import _guidance_slack
     c = CONFIGS[name]
     h, w, C = c["h"], c["w"], c["C"]
     fp16 = c["math"] == "fp16"
-    argv = ["--crop_size", f"{w},{h}", "--target_crop_size", f"{w},{h}", "--imagenet_pretrained", "False",
-            "--save_dir", "", "--num_classes", str(C), "--target_mode", c["mode"], "--multi", str(c["multi"]),
-            "--lambda_target", str(c["lt"]), "--conv_math", c["math"], "--iter_max", "200000"]
-    args, _, _ = init_args(build_parser().parse_args(argv))
-    tr = UDATrainer(args, cuda=True)
+    tr, args, cfg = _trainer(c)
     try:
-        cfg = dict(lr=args.lr, iter_max=200000, lambda_seg=args.lambda_seg, IW_ratio=args.IW_ratio,
-                   threshold=args.threshold, target_mode=c["mode"], multi=args.multi, lambda_target=c["lt"])
         sd0 = {k: v.cpu().clone() for k, v in tr.model.state_dict().items()}
-        model = orc.Model(sd0, C)
+        # fp16: the oracle that rounds the conv operands as the kernels do; the fp32 oracle beside it
+        model = orc.Model(sd0, C, f16_wgrad=f16_wgrad_policy(C) if fp16 else None)
         opt = orc.SGDMult(model.params, model.names, cfg["lr"])
+        m32 = orc.Model(sd0, C) if fp16 else None
+        opt32 = orc.SGDMult(m32.params, m32.names, cfg["lr"]) if fp16 else None
         m64 = None if fp16 else orc.Model(sd0, C, dtype=torch.float64)
         opt64 = None if fp16 else orc.SGDMult(m64.params, m64.names, cfg["lr"])
         tr.optimizer.zero_grad()
         for it in range(2 if fp16 else 1):
             if it:
                 _resync(tr, model, opt)
+                _resync(tr, m32, opt32)
             p0 = {n: p.detach().cpu().clone() for n, p in tr.model.named_parameters()}
             xs, ys = synthetic_image(h, w, 7 + it), synthetic_labels(h, w, C, 7 + it)
             xt = synthetic_image(h, w, 507 + it)
+            if it == 0:
+                # north_star: logits within 1e-3 of the reference path on identical inputs at full size
+                assert _pair_logits_vs_oracle(tr, model, xs, xt, name) < 1e-3
             tr.uda_step(xs.cuda(), ys.cuda(), xt.cuda())
             torch.cuda.synchronize()
             slack = (_guidance_slack(model, xt, cfg["threshold"], cfg["lambda_seg"] * c["lt"]) if args.multi else 0.0)
             out = orc.uda_step(model, opt, xs, ys, xt, cfg, it)
+            out32 = orc.uda_step(m32, opt32, xs, ys, xt, cfg, it) if fp16 else None
             if m64 is not None:
                 orc.uda_step(m64, opt64, xs, ys, xt, cfg, it)
-            tol = (1e-2 if it == 0 else 3e-2) if fp16 else 1e-3
             mine = {"loss_seg": tr.loss_val.item(), "loss_target": tr.loss_target.item()}
             if args.multi:
                 mine["loss_target_2"] = tr.loss_target_2.item()
             for k, v in mine.items():
                 rel = abs(v - out[k]) / max(abs(out[k]), 1e-30)
-                print(f"{name} it{it} {k}: gpu {v:.7g} oracle {out[k]:.7g} rel {rel:.2e} (slack {slack:.2e})")
+                extra = ""
+                if fp16:
+                    extra = f" | fp32 oracle {out32[k]:.7g} rel {abs(v - out32[k]) / max(abs(out32[k]), 1e-30):.2e}"
+                print(f"{name} it{it} {k}: gpu {v:.7g} oracle{'-fp16' if fp16 else ''} {out[k]:.7g} rel {rel:.2e} "
+                      f"(slack {slack:.2e}){extra}")
                 ab = slack if k == "loss_target_2" else 0.0
-                assert v == pytest.approx(out[k], rel=tol, abs=ab), (name, it, k, v, out[k])
+                assert v == pytest.approx(out[k], rel=1e-3, abs=ab), (name, it, k, v, out[k])
             if c["mode"] == "IW_maxsquare":
-                hg = tr.target_loss.last_hist.cpu().numpy().astype(np.int64)
-                flips = int(np.abs(hg - out["hist"]).sum()) // 2
-                print(f"{name} it{it} IW histogram: {flips} argmax flips of {h * w} pixels")
-                assert hg.sum() == out["hist"].sum() == h * w
-                if not fp16:
-                    assert flips <= 0.001 * h * w, (name, hg, out["hist"])
+                flips = _hist_flips(tr, out)
+                extra = f" (fp32 oracle: {_hist_flips(tr, out32)})" if fp16 else ""
+                print(f"{name} it{it} IW histogram: {flips} argmax flips of {h * w} pixels{extra}")
+                assert flips <= 0.001 * h * w, (name, it, flips)
             if m64 is None:
                 continue
             e_gpu_all = e_cpu_all = 0.0
@@ -134,51 +200,69 @@ def test_config_full_size(name):
 def test_config5_fp16_loss_curve():
     """configs[4]'s parity criterion, "loss curve vs fp32 CPU within tolerance" (SURVEY.md §8d), at a
     reduced 16-class size (640x380, the same 16-class heads, IW + multi, every conv on the fp16 MFMA
-    path; tools/solve_gta5.py:335-387):
-      - ten iterations with the fp32 oracle re-synced to the GPU state before each one: every
-        iteration's losses within 1e-2 of the oracle's (one iteration's fp16 operand rounding), the
-        guidance CE with its threshold slack on top, the IW histogram within 2 % of the pixels;
-      - then five iterations WITHOUT re-syncing (both sides from the same state): the curve's drift
-        printed per iteration and held within 2e-1 relative - fp16 rounding compounds through the
-        updates of a random-init bs=1 network, and the IW argmax weights and the guidance threshold
-        make the free trajectory chaotic: two stream-K partitions of the same fp16 GEMMs (r04) drifted
-        1.7e-2 and 8.9e-2 on loss_target_2 by the fifth free iteration; no divergence."""
+    path; tools/solve_gta5.py:335-387), measured against the envelope of a correct fp16 implementation
+    - the oracle's fp16-operand emulation (oracle conv_f16), which rounds every conv operand as the
+    kernels do and differs from them only in fp32 summation order:
+      - iterations 0-9 with the emulation re-synced to the GPU state before each one: every loss
+        within 1e-3 of the emulation's (the guidance CE with its threshold slack on top), the IW
+        histogram within 0.1 % of the pixels - fp32-level bars: an fp16 error source the kernels do not
+        share with the emulation fails here;
+      - iterations 10-14 with the emulation AND the fp32 oracle started from the GPU state at iteration
+        10 and run free: per loss and iteration, the GPU's distance from the fp32 oracle within twice
+        the largest distance the emulation has reached from it so far, plus 1e-3 (one iteration's
+        fp32-level noise) and the guidance slack - the fp16 drift of the curve is what a correct fp16
+        implementation shows, not a fixed bar.  The trajectory of a random-init bs=1 network is chaotic
+        (the IW argmax weights and the guidance threshold amplify rounding), so the envelope is the
+        emulation's own drift, printed per iteration."""
     from test_gpu_model import _guidance_slack
     h, w, C = 380, 640, 16
-    argv = ["--crop_size", f"{w},{h}", "--target_crop_size", f"{w},{h}", "--imagenet_pretrained", "False",
-            "--save_dir", "", "--num_classes", str(C), "--target_mode", "IW_maxsquare", "--multi", "True",
-            "--lambda_target", "0.1", "--conv_math", "fp16", "--iter_max", "200000"]
-    args, _, _ = init_args(build_parser().parse_args(argv))
-    tr = UDATrainer(args, cuda=True)
+    c = dict(w=w, h=h, C=C, mode="IW_maxsquare", multi=True, lt=0.1, math="fp16")
+    tr, args, cfg = _trainer(c)
     try:
-        cfg = dict(lr=args.lr, iter_max=200000, lambda_seg=args.lambda_seg, IW_ratio=args.IW_ratio,
-                   threshold=args.threshold, target_mode="IW_maxsquare", multi=True, lambda_target=0.1)
-        model = orc.Model({k: v.cpu().clone() for k, v in tr.model.state_dict().items()}, C)
-        opt = orc.SGDMult(model.params, model.names, cfg["lr"])
+        sd = {k: v.cpu().clone() for k, v in tr.model.state_dict().items()}
+        m16 = orc.Model(sd, C, f16_wgrad=f16_wgrad_policy(C))
+        opt16 = orc.SGDMult(m16.params, m16.names, cfg["lr"])
+        m32 = orc.Model(sd, C)
+        opt32 = orc.SGDMult(m32.params, m32.names, cfg["lr"])
         tr.optimizer.zero_grad()
         keys = ("loss_seg", "loss_target", "loss_target_2")
+        env = dict.fromkeys(keys, 0.0)  # the emulation's largest relative drift from the fp32 oracle so far
         for it in range(15):
             resync = it < 10
-            if resync:
-                _resync(tr, model, opt)
+            if it <= 10:
+                _resync(tr, m16, opt16)
+            if it == 10:
+                _resync(tr, m32, opt32)
             xs, ys = synthetic_image(h, w, 40 + it), synthetic_labels(h, w, C, 40 + it)
             xt = synthetic_image(h, w, 540 + it)
             tr.uda_step(xs.cuda(), ys.cuda(), xt.cuda())
             torch.cuda.synchronize()
-            slack = _guidance_slack(model, xt, cfg["threshold"], cfg["lambda_seg"] * cfg["lambda_target"])
-            out = orc.uda_step(model, opt, xs, ys, xt, cfg, it)
             mine = dict(zip(keys, (tr.loss_val.item(), tr.loss_target.item(), tr.loss_target_2.item())))
-            hg = tr.target_loss.last_hist.cpu().numpy().astype(np.int64)
-            flips = int(np.abs(hg - out["hist"]).sum()) // 2
-            rels = {k: abs(mine[k] - out[k]) / max(abs(out[k]), 1e-30) for k in keys}
-            print(f"cfg5 fp16 it{it} {'resynced' if resync else 'free'}: " +
-                  " ".join(f"{k} {mine[k]:.6g}/{out[k]:.6g} ({rels[k]:.1e})" for k in keys) +
-                  f" IW flips {flips} of {h * w} (guidance slack {slack:.1e})")
-            tol = 1e-2 if resync else 2e-1
-            for k in keys:
-                ab = slack if k == "loss_target_2" else 0.0
-                assert mine[k] == pytest.approx(out[k], rel=tol, abs=ab), (it, k, mine[k], out[k])
             if resync:
-                assert flips <= 0.02 * h * w, (it, flips)
+                slack = _guidance_slack(m16, xt, cfg["threshold"], cfg["lambda_seg"] * cfg["lambda_target"])
+                out = orc.uda_step(m16, opt16, xs, ys, xt, cfg, it)
+                flips = _hist_flips(tr, out)
+                rels = {k: abs(mine[k] - out[k]) / max(abs(out[k]), 1e-30) for k in keys}
+                print(f"cfg5 fp16 it{it} resynced vs emulation: " +
+                      " ".join(f"{k} {mine[k]:.6g}/{out[k]:.6g} ({rels[k]:.1e})" for k in keys) +
+                      f" IW flips {flips} of {h * w} (guidance slack {slack:.1e})")
+                for k in keys:
+                    ab = slack if k == "loss_target_2" else 0.0
+                    assert mine[k] == pytest.approx(out[k], rel=1e-3, abs=ab), (it, k, mine[k], out[k])
+                assert flips <= 0.001 * h * w, (it, flips)
+                continue
+            slack = _guidance_slack(m32, xt, cfg["threshold"], cfg["lambda_seg"] * cfg["lambda_target"])
+            o16 = orc.uda_step(m16, opt16, xs, ys, xt, cfg, it)
+            o32 = orc.uda_step(m32, opt32, xs, ys, xt, cfg, it)
+            line = []
+            for k in keys:
+                ref = max(abs(o32[k]), 1e-30)
+                d_gpu, d16 = abs(mine[k] - o32[k]) / ref, abs(o16[k] - o32[k]) / ref
+                env[k] = max(env[k], d16)
+                bar = 2 * env[k] + 1e-3 + (slack / ref if k == "loss_target_2" else 0.0)
+                line.append(f"{k} gpu {d_gpu:.1e} emul {d16:.1e} bar {bar:.1e} (gpu-emul "
+                            f"{abs(mine[k] - o16[k]) / ref:.1e})")
+                assert d_gpu <= bar, (it, k, mine[k], o16[k], o32[k])
+            print(f"cfg5 fp16 it{it} free, drift from the fp32 oracle: " + "; ".join(line))
     finally:
         ops.set_conv_math("fp32")

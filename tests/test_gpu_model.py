@@ -44,7 +44,8 @@ def _guidance_slack(model, xt, thr, scale, eps=5e-4):
     > 0.95 while x1 disagrees), so the bar is the sum of their possible contributions."""
     import torch.nn.functional as F
     with torch.no_grad():
-        r2, r1 = orc.forward(model.params, model.buffers, xt)
+        bufs = {k: v.clone() for k, v in model.buffers.items()}  # (train mode updates the running stats)
+        r2, r1 = orc.forward(model.params, bufs, xt, conv=model.conv)
         P, P2 = F.softmax(r2, 1), F.softmax(r1, 1)
         mp, mp2 = P.max(1)[0], P2.max(1)[0]
         top2, cls2 = ((P + P2) / 2).topk(2, dim=1)

@@ -153,7 +153,57 @@ def test_aspp_shift_form_matches_direct(cin, c, h, w, n, d0, d1, monkeypatch):
         assert _rel(a, b) < 1e-5, i
 
 
-@pytest.mark.parametrize("c,hi,wi,ho,wo", [(19, 65, 129, 512, 1024), (19, 33, 65, 256, 512), (16, 81, 161, 640, 1280), (3, 5, 7, 11, 13)])
+@pytest.mark.parametrize("math", ["bf16", "fp16"])
+@pytest.mark.parametrize("cin,c,h,w,n,d0,d1", [(2048, 19, 65, 129, 2, 6, 12), (1024, 16, 96, 161, 2, 6, 12),
+                                              (256, 19, 9, 17, 1, 6, 12), (128, 5, 13, 7, 2, 2, 5)])
+def test_aspp_shift_form_low_precision(math, cin, c, h, w, n, d0, d1):
+    """The shift form of the heads in the bf16 and fp16 conv maths against fp64 convs on
+    the operands as its GEMMs round them: bf16 = RNE of every operand; fp16 = x and the head's stacked
+    weight W' (both branches: one tensor, one scale) per tensor, dY per tensor for the data gradient
+    (W'^T G, K = 18*C - not a multiple of 16 for C = 19 or 5), and per row of dY and x for the weight
+    gradient where the plan runs the split kernel (msl_conv_wgrad_split; exact below 128 rows, C = 5).
+    The only admissible difference is the fp32 accumulation (1e-5 of max|ref|)."""
+    from oracle.msl_oracle import round_f16
+    from maxsquareloss_amd import hip
+    g = torch.Generator().manual_seed(cin + 3 * c + h)
+    shape = (1, cin, n, h, w) if n > 1 else (1, cin, h, w)
+    x = torch.relu(torch.randn(shape, generator=g))
+    ws = [torch.randn(c, cin, 3, 3, generator=g) * 0.01 for _ in range(2)]
+    bs = [torch.randn(c, generator=g) for _ in range(2)]
+    gy = torch.randn((1, c) + shape[2:], generator=g) * 1e-4
+    ops.set_conv_math(math)
+    try:
+        leaves = [t.to(DEV).requires_grad_() for t in (x, ws[0], bs[0], ws[1], bs[1])]
+        y = ops.aspp2(*leaves, d0, d1, ops.PackCache())
+        y.backward(gy.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        ops.set_conv_math("fp32")
+    batch = lambda t: t[0].transpose(0, 1) if n > 1 else t  # noqa: E731  [C][N][H][W] -> (N, C, H, W)
+    xb, gb = batch(x).double(), batch(gy).double()
+    if math == "bf16":
+        rx = rd = _bf(xb)
+        rws = rwd = [_bf(t) for t in ws]
+        rgd = rgw = _bf(gb)
+    else:
+        wst = round_f16(torch.stack(ws).double())
+        rx, rws, rwd, rgd = round_f16(xb), list(wst), list(wst), round_f16(gb)
+        split = hip.load().msl_conv_wgrad_split(1, 1, cin, 18 * c, h, w, n)
+        rd, rgw = (round_f16(xb, 1), round_f16(gb, 1)) if split else (xb, gb)
+    conv = lambda a, wt, dd: F.conv2d(a, wt, padding=dd, dilation=dd)  # noqa: E731
+    yr = conv(rx, rws[0], d0) + conv(rx, rws[1], d1) + (bs[0] + bs[1]).double().view(1, -1, 1, 1)
+    assert _rel(batch(y.detach().cpu()), yr) < 1e-5
+    xr = rx.clone().requires_grad_()
+    (conv(xr, rwd[0], d0) + conv(xr, rwd[1], d1)).backward(rgd)
+    assert _rel(batch(leaves[0].grad.cpu()), xr.grad) < 1e-5
+    for i, (wt, dd) in enumerate(((ws[0], d0), (ws[1], d1))):
+        wr = wt.double().requires_grad_()
+        conv(rd, wr, dd).backward(rgw)
+        assert _rel(leaves[1 + 2 * i].grad, wr.grad) < 1e-5, i
+        assert _rel(leaves[2 + 2 * i].grad, gb.sum((0, 2, 3))) < 1e-5, i
+
+
+@pytest.mark.parametrize("c,hi,wi,ho,wo",[(19, 65, 129, 512, 1024), (19, 33, 65, 256, 512), (16, 81, 161, 640, 1280), (3, 5, 7, 11, 13)])
 def test_upsample(c, hi, wi, ho, wo):
     g = torch.Generator().manual_seed(hi)
     x = torch.randn(1, c, hi, wi, generator=g) * 3

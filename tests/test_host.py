@@ -420,3 +420,20 @@ def test_sk_tile_order_is_a_bijection(tiles_m, tiles_n, gm):
     if gm == tiles_m:
         for t in range(tiles_m * tiles_n):
             assert _sk_tile(t, tiles_m, tiles_n, gm) == (t % tiles_m, t // tiles_m)
+
+
+def test_wgrad_split_plan_query():
+    """msl_conv_wgrad_split (a host-only plan query): the split (fp16-rounding in the fp16 math) weight
+    gradient runs where both sides have >= 128 channels and its items fill the chip - layer3 / layer4 and
+    the wide 1x1 convs at the 1024x512 pair - and the fp32-accurate tiles below 128 channels."""
+    from maxsquareloss_amd import hip
+    lib = hip.load(require_gpu=False)
+    assert lib.msl_conv_wgrad_split(1, 9, 256, 256, 65, 129, 2) == 1    # layer3 3x3
+    assert lib.msl_conv_wgrad_split(1, 9, 512, 512, 65, 129, 2) == 1    # layer4 3x3
+    assert lib.msl_conv_wgrad_split(1, 1, 1024, 256, 65, 129, 2) == 1   # layer3 conv1
+    assert lib.msl_conv_wgrad_split(1, 1, 256, 1024, 65, 129, 2) == 1   # layer3 conv3 (swapped operands)
+    assert lib.msl_conv_wgrad_split(1, 1, 2048, 342, 65, 129, 2) == 1   # layer6 head, shift form
+    assert lib.msl_conv_wgrad_split(1, 9, 64, 64, 129, 257, 2) == 0     # layer1 3x3
+    assert lib.msl_conv_wgrad_split(1, 1, 64, 256, 129, 257, 2) == 0    # layer1 conv3
+    assert lib.msl_conv_wgrad_split(1, 9, 64, 64, 0, 257, 2) == -3      # bad dimensions
+    assert lib.msl_conv_wgrad_split(1, 3, 64, 64, 9, 9, 1) == -3        # 1 or 9 taps only

@@ -224,3 +224,49 @@ def test_preprocess_kat():
                     assert np.array_equal(lut[d].astype(np.float32), want), key
                     n += 1
     assert n == 3 * 2 * 8
+
+
+def test_round_f16_is_fp16_rounding_under_a_pow2_scale():
+    """oracle.round_f16 (the fp16 path's operand rounding, emulated): the absolute maximum lands in
+    [2^14, 2^15) after scaling, every value is an fp16 number times the inverse scale, rounding is to
+    nearest (|error| <= half an fp16 ulp of the scaled value), per-row scales along `dim`."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4, 7, 5, 6, generator=g) * torch.logspace(-8, 3, 4).view(4, 1, 1, 1)
+    for dim in (None, 0, 1):
+        r = orc.round_f16(x, dim)
+        if dim is None:
+            m = x.abs().max().view(1, 1, 1, 1)
+        else:
+            m = x.abs().transpose(0, dim).reshape(x.shape[dim], -1).max(1)[0]
+            m = m.view([-1 if i == dim else 1 for i in range(4)])
+        sc = torch.ldexp(torch.ones_like(m), 15 - torch.frexp(m).exponent)
+        assert bool(((m * sc >= 2 ** 14) & (m * sc < 2 ** 15)).all())
+        s = (r * sc).double()
+        assert torch.equal(s, s.half().double())  # representable in fp16
+        ulp = torch.ldexp(torch.ones_like(s), torch.frexp((x * sc).abs().clamp_min(2 ** -14)).exponent - 11)
+        assert bool(((s - (x * sc).double()).abs() <= ulp.double() / 2 + 1e-30).all())
+    assert torch.equal(orc.round_f16(orc.round_f16(x)), orc.round_f16(x))  # idempotent
+
+
+def test_conv_f16_emulation_rounds_every_product_operand():
+    """oracle.conv_f16: forward = conv of the rounded operands; data gradient = transposed conv of the
+    rounded dy and W; weight gradient from per-channel-rounded x and dy when the predicate says the
+    kernel rounds them, exact otherwise; the bias gradient exact."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(1, 8, 9, 11, generator=g)
+    w = torch.randn(6, 8, 3, 3, generator=g) * 0.01
+    b = torch.randn(6, generator=g)
+    gy = torch.randn(1, 6, 9, 11, generator=g) * 1e-5
+    for rounds in (True, False):
+        seen = []
+        conv = orc.conv_f16(lambda *a: seen.append(a) or rounds)
+        xv, wv, bv = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+        y = conv(xv, wv, bv, 1, 2, 2)
+        assert torch.equal(y, F.conv2d(orc.round_f16(x), orc.round_f16(w), b, 1, 2, 2))
+        y.backward(gy)
+        assert seen == [(8, 6, 3, 9, 11)]
+        gx = torch.nn.grad.conv2d_input(x.shape, orc.round_f16(w), orc.round_f16(gy), 1, 2, 2)
+        xr, gr = (orc.round_f16(x, 1), orc.round_f16(gy, 1)) if rounds else (x, gy)
+        gw = torch.nn.grad.conv2d_weight(xr, w.shape, gr, 1, 2, 2)
+        assert torch.equal(xv.grad, gx) and torch.equal(wv.grad, gw)
+        assert torch.equal(bv.grad, gy.sum((0, 2, 3)))
