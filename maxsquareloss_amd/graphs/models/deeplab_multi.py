@@ -185,10 +185,14 @@ class ResNetMulti(nn.Module):
     def _make_pred_layer(self, block, inplanes, dilation_series, padding_series, num_classes):
         return block(inplanes, dilation_series, padding_series, num_classes)
 
-    # with keep_split, _heads leaves layer3's output in split_out: the point where a data-parallel step
-    # splits its backward in two (utils/graph.py: the gradients of layer4 and the heads are exchanged
-    # while the backward through layer3 .. the stem runs)
+    # With keep_split, _heads cuts the graph at layer3's output and after the layer3 blocks in split_cuts:
+    # the points where a captured data-parallel step splits its backward into segments (utils/graph.py),
+    # so the gradients each segment finishes (layer4 and the heads; then groups of layer3 blocks) are
+    # exchanged while the next segments' backward runs.  split_out: the cuts' (x, leaf) pairs in forward
+    # order.  r05: cuts after blocks 14, 6 and 2 leave 11.9 % of the live gradient bytes (layer3.0-2,
+    # layer2, layer1, the stem) to the last segment.
     keep_split = False
+    split_cuts = (14, 6, 2)
     split_out = None
 
     def split_params(self):
@@ -196,20 +200,39 @@ class ResNetMulti(nn.Module):
         output: layer4 and both heads."""
         return [p for m in (self.layer4, self.layer5, self.layer6) for p in m.parameters() if p.requires_grad]
 
+    def split_segments(self):
+        """The trainable parameters each segment of the split backward finishes, in backward order:
+        [layer4 + heads, layer3 blocks after the last cut, ..., after the first cut]; the last segment
+        (layer3 up to the first cut, layer2, layer1, the stem) finishes the rest."""
+        groups, hi = [self.split_params()], len(self.layer3)
+        for c in sorted(self.split_cuts, reverse=True):
+            groups.append([p for b in range(c + 1, hi) for p in self.layer3[b].parameters() if p.requires_grad])
+            hi = c + 1
+        return groups
+
+    def _cut(self, x):
+        """A detached leaf standing in for x downstream: the backward of what reads it stops there
+        (backward(inputs=[x]) would run x's own node, a BN), and its .grad seeds the next segment."""
+        xd = x.detach().requires_grad_()
+        if hasattr(x, "_msl_absmax"):
+            xd._msl_absmax = x._msl_absmax  # the BN's absmax tag (same version counter)
+        self.split_out.append((x, xd))
+        return xd
+
     def _heads(self, x):
         """The trunk and both heads on (1,3,H,W) or an image batch (1,3,N,H,W): (layer6, layer5)
         low-resolution logits."""
         x = self.maxpool(ops.bn_act(self.bn1, self.conv1(x), relu=True))
         x = self.layer1(x)
         x = self.layer2(x)
-        x = self.layer3(x)
         if self.keep_split:
-            # the heads read a detached leaf: their backward stops there (backward(inputs=[x]) would
-            # run x's own node, layer3's last BN), and its .grad seeds the trunk's backward
-            xd = x.detach().requires_grad_()
-            if hasattr(x, "_msl_absmax"):
-                xd._msl_absmax = x._msl_absmax  # the BN's absmax tag (same version counter)
-            self.split_out, x = (x, xd), xd
+            self.split_out = []
+            for i, blk in enumerate(self.layer3):
+                x = blk(x)
+                if i in self.split_cuts or i == len(self.layer3) - 1:
+                    x = self._cut(x)
+        else:
+            x = self.layer3(x)
         x1 = self.layer5(x)
         x2 = self.layer4(x)
         x2 = self.layer6(x2)

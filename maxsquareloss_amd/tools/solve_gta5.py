@@ -22,6 +22,7 @@ validation/eval path are out of scope.
 import argparse
 import os
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -126,13 +127,18 @@ class UDATrainer(Trainer):
                 if self.reducer is None:
                     self._graphed = GraphedStep(self, self._uda_body)
                 elif self.pair and x_s.shape == x_t.shape and self._split_ok():
-                    # the backward captured in two segments split at layer3's output: the gradients of
-                    # layer4 and the heads are exchanged while the rest of the backward replays
-                    n_early = len(self.model.split_params())
+                    # the backward captured in segments split at layer3's output and inside layer3 (the
+                    # model's split_cuts): the gradients each segment finished are exchanged while the
+                    # next segments replay
+                    ends = list(np.cumsum([len(g) for g in self.model.split_segments()]))
+                    self.reducer.set_breaks(ends)
+                    red = self.reducer
+                    between = [lambda n=ends[0]: red.reduce_early(n)]
+                    between += [lambda n=n: red.reduce_more(n) for n in ends[1:]]
                     self._graphed = GraphedStep(
                         self, self._uda_grads, update=self._uda_update,
-                        segments=[self._uda_grads_head, self._uda_grads_trunk],
-                        between=[lambda: self.reducer.reduce_early(n_early), self.reducer.reduce_rest])
+                        segments=[self._uda_grads_head] + [self._uda_grads_trunk] * len(ends),
+                        between=between + [red.reduce_rest])
                 else:
                     self._graphed = GraphedStep(self, self._uda_grads, exchange=self.reducer.reduce_all,
                                                 update=self._uda_update)
@@ -192,16 +198,22 @@ class UDATrainer(Trainer):
         ops.wgrad_join(self.device)  # the side-stream weight gradients (ops.ASYNC_WGRAD) rejoin
 
     def _split_ok(self):
-        """Whether the parameters finished at layer3's output lead the flat gradient buffer (its
-        backward order), so reduce_early's buckets hold final gradients only."""
-        early = {id(p) for p in self.model.split_params()}
-        first = self.optimizer.grads.params[:len(early)]
-        return len(early) > 0 and {id(p) for p in first} == early
+        """Whether the parameters each backward segment finishes (model.split_segments) lead the flat
+        gradient buffer (its backward order) in segment order, so the buckets launched after a segment
+        hold final gradients only."""
+        order = [id(p) for p in self.optimizer.grads.params]
+        k = 0
+        for grp in self.model.split_segments():
+            ids = {id(p) for p in grp}
+            if not ids or set(order[k:k + len(ids)]) != ids:
+                return False
+            k += len(ids)
+        return True
 
     def _uda_grads_head(self, x_s, y_s, x_t):
         """The pair's forward and the backward through the heads and layer4, stopping at layer3's
-        output (its gradient kept for _uda_grads_trunk): the first segment of a captured data-parallel
-        step (utils/graph.py).  The two segments run exactly the kernels of _uda_grads, in its order."""
+        output (the cuts kept for _uda_grads_trunk): the first segment of a captured data-parallel step
+        (utils/graph.py).  The segments run exactly the kernels of _uda_grads, in its order."""
         m = self.model
         m.keep_split = True
         try:
@@ -217,10 +229,11 @@ class UDATrainer(Trainer):
         self._split = split
 
     def _uda_grads_trunk(self):
-        """The rest of the backward: from layer3's output through layer3 .. the stem."""
-        (x3, xd), self._split = self._split, None
+        """The next segment of the backward: from the last remaining cut back to the one before it (the
+        last segment: through layer3's first blocks .. the stem)."""
+        x, xd = self._split.pop()
         g, xd.grad = xd.grad, None
-        torch.autograd.backward([x3], [g])
+        torch.autograd.backward([x], [g])
         ops.wgrad_join(self.device)
 
     def _uda_update(self):

@@ -25,10 +25,13 @@ Captured steps (utils/graph.py, --graph): the bucket countdown is host-driven, s
 cannot launch collectives from inside the backward.  There the reducer is `deferred` while the
 iteration is captured (no hook launches anything) and the backward is captured as two graphs, split at
 layer3's output (r04): the first (forward + the backward through the heads and layer4) leaves the
-gradients of the first `n_early` parameters in backward order final, `reduce_early()` all-reduces the
-buckets made of those alone on RCCL's stream while the second graph (the backward through layer3 ..
-the stem) replays on the compute stream, and `reduce_rest()` launches the remaining buckets and joins
-the exchange before the SGD graph.  Without a split (two-pass mode) `reduce_all()` exchanges every
+gradients of the first `n_early` parameters in backward order final, and `reduce_early()` all-reduces
+the buckets made of those alone on RCCL's stream while the next graph replays on the compute stream.
+r05: the backward is also cut inside layer3 (the model's split_cuts); after each further segment
+`reduce_more()` launches the buckets it finished (bucket bounds end at every segment's end,
+`set_breaks`), and `reduce_rest()` launches the rest after the last segment and joins the exchange
+before the SGD graph: 88 % of the live gradient bytes are launched before the last segment (layer3.0-2,
+layer2, layer1, the stem) replays.  Without a split (two-pass mode) `reduce_all()` exchanges every
 bucket after the backward.
 """
 import numpy as np
@@ -42,25 +45,33 @@ class GradReducer:
         self.flat = optimizer.grads
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-        cap = int(bucket_cap_mb * 1024 * 1024 / 4)
-        # buckets = contiguous parameter ranges of ~cap elements in flat (backward) order
-        self.bucket_of = np.zeros(len(self.flat.params), dtype=np.int64)
-        bounds, start_p, acc = [], 0, 0
-        for i, p in enumerate(self.flat.params):
-            acc += p.numel()
-            self.bucket_of[i] = len(bounds)
-            if acc >= cap:
-                bounds.append((start_p, i + 1))
-                start_p, acc = i + 1, 0
-        if start_p < len(self.flat.params):
-            bounds.append((start_p, len(self.flat.params)))
-        self.bounds = bounds
+        self.cap = int(bucket_cap_mb * 1024 * 1024 / 4)
+        self.set_breaks([])
         self.live = None        # bool mask of parameters that receive gradients
         self.armed = False
         self.works = []
         self.deferred = False   # True while a graph captures the backward (utils/graph.py)
         self.flat.listeners.append(self._on_grad)
         optimizer.grad_scale = 1.0 / self.world
+
+    def set_breaks(self, breaks):
+        """Buckets = contiguous parameter ranges of ~cap elements in flat (backward) order that also
+        end at every index in `breaks` (the parameter counts a split backward's segments finish, so no
+        bucket waits for a later segment)."""
+        ends = set(int(b) for b in breaks)
+        self.bucket_of = np.zeros(len(self.flat.params), dtype=np.int64)
+        bounds, start_p, acc = [], 0, 0
+        for i, p in enumerate(self.flat.params):
+            acc += p.numel()
+            self.bucket_of[i] = len(bounds)
+            if acc >= self.cap or (i + 1) in ends:
+                bounds.append((start_p, i + 1))
+                start_p, acc = i + 1, 0
+        if start_p < len(self.flat.params):
+            bounds.append((start_p, len(self.flat.params)))
+        self.bounds = bounds
+        if getattr(self, "live", None) is not None:
+            self.has_live = [bool(self.live[lo:hi].any()) for lo, hi in self.bounds]
 
     def _elem_range(self, b):
         lo, hi = self.bounds[b]
@@ -129,6 +140,14 @@ class GradReducer:
         self.works = []
         self.next = 0
         while self.next < len(self.bounds) and self.bounds[self.next][1] <= n_early:
+            if self.has_live[self.next]:
+                self._launch(self.next)
+            self.next += 1
+
+    def reduce_more(self, n_final):
+        """reduce_early's continuation after a later segment: launch the next live buckets made only
+        of the first `n_final` parameters."""
+        while self.next < len(self.bounds) and self.bounds[self.next][1] <= n_final:
             if self.has_live[self.next]:
                 self._launch(self.next)
             self.next += 1

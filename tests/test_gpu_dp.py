@@ -213,18 +213,23 @@ def _graph_worker(rank, world, port, q):
                 losses.append((tr.loss_val.item(), tr.loss_target.item(), tr.loss_target_2.item()))
             if graph:
                 assert tr._graphed is not None and tr._graphed.replays == 3 and tr._graphed.graph_update is not None
-                # the backward replays as two segments split at layer3's output; the buckets of layer4
-                # and the heads (the leading parameters in backward order) launch between them, the
-                # rest after the second
-                assert len(tr._graphed.graphs) == 2, len(tr._graphed.graphs)
-                n_early = len(tr.model.split_params())
-                r1 = log.index(("replay", 1))
-                early = [b for k, b in log[:r1] if k == "launch"]
-                late = [b for k, b in log[r1:] if k == "launch"]
-                assert log[0] == ("replay", 0) and early and late, log
-                assert all(red.bounds[b][1] <= n_early for b in early), (early, n_early)
-                assert all(red.bounds[b][1] > n_early for b in late), (late, n_early)
-                assert early + late == [b for b in range(len(red.bounds)) if red.has_live[b]], log
+                # the backward replays as segments split at layer3's output and inside layer3 (split_cuts);
+                # after each segment the buckets it finished launch (bucket bounds end at every segment's
+                # end), the rest after the last one
+                ends = list(np.cumsum([len(g) for g in tr.model.split_segments()]))
+                assert len(tr._graphed.graphs) == 1 + len(ends), len(tr._graphed.graphs)
+                assert all(any(hi == e for _, hi in red.bounds) for e in ends), (ends, red.bounds)
+                assert log[0] == ("replay", 0), log
+                seen = []
+                for i in range(len(ends) + 1):
+                    r0 = log.index(("replay", i))
+                    r1 = log.index(("replay", i + 1)) if i < len(ends) else len(log)
+                    got_b = [b for k, b in log[r0:r1] if k == "launch"]
+                    lo = ends[i - 1] if i else 0
+                    hi = ends[i] if i < len(ends) else len(red.flat.params)
+                    assert got_b and all(lo < red.bounds[b][1] <= hi for b in got_b), (i, got_b, lo, hi)
+                    seen += got_b
+                assert seen == [b for b in range(len(red.bounds)) if red.has_live[b]], log
             out[graph] = (losses, torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).cpu().numpy())
             del tr
         q.put((rank, "ok", out))
@@ -236,9 +241,9 @@ def _graph_worker(rank, world, port, q):
 
 
 def test_graphed_dp_step_matches_eager_dp():
-    """The captured data-parallel step (utils/graph.py: the forward/backward passes as two graphs
-    split at layer3's output with the exchange of the first one's gradients launched between their
-    replays, then the rest of the exchange, then the graph of the SGD step) against the eager DP
+    """The captured data-parallel step (utils/graph.py: the forward/backward passes as graphs split at
+    layer3's output and inside layer3, the exchange of each segment's gradients launched after its
+    replay, the rest of the exchange after the last, then the graph of the SGD step) against the eager DP
     step with the overlapped bucket countdown, 2 ranks (gloo) x 4 UDA iterations: every loss and
     every parameter bit-identical (the step has no library kernel and the 2-rank sum is exact in
     either order), and the two replicas' parameters identical after every run (one exchange per

@@ -337,9 +337,10 @@ def test_loss_bwd_chunk_lds_bound(hi, wi, ho, wo):
 
 
 def _split_worker(rank, world, port, q):
-    """The split exchange of a captured DP step (utils/graph.py segments; solve_gta5.uda_step): after
-    the first backward segment reduce_early launches only the buckets made of the parameters that
-    segment finished, reduce_rest the others after the second segment."""
+    """The split exchange of a captured DP step (utils/graph.py segments; solve_gta5.uda_step): bucket
+    bounds end at each segment's end (set_breaks); after the first backward segment reduce_early launches
+    only the buckets made of the parameters that segment finished, after the second reduce_more the next
+    ones, reduce_rest the others after the last segment."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
@@ -349,6 +350,9 @@ def _split_worker(rank, world, port, q):
     plist = [p for p in net.parameters()]
     opt = SGD([{"params": plist, "lr": 0.1}], lr=0.1, momentum=0.9, weight_decay=5e-4)
     red = GradReducer(opt, bucket_cap_mb=0.0002)
+    ends = [4, 5]                                 # the parameters two segments finish (backward order; the
+                                                  # first two, l3, are dead)
+    red.set_breaks(ends)
     g = torch.Generator().manual_seed(7 + rank)
     x = torch.randn(4, 8, generator=g)
     opt.zero_grad()
@@ -361,14 +365,15 @@ def _split_worker(rank, world, port, q):
     red.deferred = True                           # as under a graph capture: no hooks armed
     red.prepare_for_backward()
     net(x).sum().backward()
-    n_early = red.bounds[0][1]                    # the parameters of the first bucket (backward order)
     log.append(("segment", 1))
-    red.reduce_early(n_early)
+    red.reduce_early(ends[0])
     log.append(("segment", 2))
+    red.reduce_more(ends[1])
+    log.append(("segment", 3))
     red.reduce_rest()
     red.deferred = False
     q.put((rank, log, list(red.bounds), [bool(h) for h in red.has_live],
-           opt.grads.flat.detach().numpy().copy(), n_early))
+           opt.grads.flat.detach().numpy().copy(), ends))
     dist.destroy_process_group()
 
 
@@ -383,15 +388,39 @@ def test_dp_bucket_launches_interleave_gloo():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    log, bounds, has_live, flat0, n_early = got[0]
-    seg2 = log.index(("segment", 2))
-    early = [b for k, b in log[:seg2] if k == "launch"]
-    late = [b for k, b in log[seg2:] if k == "launch"]
+    log, bounds, has_live, flat0, ends = got[0]
+    assert all(any(hi == e for _, hi in bounds) for e in ends), (bounds, ends)  # buckets end at segment ends
     assert log[0] == ("segment", 1)                       # nothing launched inside the backward
-    assert early and late, (log, bounds, has_live)
-    assert all(bounds[b][1] <= n_early for b in early) and all(bounds[b][1] > n_early for b in late)
-    assert sorted(early + late) == [b for b in range(len(bounds)) if has_live[b]]
+    cuts = [log.index(("segment", i)) for i in (1, 2, 3)] + [len(log)]
+    limits = [0] + ends + [max(hi for _, hi in bounds)]
+    seen = []
+    for i in range(3):
+        launched = [b for k, b in log[cuts[i]:cuts[i + 1]] if k == "launch"]
+        assert launched, (i, log, bounds, has_live)
+        assert all(limits[i] < bounds[b][1] <= limits[i + 1] for b in launched), (i, launched, bounds)
+        seen += launched
+    assert seen == [b for b in range(len(bounds)) if has_live[b]]
     assert np.array_equal(flat0, got[1][3])              # both ranks hold the same reduced buffer
+
+
+def test_split_segments_lead_the_flat_gradient_order():
+    """The captured DP step's backward segments (model.split_cuts, r05): each segment's parameters
+    follow the previous ones' in the flat buffer's backward order (UDATrainer._split_ok, so a bucket
+    launched after a segment holds final gradients only), and >= 85 % of the live gradient bytes belong
+    to segments before the last one (launched while the last segment replays)."""
+    import types
+    from maxsquareloss_amd.graphs.models.deeplab_multi import DeeplabMulti
+    from maxsquareloss_amd.tools.solve_gta5 import UDATrainer
+    from maxsquareloss_amd.utils.optim import SGD
+    m = DeeplabMulti(19, pretrained=False)
+    opt = SGD(m.optim_parameters(types.SimpleNamespace(lr=2.5e-4)), lr=2.5e-4, momentum=0.9, weight_decay=5e-4)
+    assert UDATrainer._split_ok(types.SimpleNamespace(optimizer=opt, model=m))
+    segs = m.split_segments()
+    assert len(segs) == 1 + len(m.split_cuts)
+    dead = {id(p) for n, p in m.named_parameters() if ".conv2d_list.2." in n or ".conv2d_list.3." in n}  # Q1
+    live = sum(p.numel() for p in opt.grads.params if id(p) not in dead)
+    early = sum(p.numel() for g in segs for p in g if id(p) not in dead)
+    assert early / live >= 0.85, early / live
 
 
 def _sk_tile(t, tiles_m, tiles_n, gm):
