@@ -613,7 +613,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
           a.bnpart = img_npart;
         } else {
           float* part = ws_partials(ws, ws_bytes, 1);
-          hipLaunchKernelGGL(k_absmax, dim3(kNPart), rblock, 0, st, img, (long long)cimg * P, 0LL, 1, part);
+          hipLaunchKernelGGL(k_absmax, dim3(kNPart), block, 0, st, img, (long long)cimg * P, 0LL, 1, part);
           MSL_CHECK_LAUNCH();
           a.bpart = part;
           a.bnpart = kNPart;
@@ -629,9 +629,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
           const long long n = (long long)a.ncb * 2 * P;
           const dim3 sgrid((unsigned)std::min<long long>(cdiv(n, 256), 8192));
           if constexpr (MT == kMathH1P)
-            hipLaunchKernelGGL(k_split_img<1>, sgrid, rblock, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
+            hipLaunchKernelGGL(k_split_img<1>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
           else
-            hipLaunchKernelGGL(k_split_img<2>, sgrid, rblock, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
+            hipLaunchKernelGGL(k_split_img<2>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
           MSL_CHECK_LAUNCH();
           a.Bx6 = planes;
         }
