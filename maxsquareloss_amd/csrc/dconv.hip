@@ -430,33 +430,25 @@ static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials 
   return reinterpret_cast<float*>((char*)ws + ((ws_bytes - (size_t)k * kPartBytes) & ~(size_t)15));
 }
 
-// The forward-form kernel, plain or with the accumulate epilogue (a template form of its own).  The
-// f16x3 / fp16 forms run k_igemm_fwd_kg2 (r05: two K groups per 512-thread workgroup, one per CU).
-template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false, bool ACC = false, bool BD = false,
-          bool BP = false>
-static void launch_one(dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk) {
-  if constexpr (MT == kMathH3P || MT == kMathH1P)
-    hipLaunchKernelGGL((k_igemm_fwd_kg2<BM, kSkBN, G, ST, WM, WN, PW, MT, ACC, BD, BP>), grid, block, 0, st, a, sk);
-  else
-    hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, ACC, BD, BP>), grid, block, 0, st, a, sk);
-}
-
+// The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
 template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
 static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk,
                       bool bp = false) {
-  if constexpr (MT == kMathH3P || MT == kMathH1P) {  // two waves per SIMD (k_igemm_fwd_kg2)
+  if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
     if constexpr (!PW && (BM == 128 || BM == 64) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
       // (accumulating BD / BP forms at 64 rows only: the pointwise M <= 64 data gradients; no 3x3 call
       // accumulates, and the 128-row accumulating 3x3 forms are not instantiated)
       if (bp) {  // the image operand pre-split by k_split_img (never for the pointwise kernels: no BP / BD form)
         if constexpr (BM == 64) {
           if (accum) {
-            launch_one<BM, G, ST, WM, WN, MT, PW, true, true, true>(grid, block, st, a, sk);
+            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0,
+                               st, a, sk);
             return;
           }
         }
         if (!accum) {
-          launch_one<BM, G, ST, WM, WN, MT, PW, false, true, true>(grid, block, st, a, sk);
+          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true, true>), grid, block, 0,
+                             st, a, sk);
           return;
         }
       }
@@ -468,20 +460,22 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
       if (a.cimg % kCB == 0) {
         if constexpr (BM == 64) {
           if (accum) {
-            launch_one<BM, G, ST, WM, WN, MT, PW, true, true>(grid, block, st, a, sk);
+            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a,
+                               sk);
             return;
           }
         }
         if (!accum) {
-          launch_one<BM, G, ST, WM, WN, MT, PW, false, true>(grid, block, st, a, sk);
+          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true>), grid, block, 0, st, a,
+                             sk);
           return;
         }
       }
     }
     if (accum)
-      launch_one<BM, G, ST, WM, WN, MT, PW, true>(grid, block, st, a, sk);
+      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true>), grid, block, 0, st, a, sk);
     else
-      launch_one<BM, G, ST, WM, WN, MT, PW, false>(grid, block, st, a, sk);
+      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false>), grid, block, 0, st, a, sk);
   } else {
     if (accum)
       hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
@@ -574,11 +568,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     // at least as many tiles as workers: whole rounds of tiles data-parallel, stream-K over the
     // rest (SkArgs); fewer: pure stream-K.  Every stream-K worker must own at least one iteration:
     // the piece count of a tile is the number of workgroups its iteration range touches.
-    // workers: 512 (two 256-thread workgroups per CU), or 256 for the f16x3 / fp16 forms (one 512-thread
-    // workgroup of two K groups per CU, k_igemm_fwd_kg2)
-    const bool kg2 = X6L && F16 && (pl.bm == 128 || small_f16);
-    const int nwk = kg2 ? kSkNW / 2 : kSkNW;
-    sk.tdp = (g_sk_hybrid && tiles >= nwk) ? (int)(tiles / nwk * nwk) : 0;
+    sk.tdp = (g_sk_hybrid && tiles >= kSkNW) ? (int)(tiles / kSkNW * kSkNW) : 0;
     // Tile order (r04): m fastest when whole rounds of tiles run data-parallel (hybrid): one XCD's
     // workers then hold every m-block of a few pixel blocks, so each image block is fetched once and
     // re-read from that L2 (same box: 256 -> 1024 fwd 42.7 vs 49.8 us, 2048 -> 512 dgrad 127 vs 141,
@@ -588,7 +578,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     // 101 us m fastest; layer3 fwd 79 vs 77.7; profiles/r04_aspp_tile_order.txt).
     sk.gm = sk.tdp > 0 ? pl.tiles_m : 1;
     const long long T = (tiles - sk.tdp) * sk.KS;
-    sk.NW = (int)std::min<long long>(nwk, T);
+    sk.NW = (int)std::min<long long>(kSkNW, T);
     // the remainder after data-parallel rounds (e.g. 16 tiles x 16 K-steps of a 256 -> 1024 pointwise
     // GEMM): at one or two K-steps per worker every worker writes a whole 64-KB piece for almost no
     // work; at least kSkMinIt K-steps each (512 -> 2048 fwd 75.9 vs 82.2 us, 2048 -> 512 dgrad 85.6 vs
@@ -598,8 +588,8 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     sk.T = (int)T;
     a.C = out;
     a.bias = bias;
-    const dim3 grid(sk.tdp > 0 ? nwk : sk.NW), block(kg2 ? 512 : 256);
-    const dim3 rgrid(pl.bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp)), rblock(256);
+    const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
+    const dim3 rgrid(pl.bm * kSkBN / 1024, (unsigned)(tiles - sk.tdp));
     const bool reduce = T > 0;
     if (X6L && (pl.bm == 128 || small_f16)) {
       // the x6 kernel stages its weights from the bf16 planes that pack() split once, behind
@@ -661,9 +651,9 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
       MSL_CHECK_LAUNCH();
       if (reduce) {
         if (small_f16)
-          hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, rblock, 0, st, a, sk);
+          hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
         else
-          hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, rblock, 0, st, a, sk);
+          hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
       }
     } else if (pl.bm == 128) {
       if (pl.G == 2)

@@ -1029,7 +1029,7 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
 // each, more than the K-step's 12 MFMAs).  Every wave of the 1 x 4 layout reads its own 32 columns,
 // so nothing is lost by not sharing B through LDS.
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false, bool BP = false, int KG = 1>
+          bool BD = false, bool BP = false>
 __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -1063,24 +1063,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   static_assert(AHALF || A_INST % 4 == 0, "A instructions split evenly over waves");
   static_assert(!AHALF || (G == 1 && BM == 64), "half-wave A pieces: one K-step of 64 rows per stage");
   static_assert((STAGES - 2) * INST_W < 64, "vmcnt range");
-  // KG = 2 (r05): a workgroup of two 4-wave groups on one CU, each running this K-loop over one half
-  // of every tile segment's K-steps in a ring of its own; group 1's accumulators then go through LDS
-  // to group 0, which adds them (in that fixed order) and stores.  A tile is reduced inside its CU
-  // instead of through stream-K pieces in HBM and a k_sk_reduce pass, and with one workgroup per CU
-  // the 256 workers need half the tiles per data-parallel round.
-  static_assert(KG == 1 || KG == 2, "one or two K groups");
-  constexpr int RING = STAGES * STAGE;
-  constexpr int RED = KG > 1 ? TM * TN * 16 * 256 : 0;  // group 1's accumulators, [reg][wave][lane]
-  constexpr int SMEM = KG * RING > RED ? KG * RING : RED;
   // ONE __shared__ object: a second one (even a 4-byte flag) makes hipcc emit vmcnt(0) before the
   // first ds_read after every DMA issue, which drains the in-flight stage (cdna_hip_programming.md
   // §5, M = 256 item 4(a)).
-  __shared__ __attribute__((aligned(16))) float smem_all[SMEM];
+  __shared__ __attribute__((aligned(16))) float smem[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int grp = KG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;  // K group (wave-uniform)
-  const int wid = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);         // wave within its group
-  float* smem = smem_all + grp * RING;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
   // XCD-aware worker id: workgroups b, b+8, ... share an XCD and get consecutive ranges
   const int nb = gridDim.x, b = blockIdx.x;
@@ -1131,14 +1120,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     } else {
       break;
     }
-    // this group's K-steps [kg_a, kg_a + nst) of the segment; both groups step `steps` times (the same
-    // barriers), a group with fewer real K-steps only issues loads in its last step
-    int kg_a = k_a, nst = k_b - k_a, steps = nst;
-    if constexpr (KG > 1) {
-      steps = (nst + 1) >> 1;
-      kg_a = k_a + grp * steps;
-      nst = grp ? nst - steps : steps;
-    }
+    const int nst = k_b - k_a;
     int tm, tn;
     sk_tile(t, sk.tiles_m, sk.tiles_n, sk.gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
@@ -1172,7 +1154,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     const int pqd = pbd / a.W, pxd = pbd - pqd * a.W, pyd = pqd % a.H;
     {
       // wave-uniform: the cursor lives in scalar registers (it feeds the scalar channel offsets)
-      const int ks0 = __builtin_amdgcn_readfirstlane(kg_a * G);
+      const int ks0 = __builtin_amdgcn_readfirstlane(k_a * G);
       const int tq = ks0 / a.ncb;  // branch*taps + tap
       c_cb = ks0 - tq * a.ncb;
       c_tap = tq;
@@ -1302,9 +1284,9 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // the compiler's wait-count analysis saw paths with no younger loads and drained the queue -
       // vmcnt(0) - before the split of every first and fourth K-step; r04.  Those drains had also
       // hidden the LDS-DMA ordering race described at the wait below.)
-      issue(kg_a, 0, bdq[0]);
-      issue(kg_a + 1, 1, bdq[1]);
-      issue(kg_a + 2, 2, bdq[2]);
+      issue(k_a, 0, bdq[0]);
+      issue(k_a + 1, 1, bdq[1]);
+      issue(k_a + 2, 2, bdq[2]);
       // K-step i: wait until stage i + 1 landed (only stage i + 2 younger), barrier (stage i + 1 is
       // complete in every wave's LDS pieces, and every wave has read slot i - 1's fragments, at step
       // i - 2), issue stage i + 3 into that slot and ring entry, read + split K-step i + 1's fragments,
@@ -1320,40 +1302,34 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         wait_vmcnt<2 * A_INST_W>();
         __builtin_amdgcn_s_barrier();
         const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
-        auto mid = [&] { issue(kg_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt); };
-        if (KG == 1 || i < nst) {
-          if constexpr (BP)
-            mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
-          else
-            mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
-        } else {
-          mid();
-        }
+        auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt); };
+        if constexpr (BP)
+          mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
+        else
+          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       };
       int i = 0;
-      for (; i + 4 <= steps; i += 4) {
+      for (; i + 4 <= nst; i += 4) {
         step(i, bdq[0], bdq[3]);
         step(i + 1, bdq[1], bdq[0]);
         step(i + 2, bdq[2], bdq[1]);
         step(i + 3, bdq[3], bdq[2]);
       }
-      if (i < steps) step(i, bdq[0], bdq[3]);
-      if (i + 1 < steps) step(i + 1, bdq[1], bdq[0]);
-      if (i + 2 < steps) step(i + 2, bdq[2], bdq[1]);
+      if (i < nst) step(i, bdq[0], bdq[3]);
+      if (i + 1 < nst) step(i + 1, bdq[1], bdq[0]);
+      if (i + 2 < nst) step(i + 2, bdq[2], bdq[1]);
       wait_vmcnt<0>();  // the stages issued past the end land before the slots are reused
     } else {
       // as in the BD form: a stage issued every K-step, past the end too, so one wait count
 #pragma unroll
-    for (int k = 0; k < STAGES - 1; ++k) issue(kg_a + k, k, bdq[0]);
-    for (int i = 0; i < steps; ++i) {
+    for (int k = 0; k < STAGES - 1; ++k) issue(k_a + k, k, bdq[0]);
+    for (int i = 0; i < nst; ++i) {
       wait_vmcnt<(STAGES - 2) * INST_W>();
       __builtin_amdgcn_s_barrier();
       const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
-      auto mid = [&] { issue(kg_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, bdq[0]); };
-      if (KG > 1 && i >= nst)
-        mid();
-      else if constexpr (MT == kMathBf16)
+      auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, bdq[0]); };
+      if constexpr (MT == kMathBf16)
         mfma_stage_bf16<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (MT == kMathX6)
         mfma_stage_x6<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
@@ -1372,30 +1348,6 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     wait_vmcnt<0>();  // the stages issued past the end land before the slots are reused
     }
 
-    if constexpr (KG > 1) {
-      // group 1's sums to group 0 through LDS (over the rings: every wave's ring reads and DMA pieces
-      // are done - each waited for its own - once all waves pass the barrier); group 0 adds them in
-      // that order (deterministic) and goes on to the store; group 1 to the next segment
-      __builtin_amdgcn_s_barrier();
-      if (grp) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) smem_all[(((i * TN + j) * 16 + r) * 4 + wid) * 64 + lane] = acc[i][j][r];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (grp) continue;
-      const float* red = lds_after_barrier(smem_all);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] += red[(((i * TN + j) * 16 + r) * 4 + wid) * 64 + lane];
-    }
     if constexpr (H3) {  // exact: both factors are powers of two
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -1483,14 +1435,6 @@ template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, in
           bool BD = false, bool BP = false>
 __global__ void __launch_bounds__(256, 2) k_igemm_fwd_sk2(FwdArgs a, SkArgs sk) {
   fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD, BP>(a, sk);
-}
-
-// The same with two K groups per workgroup (KG = 2, r05): 512 threads, one workgroup per CU, the same
-// register budget per wave (two waves per SIMD).
-template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false, bool BP = false>
-__global__ void __launch_bounds__(512, 1) k_igemm_fwd_kg2(FwdArgs a, SkArgs sk) {
-  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD, BP, 2>(a, sk);
 }
 
 // sum of pieces w_lo..w_hi in that order (deterministic), eight loads in flight per step: a tile

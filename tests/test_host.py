@@ -303,8 +303,8 @@ def test_hot_kernels_keep_their_occupancy():
         if m and kern:
             info[kern][m.group(1)] = int(m.group(2))
     hot = [k for k in info if k.startswith("_ZN3msl14k_igemm_fwd_skILi128ELi128ELi1ELi4ELi2ELi2ELb0ELi3E")
-           or k.startswith("_ZN3msl15k_igemm_fwd_kg2ILi128ELi128ELi1ELi4ELi1ELi4ELb0ELi5E")
-           or k.startswith("_ZN3msl15k_igemm_fwd_kg2ILi128ELi128ELi1ELi4ELi1ELi4ELb0ELi8E")
+           or k.startswith("_ZN3msl15k_igemm_fwd_sk2ILi128ELi128ELi1ELi4ELi1ELi4ELb0ELi5E")
+           or k.startswith("_ZN3msl15k_igemm_fwd_sk2ILi128ELi128ELi1ELi4ELi1ELi4ELb0ELi8E")
            or k.startswith("_ZN3msl10k_wgrad_x6")]
     # the x6, f16x3 and fp16 forwards (plain, accumulating; + the plain BD and BP forms: no 3x3 call
     # accumulates) and the three weight-gradient forms
