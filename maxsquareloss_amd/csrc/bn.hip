@@ -486,7 +486,7 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
       s[2 * q + 1] = s2;
     }
     block_sum_d16<2 * NIP>(s, red);
-    float alpha[NIP], bsh[NIP];
+    float alpha[NIP], bsh[NIP], mean[NIP], unbiased[NIP];
 #pragma unroll
     for (int q = 0; q < NIP; ++q) {
       const int r = c * a.NI + i0 + q;
@@ -494,21 +494,27 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
       const double dm = s[2 * q] / n;
       double var = __fma_rn(-dm, dm, __ddiv_rn(s[2 * q + 1], n));
       if (var < 0.0) var = 0.0;
-      const float mean = (float)(shift[q] + dm);
+      mean[q] = (float)(shift[q] + dm);
+      unbiased[q] = (float)(P > 1 ? var * n / (n - 1.0) : var);
       const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
       if (t == 0) {
-        if (a.update_running) {  // image by image, in order
-          const float m = a.momentum;
-          const float unbiased = (float)(P > 1 ? var * n / (n - 1.0) : var);
-          a.running_mean[c] = running_blend(a.running_mean[c], m, mean);
-          a.running_var[c] = running_blend(a.running_var[c], m, unbiased);
-          if (c == 0 && a.num_batches) a.num_batches[0] += 1;
-        }
-        a.save_mean[r] = mean;
+        a.save_mean[r] = mean[q];
         a.save_invstd[r] = invstd;
       }
       alpha[q] = invstd * (a.gamma ? a.gamma[c] : 1.f);
-      bsh[q] = __fmaf_rn(-mean, alpha[q], a.beta ? a.beta[c] : 0.f);
+      bsh[q] = __fmaf_rn(-mean[q], alpha[q], a.beta ? a.beta[c] : 0.f);
+    }
+    if (t == 0 && a.update_running) {  // image by image, in order, in registers
+      const float m = a.momentum;
+      float rm = a.running_mean[c], rvar = a.running_var[c];
+#pragma unroll
+      for (int q = 0; q < NIP; ++q) {
+        rm = running_blend(rm, m, mean[q]);
+        rvar = running_blend(rvar, m, unbiased[q]);
+      }
+      a.running_mean[c] = rm;
+      a.running_var[c] = rvar;
+      if (c == 0 && a.num_batches) a.num_batches[0] += NIP;
     }
     // the residual is loaded after the statistics: not live across the reduction, so the EPT <= 16
     // one-image forms fit 64 VGPRs (two 1024-thread blocks per CU)
