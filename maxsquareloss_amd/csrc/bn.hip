@@ -125,9 +125,13 @@ __device__ __forceinline__ void bn_row_stats(const BnArgs& a, int r, float& mean
 
 // (1 - m) * old + m * v with every operation rounded on its own: whether the compiler contracts
 // this into an fma depended on the kernel around it, so the pair, per-image and split forms rounded
-// the running variance differently (r03: the pair form's running_var was 1 ulp off the per-image loop)
+// the running statistics differently (r03: the pair form's running_var 1 ulp off the per-image loop;
+// r05: the two-image form's running_mean up to 4 ulps).  HIP's __fmul_rn / __fadd_rn are the plain
+// operators (without OCML_BASIC_ROUNDED_OPERATIONS), which hipcc's -ffp-contract=fast may fuse; under
+// contract(off) these operations carry no contract flag.
 __device__ __forceinline__ float running_blend(float old, float m, float v) {
-  return __fadd_rn(__fmul_rn(__fsub_rn(1.f, m), old), __fmul_rn(m, v));
+#pragma clang fp contract(off)
+  return (1.f - m) * old + m * v;
 }
 
 // running statistics of channel c <- image n's batch statistics (one image after the other)

@@ -18,6 +18,14 @@ namespace msl {
 
 constexpr int kSgdBlockElems = 4096;
 
+// buf * momentum + d with the product rounded on its own, as torch-CPU's buf.mul_(momentum).add_(d)
+// (train_source.py:139-144 through torch.optim.SGD): HIP's __fmul_rn / __fadd_rn are the plain
+// operators, which hipcc's -ffp-contract=fast may fuse into an fma; under contract(off) they are not
+__device__ __forceinline__ float momentum_blend(float b, float mom, float d) {
+#pragma clang fp contract(off)
+  return b * mom + d;
+}
+
 __global__ void __launch_bounds__(256) k_sgd(const msl_sgd_entry* __restrict__ entries,
                                               const int32_t* __restrict__ block_entry,
                                               const long long* __restrict__ block_offset,
@@ -36,7 +44,7 @@ __global__ void __launch_bounds__(256) k_sgd(const msl_sgd_entry* __restrict__ e
     float b = e.has_buf ? e.momentum[i] : 0.f;
     for (int r = 0; r < e.mult; ++r) {
       const float d = __fmaf_rn(p, wd, g);
-      b = e.has_buf ? __fadd_rn(__fmul_rn(b, mom), d) : d;
+      b = e.has_buf ? momentum_blend(b, mom, d) : d;
       p = __fmaf_rn(b, nlr, p);
     }
     e.param[i] = p;
