@@ -126,7 +126,7 @@ __device__ __forceinline__ void bn_row_stats(const BnArgs& a, int r, float& mean
 // (1 - m) * old + m * v with every operation rounded on its own: whether the compiler contracts
 // this into an fma depended on the kernel around it, so the pair, per-image and split forms rounded
 // the running statistics differently (r03: the pair form's running_var 1 ulp off the per-image loop;
-// r05: the two-image form's running_mean up to 4 ulps).  HIP's __fmul_rn / __fadd_rn are the plain
+// r05: a two-image form's running_mean up to 4 ulps).  HIP's __fmul_rn / __fadd_rn are the plain
 // operators (without OCML_BASIC_ROUNDED_OPERATIONS), which hipcc's -ffp-contract=fast may fuse; under
 // contract(off) these operations carry no contract flag.
 __device__ __forceinline__ float running_blend(float old, float m, float v) {
@@ -412,25 +412,21 @@ static bool bn_fused_shape(int c, int p) {
   return p <= 16 * kBnFusedThreads || (c >= 128 && p <= kBnFusedMaxP);
 }
 
-// Block sums of N doubles over the 16 waves of a fused block, each value summed in the same fixed
-// order (wave order) whatever N: the two-image forms (NIP = 2) reduce both images' sums in one pass
-// and get exactly the one-image sums.
-template <int N>
-__device__ __forceinline__ void block_sum_d16(double (&v)[N], double* red) {
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = wave_sum_d(v[k]);
+__device__ __forceinline__ void block_sum2_d16(double& a, double& b, double* red) {
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) red[N * w + k] = v[k];
+    red[2 * w] = a;
+    red[2 * w + 1] = b;
   }
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = 0.0;
+  a = 0.0;
+  b = 0.0;
 #pragma unroll
   for (int i = 0; i < kBnFusedThreads / 64; ++i) {  // fixed order: deterministic
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] += red[N * i + k];
+    a += red[2 * i];
+    b += red[2 * i + 1];
   }
 }
 
@@ -448,106 +444,78 @@ __device__ __forceinline__ void bn_st(__amdgpu_buffer_rsrc_t r, unsigned voff, i
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, j * kBnFusedThreads * 4, 0);
 }
 constexpr int kBnTwoBlockEpt = 16;  // forms built for two blocks per CU (64 VGPRs)
-// waves per SIMD the fused forms are built for: two 1024-thread blocks per CU up to 16 elements per
-// lane; the two-image forms (NIP = 2, twice the live operands) and the 33-element forms one block
-template <int EPT, int NIP>
-constexpr int bn_waves_per_eu() { return NIP == 1 && EPT <= kBnTwoBlockEpt ? 8 : 4; }
 
-// One block per channel (1024 threads); the channel's NI images in groups of NIP.  NIP = 2 (r05, an
-// image pair on <= 256 channels, where the grid is one block per CU): both images' loads are in flight
-// together and their statistics reduced in one pass - the one-image form paid the load latency and the
-// block reduction once per image, one after the other (14 us for a 256-channel pair at 2.5 TB/s).
-// Same operations and order per image: the results are bit-identical to NIP = 1.
-template <int EPT, int NIP>
-__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(bn_waves_per_eu<EPT, NIP>()))) k_bn_fwd_fused(BnArgs a) {
-  __shared__ double red[2 * NIP * kBnFusedThreads / 64];
+template <int EPT>
+__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= kBnTwoBlockEpt ? 8 : 1))) k_bn_fwd_fused(BnArgs a) {
+  __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
-  const unsigned vo = (unsigned)t * 4u;
   float am = 0.f;
-  for (int i0 = 0; i0 < a.NI; i0 += NIP) {  // the channel's images, NIP at a time
-    if (i0) __syncthreads();                 // red[] is reused
-    float xv[NIP][EPT];
-    double shift[NIP], s[2 * NIP];
+  for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
+  if (img) __syncthreads();               // red[] is reused
+  const int r = c * a.NI + img;
+  const long long base = (long long)r * P;
+  const float* xc = a.x + base;
+  const unsigned vo = (unsigned)t * 4u;
+  const __amdgpu_buffer_rsrc_t rx = bn_row(xc, P);
+  float xv[EPT];
 #pragma unroll
-    for (int q = 0; q < NIP; ++q) {
-      const __amdgpu_buffer_rsrc_t rx = bn_row(a.x + (long long)(c * a.NI + i0 + q) * P, P);
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
+  }
+  const double shift = (double)xc[0];
+  double s1 = 0.0, s2 = 0.0;
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) xv[q][j] = j * kBnFusedThreads + t < P ? bn_ld(rx, vo, j) : 0.f;
+  for (int j = 0; j < EPT; ++j) {
+    if (j * kBnFusedThreads + t < P) {
+      const double d = (double)xv[j] - shift;
+      s1 = __dadd_rn(s1, d);  // explicit roundings: the single-image and pair forms agree bit for bit
+      s2 = __fma_rn(d, d, s2);
     }
-#pragma unroll
-    for (int q = 0; q < NIP; ++q) {
-      shift[q] = (double)a.x[(long long)(c * a.NI + i0 + q) * P];
-      double s1 = 0.0, s2 = 0.0;
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        if (j * kBnFusedThreads + t < P) {
-          const double d = (double)xv[q][j] - shift[q];
-          s1 = __dadd_rn(s1, d);  // explicit roundings: the single-image and pair forms agree bit for bit
-          s2 = __fma_rn(d, d, s2);
-        }
-      }
-      s[2 * q] = s1;
-      s[2 * q + 1] = s2;
-    }
-    block_sum_d16<2 * NIP>(s, red);
-    float alpha[NIP], bsh[NIP], mean[NIP], unbiased[NIP];
-#pragma unroll
-    for (int q = 0; q < NIP; ++q) {
-      const int r = c * a.NI + i0 + q;
-      const double n = (double)P;
-      const double dm = s[2 * q] / n;
-      double var = __fma_rn(-dm, dm, __ddiv_rn(s[2 * q + 1], n));
-      if (var < 0.0) var = 0.0;
-      mean[q] = (float)(shift[q] + dm);
-      unbiased[q] = (float)(P > 1 ? var * n / (n - 1.0) : var);
-      const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-      if (t == 0) {
-        a.save_mean[r] = mean[q];
-        a.save_invstd[r] = invstd;
-      }
-      alpha[q] = invstd * (a.gamma ? a.gamma[c] : 1.f);
-      bsh[q] = __fmaf_rn(-mean[q], alpha[q], a.beta ? a.beta[c] : 0.f);
-    }
-    if (t == 0 && a.update_running) {  // image by image, in order, in registers
+  }
+  block_sum2_d16(s1, s2, red);
+  const double n = (double)P;
+  const double dm = s1 / n;
+  double var = __fma_rn(-dm, dm, __ddiv_rn(s2, n));
+  if (var < 0.0) var = 0.0;
+  const float mean = (float)(shift + dm);
+  const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+  if (t == 0) {
+    if (a.update_running) {
       const float m = a.momentum;
-      float rm = a.running_mean[c], rvar = a.running_var[c];
-#pragma unroll
-      for (int q = 0; q < NIP; ++q) {
-        rm = running_blend(rm, m, mean[q]);
-        rvar = running_blend(rvar, m, unbiased[q]);
-      }
-      a.running_mean[c] = rm;
-      a.running_var[c] = rvar;
-      if (c == 0 && a.num_batches) a.num_batches[0] += NIP;
+      const float unbiased = (float)(P > 1 ? var * n / (n - 1.0) : var);
+      a.running_mean[c] = running_blend(a.running_mean[c], m, mean);
+      a.running_var[c] = running_blend(a.running_var[c], m, unbiased);
+      if (c == 0 && a.num_batches) a.num_batches[0] += 1;
     }
-    // the residual is loaded after the statistics: not live across the reduction, so the EPT <= 16
-    // one-image forms fit 64 VGPRs (two 1024-thread blocks per CU)
-    float rv[NIP][EPT];
+    a.save_mean[r] = mean;
+    a.save_invstd[r] = invstd;
+  }
+  const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
+  const float bsh = __fmaf_rn(-mean, alpha, a.beta ? a.beta[c] : 0.f);
+  const __amdgpu_buffer_rsrc_t ry = bn_row(a.y + base, P);
+  // the residual is loaded after the statistics: not live across the reduction, so the EPT <= 16
+  // forms fit 64 VGPRs (two 1024-thread blocks per CU)
+  float rv[EPT];
+  if (a.residual) {
+    const __amdgpu_buffer_rsrc_t rr = bn_row(a.residual + base, P);
 #pragma unroll
-    for (int q = 0; q < NIP; ++q) {
-      if (a.residual) {
-        const __amdgpu_buffer_rsrc_t rr = bn_row(a.residual + (long long)(c * a.NI + i0 + q) * P, P);
+    for (int j = 0; j < EPT; ++j) rv[j] = j * kBnFusedThreads + t < P ? bn_ld(rr, vo, j) : 0.f;
+  } else {
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) rv[q][j] = j * kBnFusedThreads + t < P ? bn_ld(rr, vo, j) : 0.f;
-      } else {
+    for (int j = 0; j < EPT; ++j) rv[j] = 0.f;
+  }
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) rv[q][j] = 0.f;
-      }
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    if (e < P) {
+      float v = __fmaf_rn(xv[j], alpha, bsh);
+      v += rv[j];
+      v = a.relu ? fmaxf(v, 0.f) : v;
+      bn_st(ry, vo, j, v);
+      am = fmaxf(am, fabsf(v));
     }
-#pragma unroll
-    for (int q = 0; q < NIP; ++q) {
-      const __amdgpu_buffer_rsrc_t ry = bn_row(a.y + (long long)(c * a.NI + i0 + q) * P, P);
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        if (j * kBnFusedThreads + t < P) {
-          float v = __fmaf_rn(xv[q][j], alpha[q], bsh[q]);
-          v += rv[q][j];
-          v = a.relu ? fmaxf(v, 0.f) : v;
-          bn_st(ry, vo, j, v);
-          am = fmaxf(am, fabsf(v));
-        }
-      }
-    }
+  }
   }  // images
   if (a.absmax) {
     __shared__ float redm[kBnFusedThreads / 64];
@@ -556,88 +524,73 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
   }
 }
 
-template <int EPT, int NIP>
-__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(bn_waves_per_eu<EPT, NIP>()))) k_bn_bwd_fused(BnBwdArgs a) {
-  __shared__ double red[2 * NIP * kBnFusedThreads / 64];
+template <int EPT>
+__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= kBnTwoBlockEpt ? 8 : 1))) k_bn_bwd_fused(BnBwdArgs a) {
+  __shared__ double red[2 * kBnFusedThreads / 64];
   const int c = blockIdx.x, t = threadIdx.x, P = a.P;
-  const unsigned vo = (unsigned)t * 4u;
   float am = 0.f;
   float dg = 0.f, db = 0.f;  // the parameter gradients, image by image (thread 0)
-  const float gam = a.gamma ? a.gamma[c] : 1.f;
-  for (int i0 = 0; i0 < a.NI; i0 += NIP) {  // the channel's images, NIP at a time
-    if (i0) __syncthreads();                 // red[] is reused
-    float g[NIP][EPT], xv[NIP][EPT], mean[NIP], invstd[NIP], w[NIP];
+  for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
+  if (img) __syncthreads();               // red[] is reused
+  const int r = c * a.NI + img;
+  const long long base = (long long)r * P;
+  const float mean = a.save_mean[r], invstd = a.save_invstd[r];
+  const unsigned vo = (unsigned)t * 4u;
+  const __amdgpu_buffer_rsrc_t rdy = bn_row(a.dy + base, P), rx = bn_row(a.x + base, P);
+  float g[EPT], xv[EPT];
 #pragma unroll
-    for (int q = 0; q < NIP; ++q) {
-      const long long base = (long long)(c * a.NI + i0 + q) * P;
-      const __amdgpu_buffer_rsrc_t rdy = bn_row(a.dy + base, P), rx = bn_row(a.x + base, P);
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    g[j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
+    xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
+  }
+  const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
+  if (a.relu && a.y) {
+    const __amdgpu_buffer_rsrc_t ryy = bn_row(a.y + base, P);
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        const int e = j * kBnFusedThreads + t;
-        g[q][j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
-        xv[q][j] = e < P ? bn_ld(rx, vo, j) : 0.f;
-      }
-      mean[q] = a.save_mean[c * a.NI + i0 + q];
-      invstd[q] = a.save_invstd[c * a.NI + i0 + q];
-      w[q] = invstd[q] * gam;
+    for (int j = 0; j < EPT; ++j) {
+      const int e = j * kBnFusedThreads + t;
+      if (e < P && !(bn_ld(ryy, vo, j) > 0.f)) g[j] = 0.f;
     }
-    double s[2 * NIP];
+  } else if (a.relu) {  // y > 0 recomputed with k_bn_fwd_fused's operations (its alpha, bsh)
+    if constexpr (EPT <= kBnRemaskMaxEpt) {  // (the 33-element form spills twice as much with it)
+      const float bsh = __fmaf_rn(-mean, w, a.beta ? a.beta[c] : 0.f);
 #pragma unroll
-    for (int q = 0; q < NIP; ++q) {
-      if (a.relu && a.y) {
-        const __amdgpu_buffer_rsrc_t ryy = bn_row(a.y + (long long)(c * a.NI + i0 + q) * P, P);
-#pragma unroll
-        for (int j = 0; j < EPT; ++j) {
-          const int e = j * kBnFusedThreads + t;
-          if (e < P && !(bn_ld(ryy, vo, j) > 0.f)) g[q][j] = 0.f;
-        }
-      } else if (a.relu) {  // y > 0 recomputed with k_bn_fwd_fused's operations (its alpha, bsh)
-        if constexpr (EPT <= kBnRemaskMaxEpt) {  // (the 33-element form spills twice as much with it)
-          const float bsh = __fmaf_rn(-mean[q], w[q], a.beta ? a.beta[c] : 0.f);
-#pragma unroll
-          for (int j = 0; j < EPT; ++j)
-            if (!(__fmaf_rn(xv[q][j], w[q], bsh) > 0.f)) g[q][j] = 0.f;
-        }
-      }
-      double sg = 0.0, sgx = 0.0;
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        const float xh = (xv[q][j] - mean[q]) * invstd[q];
-        sg = __dadd_rn(sg, (double)g[q][j]);  // g = 0 past P
-        sgx = __fma_rn((double)g[q][j], (double)xh, sgx);
-      }
-      s[2 * q] = sg;
-      s[2 * q + 1] = sgx;
+      for (int j = 0; j < EPT; ++j)
+        if (!(__fmaf_rn(xv[j], w, bsh) > 0.f)) g[j] = 0.f;
     }
-    block_sum_d16<2 * NIP>(s, red);
+  }
+  double sg = 0.0, sgx = 0.0;
 #pragma unroll
-    for (int q = 0; q < NIP; ++q) {
-      const double sg = s[2 * q], sgx = s[2 * q + 1];
-      if (t == 0) {
-        if (i0 + q == 0) {
-          dg = (a.accumulate && a.dgamma) ? a.dgamma[c] + (float)sgx : (float)sgx;
-          db = (a.accumulate && a.dbeta) ? a.dbeta[c] + (float)sg : (float)sg;
-        } else {
-          dg += (float)sgx;
-          db += (float)sg;
-        }
-      }
-      const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
-      const long long base = (long long)(c * a.NI + i0 + q) * P;
-      const __amdgpu_buffer_rsrc_t rdres = bn_row(a.dres ? a.dres + base : nullptr, P);
-      const __amdgpu_buffer_rsrc_t rdx = bn_row(a.dx ? a.dx + base : nullptr, P);
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        const int e = j * kBnFusedThreads + t;
-        if (e < P) {
-          const float xh = (xv[q][j] - mean[q]) * invstd[q];
-          if (a.dres) bn_st(rdres, vo, j, g[q][j]);
-          const float d = __fmul_rn(__fmaf_rn(-xh, m2, __fsub_rn(g[q][j], m1)), w[q]);
-          if (a.dx) bn_st(rdx, vo, j, d);
-          am = fmaxf(am, fabsf(d));
-        }
-      }
+  for (int j = 0; j < EPT; ++j) {
+    const float xh = (xv[j] - mean) * invstd;
+    sg = __dadd_rn(sg, (double)g[j]);  // g = 0 past P
+    sgx = __fma_rn((double)g[j], (double)xh, sgx);
+  }
+  block_sum2_d16(sg, sgx, red);
+  if (t == 0) {
+    if (img == 0) {
+      dg = (a.accumulate && a.dgamma) ? a.dgamma[c] + (float)sgx : (float)sgx;
+      db = (a.accumulate && a.dbeta) ? a.dbeta[c] + (float)sg : (float)sg;
+    } else {
+      dg += (float)sgx;
+      db += (float)sg;
     }
+  }
+  const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
+  const __amdgpu_buffer_rsrc_t rdres = bn_row(a.dres ? a.dres + base : nullptr, P);
+  const __amdgpu_buffer_rsrc_t rdx = bn_row(a.dx ? a.dx + base : nullptr, P);
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = j * kBnFusedThreads + t;
+    if (e < P) {
+      const float xh = (xv[j] - mean) * invstd;
+      if (a.dres) bn_st(rdres, vo, j, g[j]);
+      const float d = __fmul_rn(__fmaf_rn(-xh, m2, __fsub_rn(g[j], m1)), w);
+      if (a.dx) bn_st(rdx, vo, j, d);
+      am = fmaxf(am, fabsf(d));
+    }
+  }
   }  // images
   if (t == 0) {
     if (a.dgamma) a.dgamma[c] = dg;
@@ -650,15 +603,10 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
   }
 }
 
-// The fused launch for c channels of p pixels: elements per lane by p; an image pair on <= 256
-// channels (one block per CU) with p <= 9 * 1024 runs the two-image form (its 16-element form would
-// spill: 4 waves per SIMD leave 128 VGPRs)
+
 template <typename K, typename A>
-static int bn_launch_fused(K k4, K k9, K k16, K k33, K k4p, K k9p, int c, int p, int nimg, hipStream_t st,
-                           const A& a) {
-  const bool pair = nimg == 2 && c <= 256;
-  K k = p <= 4 * kBnFusedThreads ? (pair ? k4p : k4) : p <= 9 * kBnFusedThreads ? (pair ? k9p : k9)
-        : p <= 16 * kBnFusedThreads ? k16 : k33;
+static int bn_launch_fused(K k4, K k9, K k16, K k33, int c, int p, hipStream_t st, const A& a) {
+  K k = p <= 4 * kBnFusedThreads ? k4 : p <= 9 * kBnFusedThreads ? k9 : p <= 16 * kBnFusedThreads ? k16 : k33;
   hipLaunchKernelGGL(k, dim3(c), dim3(kBnFusedThreads), 0, st, a);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -743,9 +691,7 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
   a.eps = eps;
   a.momentum = momentum;
   a.absmax = absmax;
-  if (fused)
-    return bn_launch_fused(k_bn_fwd_fused<4, 1>, k_bn_fwd_fused<9, 1>, k_bn_fwd_fused<16, 1>, k_bn_fwd_fused<33, 1>,
-                           k_bn_fwd_fused<4, 2>, k_bn_fwd_fused<9, 2>, c, p, nimg, st, a);
+  if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>, c, p, st, a);
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec)
     hipLaunchKernelGGL(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
@@ -810,8 +756,7 @@ int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const fl
   a.accumulate = accumulate_params;
   a.absmax = absmax_dx;
   if (fused)
-    return bn_launch_fused(k_bn_bwd_fused<4, 1>, k_bn_bwd_fused<9, 1>, k_bn_bwd_fused<16, 1>, k_bn_bwd_fused<33, 1>,
-                           k_bn_bwd_fused<4, 2>, k_bn_bwd_fused<9, 2>, c, p, nimg, st, a);
+    return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec) {
