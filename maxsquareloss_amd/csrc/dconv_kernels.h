@@ -540,6 +540,57 @@ __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane,
   mid();
 }
 
+// The BD stage with the split software-pipelined (r05): bv holds this K-step's B fragments, split one
+// K-step earlier, and the next K-step's raw values (bnext) are split between this K-step's MFMAs
+// (sched_group_barrier: one MFMA, then a few VALU), so the split's VALU issues while the matrix pipe
+// works instead of in front of it (the in-kernel stamps put ~70 % of a K-step in the fragment reads +
+// split + MFMA issue, with the split in series before the MFMAs: scripts/probe_sk.py).
+template <int TM, int BM, bool HI_ONLY, typename F>
+__device__ __forceinline__ void mfma_stage_hd2(const float* As, int wm, int lane, f32x16 (&acc)[TM][1],
+                                               F&& mid, float sB, const float (&bnext)[8], Split2h& bv) {
+  const int l32 = lane & 31, h = lane >> 5;
+  const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
+  Split2h nb;
+  if constexpr (HI_ONLY) {
+    f16x8 av[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bv.hi, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) nb.hi[j] = (_Float16)(bnext[j] * sB);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // then up to six VALU
+    }
+  } else {
+    Split2h av[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i].lo = Ab[(2 + h) * BM + wm + i * 32 + l32];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bv.hi, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv.lo, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv.hi, acc[i][0], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split2h_set(nb, j, bnext[j] * sB);
+#pragma unroll
+    for (int i = 0; i < 3 * TM; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // then up to five VALU
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  bv = nb;
+  mid();
+}
+
 // The BD stage with the image operand pre-split (k_split_img): braw holds the lane's hi plane (floats
 // 0..3 as 16 B) and lo plane (4..7), already scaled; no split work in the loop.
 template <int TM, int BM, bool HI_ONLY, typename F>
@@ -998,6 +1049,7 @@ struct SkArgs {
   int T;           // stream-K iterations: (tiles - tdp) * KS  (T * NW < 2^31, checked by the planner)
   int tdp;         // leading tiles that run data-parallel (a multiple of the grid size)
   int gm;          // m-blocks per tile group (sk_tile): 1 = n fastest
+  unsigned long long* prof;  // diagnostic builds only (fwd_sk_body PROF): per-wave cycle sums per loop phase
 };
 
 __device__ __forceinline__ int sk_start(int w, int T, int NW) { return (int)((unsigned)(w * T) / (unsigned)NW); }
@@ -1028,8 +1080,21 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
 // LDS-DMA left per K-step is the two A-plane pieces (the 8 dword DMA pieces of B cost ~60 issue cycles
 // each, more than the K-step's 12 MFMAs).  Every wave of the 1 x 4 layout reads its own 32 columns,
 // so nothing is lost by not sharing B through LDS.
+// PROF (diagnostic builds only, scripts/probe_sk.hip; never instantiated in the library): s_memtime stamps
+// around the BD loop's phases, summed per wave into sk.prof[wave][phase]: 0 the wait for the stage's A
+// pieces, 1 the barrier, 2 fragment reads + split + MFMA issue + the next stage's issue, 3 the closing
+// lgkmcnt(0), 4 the epilogue, 5 K-steps.  The stamps' own waits forbid overlaps the real kernel has:
+// read the shares, not the length (cdna_hip_programming.md §7, In-kernel stamps).
+__device__ __forceinline__ unsigned long long sk_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false, bool BP = false>
+          bool BD = false, bool BP = false, bool PROF = false>
 __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -1105,7 +1170,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   }
 
   f32x16 acc[TM][TN];
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};  // PROF: phase cycle sums (wave-uniform)
+  unsigned long long te = 0;
   while (true) {
+    if constexpr (PROF) {
+      if (te) ph[4] += sk_stamp() - te;  // the previous segment's epilogue (piece or output stores)
+      te = 0;
+    }
     int t, k_a, k_b;
     if (dp_t < sk.tdp) {
       t = dp_t;
@@ -1298,28 +1369,51 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // vmcnt(2 * INST_W) - a wave now and then read a stage's A slot before another wave's DMA piece
       // had landed; scripts/dbg_det.py, profiles/r04_bd_wait_race.txt).  The B registers are waited
       // for by the compiler at their use.
-      auto step = [&](int i, float (&cur)[8], float (&nxt)[8]) {
+      // BD: this K-step's B fragments, split one K-step ahead (mfma_stage_hd2); the prologue splits the first
+      Split2h bvc;
+      if constexpr (!BP) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if constexpr (H1) bvc.hi[j] = (_Float16)(bdq[0][j] * sB);
+          else split2h_set(bvc, j, bdq[0][j] * sB);
+        }
+      }
+      auto step = [&](int i, float (&cur)[8], float (&nxtraw)[8], float (&nxt)[8]) {
+        unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        if constexpr (PROF) t0 = sk_stamp();
         wait_vmcnt<2 * A_INST_W>();
+        if constexpr (PROF) t1 = sk_stamp();
         __builtin_amdgcn_s_barrier();
+        if constexpr (PROF) t2 = sk_stamp();
         const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
         auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt); };
         if constexpr (BP)
           mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
         else
-          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
+          mfma_stage_hd2<TM, BM, H1>(As, wm, lane, acc, mid, sB, nxtraw, bvc);
+        if constexpr (PROF) t3 = sk_stamp();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (PROF) {
+          const unsigned long long t4 = sk_stamp();
+          ph[0] += t1 - t0;
+          ph[1] += t2 - t1;
+          ph[2] += t3 - t2;
+          ph[3] += t4 - t3;
+          ph[5] += 1;
+        }
       };
       int i = 0;
       for (; i + 4 <= nst; i += 4) {
-        step(i, bdq[0], bdq[3]);
-        step(i + 1, bdq[1], bdq[0]);
-        step(i + 2, bdq[2], bdq[1]);
-        step(i + 3, bdq[3], bdq[2]);
+        step(i, bdq[0], bdq[1], bdq[3]);
+        step(i + 1, bdq[1], bdq[2], bdq[0]);
+        step(i + 2, bdq[2], bdq[3], bdq[1]);
+        step(i + 3, bdq[3], bdq[0], bdq[2]);
       }
-      if (i < nst) step(i, bdq[0], bdq[3]);
-      if (i + 1 < nst) step(i + 1, bdq[1], bdq[0]);
-      if (i + 2 < nst) step(i + 2, bdq[2], bdq[1]);
+      if (i < nst) step(i, bdq[0], bdq[1], bdq[3]);
+      if (i + 1 < nst) step(i + 1, bdq[1], bdq[2], bdq[0]);
+      if (i + 2 < nst) step(i + 2, bdq[2], bdq[3], bdq[1]);
       wait_vmcnt<0>();  // the stages issued past the end land before the slots are reused
+      if constexpr (PROF) te = sk_stamp();
     } else {
       // as in the BD form: a stage issued every K-step, past the end too, so one wait count
 #pragma unroll
@@ -1422,6 +1516,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         }
       }
   }
+  if constexpr (PROF) {
+    if (lane == 0) {  // vector stores of the wave-uniform sums (lane 0)
+      const int gw = blockIdx.x * (blockDim.x >> 6) + wid;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) sk.prof[gw * 8 + k] = ph[k];
+    }
+  }
 }
 
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false>
@@ -1432,9 +1533,9 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 // The same kernel held to two waves per SIMD (<= 256 VGPRs + AGPRs): the f16x3 form, left to the
 // compiler's default budget, takes 199 VGPRs + 64 AGPRs and one wave per SIMD.
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false, bool BP = false>
+          bool BD = false, bool BP = false, bool PROF = false>
 __global__ void __launch_bounds__(256, 2) k_igemm_fwd_sk2(FwdArgs a, SkArgs sk) {
-  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD, BP>(a, sk);
+  fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD, BP, PROF>(a, sk);
 }
 
 // sum of pieces w_lo..w_hi in that order (deterministic), eight loads in flight per step: a tile
