@@ -540,57 +540,6 @@ __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane,
   mid();
 }
 
-// The BD stage with the split software-pipelined (r05): bv holds this K-step's B fragments, split one
-// K-step earlier, and the next K-step's raw values (bnext) are split between this K-step's MFMAs
-// (sched_group_barrier: one MFMA, then a few VALU), so the split's VALU issues while the matrix pipe
-// works instead of in front of it (the in-kernel stamps put ~70 % of a K-step in the fragment reads +
-// split + MFMA issue, with the split in series before the MFMAs: scripts/probe_sk.py).
-template <int TM, int BM, bool HI_ONLY, typename F>
-__device__ __forceinline__ void mfma_stage_hd2(const float* As, int wm, int lane, f32x16 (&acc)[TM][1],
-                                               F&& mid, float sB, const float (&bnext)[8], Split2h& bv) {
-  const int l32 = lane & 31, h = lane >> 5;
-  const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
-  Split2h nb;
-  if constexpr (HI_ONLY) {
-    f16x8 av[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bv.hi, acc[i][0], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) nb.hi[j] = (_Float16)(bnext[j] * sB);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // then up to six VALU
-    }
-  } else {
-    Split2h av[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) av[i].lo = Ab[(2 + h) * BM + wm + i * 32 + l32];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bv.hi, acc[i][0], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv.lo, acc[i][0], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv.hi, acc[i][0], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) split2h_set(nb, j, bnext[j] * sB);
-#pragma unroll
-    for (int i = 0; i < 3 * TM; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // then up to five VALU
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  bv = nb;
-  mid();
-}
-
 // The BD stage with the image operand pre-split (k_split_img): braw holds the lane's hi plane (floats
 // 0..3 as 16 B) and lo plane (4..7), already scaled; no split work in the loop.
 template <int TM, int BM, bool HI_ONLY, typename F>
@@ -1080,11 +1029,13 @@ __device__ __forceinline__ int sk_worker_of(int i, int T, int NW) {
 // LDS-DMA left per K-step is the two A-plane pieces (the 8 dword DMA pieces of B cost ~60 issue cycles
 // each, more than the K-step's 12 MFMAs).  Every wave of the 1 x 4 layout reads its own 32 columns,
 // so nothing is lost by not sharing B through LDS.
-// PROF (diagnostic builds only, scripts/probe_sk.hip; never instantiated in the library): s_memtime stamps
-// around the BD loop's phases, summed per wave into sk.prof[wave][phase]: 0 the wait for the stage's A
-// pieces, 1 the barrier, 2 fragment reads + split + MFMA issue + the next stage's issue, 3 the closing
-// lgkmcnt(0), 4 the epilogue, 5 K-steps.  The stamps' own waits forbid overlaps the real kernel has:
-// read the shares, not the length (cdna_hip_programming.md §7, In-kernel stamps).
+// PROF (diagnostic builds only, scripts/probe_sk.hip; 0 in the library), bit 0: s_memtime stamps around
+// the BD loop's phases, summed per wave into sk.prof[wave][phase]: 0 the wait for the stage's A pieces,
+// 1 the barrier, 2 fragment reads + split + MFMA issue + the next stage's issue, 3 the closing
+// lgkmcnt(0), 4 the epilogue, 5 K-steps.  The stamps' own waits forbid overlaps the real kernel has: read
+// the shares, not the length (cdna_hip_programming.md §7, In-kernel stamps).  Timing-only ablations
+// (wrong results): bit 1 no image-operand loads (opaque zeros), bit 2 no A-plane LDS-DMA, bit 3 no
+// K-step barrier.
 __device__ __forceinline__ unsigned long long sk_stamp() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -1094,7 +1045,7 @@ __device__ __forceinline__ unsigned long long sk_stamp() {
 }
 
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false, bool BP = false, bool PROF = false>
+          bool BD = false, bool BP = false, int PROF = 0>
 __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   // one stream-K iteration = one LDS stage = G consecutive K-steps (16 channels of one tap each);
   // sk.KS counts stages per tile (a.ksteps / G).  PW: pointwise (one unshifted tap), so a B row
@@ -1173,7 +1124,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};  // PROF: phase cycle sums (wave-uniform)
   unsigned long long te = 0;
   while (true) {
-    if constexpr (PROF) {
+    if constexpr (PROF & 1) {
       if (te) ph[4] += sk_stamp() - te;  // the previous segment's epilogue (piece or output stores)
       te = 0;
     }
@@ -1266,7 +1217,8 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
           const int g = inst / (NQL * (BM / 64)), r = inst % (NQL * (BM / 64));
           const int qh = r / (BM / 64), mb = (r % (BM / 64)) * 64;
           const int ks = s * G + g;
-          dma_b128(rx, As + inst * 256, (unsigned)(((ks * NQ + qh) * a.lda + m0 + mb + lane) * 16));
+          if constexpr (!(PROF & 4))
+            dma_b128(rx, As + inst * 256, (unsigned)(((ks * NQ + qh) * a.lda + m0 + mb + lane) * 16));
         }
       } else {
         const unsigned a_base = (unsigned)s * a_stage_bytes;
@@ -1300,8 +1252,12 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
           // soffset
           const unsigned sb = (unsigned)__builtin_amdgcn_readfirstlane(cb16) * chan_bytes;
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vbdh, (int)(sb + j * chan_bytes), 0));
+          for (int j = 0; j < 8; ++j) {
+            if constexpr (PROF & 2)
+              asm volatile("v_mov_b32 %0, 0" : "=v"(bq[j]));
+            else
+              bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vbdh, (int)(sb + j * chan_bytes), 0));
+          }
         } else if constexpr (BPRE) {
           // piece (plane*2 + k half, 64-pixel half): lane = pixel, 16 B = 8 channels of a plane
 #pragma unroll
@@ -1369,31 +1325,22 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // vmcnt(2 * INST_W) - a wave now and then read a stage's A slot before another wave's DMA piece
       // had landed; scripts/dbg_det.py, profiles/r04_bd_wait_race.txt).  The B registers are waited
       // for by the compiler at their use.
-      // BD: this K-step's B fragments, split one K-step ahead (mfma_stage_hd2); the prologue splits the first
-      Split2h bvc;
-      if constexpr (!BP) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if constexpr (H1) bvc.hi[j] = (_Float16)(bdq[0][j] * sB);
-          else split2h_set(bvc, j, bdq[0][j] * sB);
-        }
-      }
-      auto step = [&](int i, float (&cur)[8], float (&nxtraw)[8], float (&nxt)[8]) {
+      auto step = [&](int i, float (&cur)[8], float (&nxt)[8]) {
         unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-        if constexpr (PROF) t0 = sk_stamp();
+        if constexpr (PROF & 1) t0 = sk_stamp();
         wait_vmcnt<2 * A_INST_W>();
-        if constexpr (PROF) t1 = sk_stamp();
-        __builtin_amdgcn_s_barrier();
-        if constexpr (PROF) t2 = sk_stamp();
+        if constexpr (PROF & 1) t1 = sk_stamp();
+        if constexpr (!(PROF & 8)) __builtin_amdgcn_s_barrier();
+        if constexpr (PROF & 1) t2 = sk_stamp();
         const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
         auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt); };
         if constexpr (BP)
           mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
         else
-          mfma_stage_hd2<TM, BM, H1>(As, wm, lane, acc, mid, sB, nxtraw, bvc);
-        if constexpr (PROF) t3 = sk_stamp();
+          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
+        if constexpr (PROF & 1) t3 = sk_stamp();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (PROF) {
+        if constexpr (PROF & 1) {
           const unsigned long long t4 = sk_stamp();
           ph[0] += t1 - t0;
           ph[1] += t2 - t1;
@@ -1404,16 +1351,16 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       };
       int i = 0;
       for (; i + 4 <= nst; i += 4) {
-        step(i, bdq[0], bdq[1], bdq[3]);
-        step(i + 1, bdq[1], bdq[2], bdq[0]);
-        step(i + 2, bdq[2], bdq[3], bdq[1]);
-        step(i + 3, bdq[3], bdq[0], bdq[2]);
+        step(i, bdq[0], bdq[3]);
+        step(i + 1, bdq[1], bdq[0]);
+        step(i + 2, bdq[2], bdq[1]);
+        step(i + 3, bdq[3], bdq[2]);
       }
-      if (i < nst) step(i, bdq[0], bdq[1], bdq[3]);
-      if (i + 1 < nst) step(i + 1, bdq[1], bdq[2], bdq[0]);
-      if (i + 2 < nst) step(i + 2, bdq[2], bdq[3], bdq[1]);
+      if (i < nst) step(i, bdq[0], bdq[3]);
+      if (i + 1 < nst) step(i + 1, bdq[1], bdq[0]);
+      if (i + 2 < nst) step(i + 2, bdq[2], bdq[1]);
       wait_vmcnt<0>();  // the stages issued past the end land before the slots are reused
-      if constexpr (PROF) te = sk_stamp();
+      if constexpr (PROF & 1) te = sk_stamp();
     } else {
       // as in the BD form: a stage issued every K-step, past the end too, so one wait count
 #pragma unroll
@@ -1516,7 +1463,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         }
       }
   }
-  if constexpr (PROF) {
+  if constexpr (PROF & 1) {
     if (lane == 0) {  // vector stores of the wave-uniform sums (lane 0)
       const int gw = blockIdx.x * (blockDim.x >> 6) + wid;
 #pragma unroll
@@ -1533,7 +1480,7 @@ __global__ void __launch_bounds__(256) k_igemm_fwd_sk(FwdArgs a, SkArgs sk) {
 // The same kernel held to two waves per SIMD (<= 256 VGPRs + AGPRs): the f16x3 form, left to the
 // compiler's default budget, takes 199 VGPRs + 64 AGPRs and one wave per SIMD.
 template <int BM, int BN, int G, int STAGES, int WM, int WN, bool PW = false, int MT = 0, bool ACC = false,
-          bool BD = false, bool BP = false, bool PROF = false>
+          bool BD = false, bool BP = false, int PROF = 0>
 __global__ void __launch_bounds__(256, 2) k_igemm_fwd_sk2(FwdArgs a, SkArgs sk) {
   fwd_sk_body<BM, BN, G, STAGES, WM, WN, PW, MT, ACC, BD, BP, PROF>(a, sk);
 }

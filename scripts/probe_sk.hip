@@ -51,12 +51,22 @@ extern "C" int probe_bd_fwd(const float* x, const float* packed, float* y, int c
   sk.T = (int)T;
   sk.prof = prof;
   const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
-  if (with_prof)
-    hipLaunchKernelGGL((k_igemm_fwd_sk2<128, kSkBN, 1, 4, 1, 4, false, kMathH3P, false, true, false, true>), grid, block,
-                       0, st, a, sk);
-  else
-    hipLaunchKernelGGL((k_igemm_fwd_sk2<128, kSkBN, 1, 4, 1, 4, false, kMathH3P, false, true, false, false>), grid,
-                       block, 0, st, a, sk);
+  // with_prof: 1 stamps; 2, 4, 8, 6, 14 timing-only ablations (dconv_kernels.h fwd_sk_body PROF)
+#define PROBE_CASE(V)                                                                                              \
+  case V:                                                                                                          \
+    hipLaunchKernelGGL((k_igemm_fwd_sk2<128, kSkBN, 1, 4, 1, 4, false, kMathH3P, false, true, false, V>), grid,     \
+                       block, 0, st, a, sk);                                                                       \
+    break;
+  switch (with_prof) {
+    PROBE_CASE(0)
+    PROBE_CASE(1)
+    PROBE_CASE(2)
+    PROBE_CASE(4)
+    PROBE_CASE(6)
+    PROBE_CASE(8)
+    PROBE_CASE(14)
+    default: return MSL_ERR_ARG;
+  }
   MSL_CHECK_LAUNCH();
   if (T > 0)
     hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), dim3(128 * kSkBN / 1024, (unsigned)(tiles - sk.tdp)), block, 0, st,
