@@ -506,10 +506,10 @@ __device__ __forceinline__ void mfma_stage_h1p(const float* As, const float* Bs,
 // f16x3 / fp16 stage with the B operand in registers (fwd_sk_body's BD form, r03): braw = this lane's
 // 8 image values B[k = 8h .. 8h+7][n = its pixel] of the K-step, loaded from global memory a few
 // K-steps ahead; A fragments from the LDS ring as in mfma_stage_h3p.  One K-step, one 32-pixel column
-// per wave (1 x 4 waves).
-template <int TM, int BM, bool HI_ONLY, typename F>
+// per wave (1 x 4 waves).  xf(j, v) maps a loaded value to the scaled operand (v * sB).
+template <int TM, int BM, bool HI_ONLY, typename F, typename X>
 __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane, f32x16 (&acc)[TM][1],
-                                              F&& mid, float sB, const float (&braw)[8]) {
+                                              F&& mid, X&& xf, const float (&braw)[8]) {
   const int l32 = lane & 31, h = lane >> 5;
   const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
   if constexpr (HI_ONLY) {
@@ -518,7 +518,7 @@ __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane,
     for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bv[j] = (_Float16)(braw[j] * sB);
+    for (int j = 0; j < 8; ++j) bv[j] = (_Float16)xf(j, braw[j]);
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bv, acc[i][0], 0, 0, 0);
   } else {
@@ -529,7 +529,7 @@ __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane,
     for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) split2h_set(bv, j, braw[j] * sB);
+    for (int j = 0; j < 8; ++j) split2h_set(bv, j, xf(j, braw[j]));
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bv.hi, acc[i][0], 0, 0, 0);
 #pragma unroll
@@ -1120,6 +1120,19 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     iA = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a.ascale[1])));
   }
 
+  // PROF & 16 (timing only): a BN-apply + ReLU of the image operand in the BD split, per-channel
+  // (alpha, beta) from an LDS table (alpha = sB, beta = 0: the identity on a non-negative image)
+  const float* tabp = nullptr;
+  if constexpr ((PROF & 16) != 0) {
+    __shared__ float bn_tab[2 * 2048];
+    for (int c = threadIdx.x; c < a.cimg; c += blockDim.x) {
+      const int cb = c >> 4, hh = (c >> 3) & 1, j = c & 7;
+      bn_tab[((cb * 2 + hh) * 2 + 0) * 8 + j] = sB;
+      bn_tab[((cb * 2 + hh) * 2 + 1) * 8 + j] = 0.f;
+    }
+    __syncthreads();
+    tabp = bn_tab;
+  }
   f32x16 acc[TM][TN];
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};  // PROF: phase cycle sums (wave-uniform)
   unsigned long long te = 0;
@@ -1201,7 +1214,9 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     };
     set_tap(c_tap);
     float bdq[4][8];  // BD: the register ring of B values (K-step i in slot i % 4)
-    auto issue = [&](int s, int slot, float (&bq)[8]) {
+    float bdv[4];     // PROF & 16: the ring's pixel validity (+inf / 0) and channel blocks
+    int bdc[4];
+    auto issue = [&](int s, int slot, float (&bq)[8], float& bv, int& bc) {
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
       if constexpr (AHALF) {
@@ -1251,6 +1266,10 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
           // drain the queue); an out-of-image pixel's voffset >= 2^31 is out of range whatever the
           // soffset
           const unsigned sb = (unsigned)__builtin_amdgcn_readfirstlane(cb16) * chan_bytes;
+          if constexpr ((PROF & 16) != 0) {
+            bv = vbdh != OOB ? __builtin_inff() : 0.f;
+            bc = __builtin_amdgcn_readfirstlane(c_cb);
+          }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             if constexpr (PROF & 2)
@@ -1311,9 +1330,9 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // the compiler's wait-count analysis saw paths with no younger loads and drained the queue -
       // vmcnt(0) - before the split of every first and fourth K-step; r04.  Those drains had also
       // hidden the LDS-DMA ordering race described at the wait below.)
-      issue(k_a, 0, bdq[0]);
-      issue(k_a + 1, 1, bdq[1]);
-      issue(k_a + 2, 2, bdq[2]);
+      issue(k_a, 0, bdq[0], bdv[0], bdc[0]);
+      issue(k_a + 1, 1, bdq[1], bdv[1], bdc[1]);
+      issue(k_a + 2, 2, bdq[2], bdv[2], bdc[2]);
       // K-step i: wait until stage i + 1 landed (only stage i + 2 younger), barrier (stage i + 1 is
       // complete in every wave's LDS pieces, and every wave has read slot i - 1's fragments, at step
       // i - 2), issue stage i + 3 into that slot and ring entry, read + split K-step i + 1's fragments,
@@ -1325,7 +1344,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // vmcnt(2 * INST_W) - a wave now and then read a stage's A slot before another wave's DMA piece
       // had landed; scripts/dbg_det.py, profiles/r04_bd_wait_race.txt).  The B registers are waited
       // for by the compiler at their use.
-      auto step = [&](int i, float (&cur)[8], float (&nxt)[8]) {
+      auto step = [&](int i, float (&cur)[8], float (&nxt)[8], float& curv, float& nxtv, int& curc, int& nxtc) {
         unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
         if constexpr (PROF & 1) t0 = sk_stamp();
         wait_vmcnt<2 * A_INST_W>();
@@ -1333,11 +1352,21 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         if constexpr (!(PROF & 8)) __builtin_amdgcn_s_barrier();
         if constexpr (PROF & 1) t2 = sk_stamp();
         const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
-        auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt); };
-        if constexpr (BP)
+        auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt, nxtv, nxtc); };
+        if constexpr (BP) {
           mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
-        else
-          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, sB, cur);
+        } else if constexpr ((PROF & 16) != 0) {
+          const float4* tq = reinterpret_cast<const float4*>(tabp + (curc * 2 + (lane >> 5)) * 16);
+          const float4 a0 = tq[0], a1 = tq[1], b0 = tq[2], b1 = tq[3];
+          const float al[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          const float be[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+          const float vm = curv;
+          mfma_stage_hd<TM, BM, H1>(
+              As, wm, lane, acc, mid,
+              [&](int j, float v) { return __builtin_amdgcn_fmed3f(fmaf(v, al[j], be[j]), 0.f, vm); }, cur);
+        } else {
+          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, [&](int, float v) { return v * sB; }, cur);
+        }
         if constexpr (PROF & 1) t3 = sk_stamp();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (PROF & 1) {
@@ -1351,25 +1380,25 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       };
       int i = 0;
       for (; i + 4 <= nst; i += 4) {
-        step(i, bdq[0], bdq[3]);
-        step(i + 1, bdq[1], bdq[0]);
-        step(i + 2, bdq[2], bdq[1]);
-        step(i + 3, bdq[3], bdq[2]);
+        step(i, bdq[0], bdq[3], bdv[0], bdv[3], bdc[0], bdc[3]);
+        step(i + 1, bdq[1], bdq[0], bdv[1], bdv[0], bdc[1], bdc[0]);
+        step(i + 2, bdq[2], bdq[1], bdv[2], bdv[1], bdc[2], bdc[1]);
+        step(i + 3, bdq[3], bdq[2], bdv[3], bdv[2], bdc[3], bdc[2]);
       }
-      if (i < nst) step(i, bdq[0], bdq[3]);
-      if (i + 1 < nst) step(i + 1, bdq[1], bdq[0]);
-      if (i + 2 < nst) step(i + 2, bdq[2], bdq[1]);
+      if (i < nst) step(i, bdq[0], bdq[3], bdv[0], bdv[3], bdc[0], bdc[3]);
+      if (i + 1 < nst) step(i + 1, bdq[1], bdq[0], bdv[1], bdv[0], bdc[1], bdc[0]);
+      if (i + 2 < nst) step(i + 2, bdq[2], bdq[1], bdv[2], bdv[1], bdc[2], bdc[1]);
       wait_vmcnt<0>();  // the stages issued past the end land before the slots are reused
       if constexpr (PROF & 1) te = sk_stamp();
     } else {
       // as in the BD form: a stage issued every K-step, past the end too, so one wait count
 #pragma unroll
-    for (int k = 0; k < STAGES - 1; ++k) issue(k_a + k, k, bdq[0]);
+    for (int k = 0; k < STAGES - 1; ++k) issue(k_a + k, k, bdq[0], bdv[0], bdc[0]);
     for (int i = 0; i < nst; ++i) {
       wait_vmcnt<(STAGES - 2) * INST_W>();
       __builtin_amdgcn_s_barrier();
       const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
-      auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, bdq[0]); };
+      auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, bdq[0], bdv[0], bdc[0]); };
       if constexpr (MT == kMathBf16)
         mfma_stage_bf16<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (MT == kMathX6)

@@ -38,8 +38,11 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--hw", type=int, nargs=2, default=[65, 129])
     ap.add_argument("--nimg", type=int, default=2)
+    ap.add_argument("--unfused", action="store_true", help="the two-kernel form (k_bn_stats + k_bn_apply)")
     args = ap.parse_args()
     lib = hip.load()
+    if args.unfused:
+        lib.msl_bn_set_fused(0)
     p = args.hw[0] * args.hw[1]
     n = args.nimg
     s = hip.stream_ptr()
@@ -79,7 +82,7 @@ def main():
         t = timed(bwd(True), args.reps)
         rec["bwd_us"] = round(t, 2)
         rec["bwd_TBps"] = round(mb * ((3 if relu else 2) + (2 if res else 1)) / t, 3)
-        if relu and not res:
+        if relu and not res and not args.unfused:
             t = timed(bwd(False), args.reps)
             rec["bwd_remask_us"] = round(t, 2)
             rec["bwd_remask_TBps"] = round(mb * 3 / t, 3)

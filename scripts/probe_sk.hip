@@ -51,7 +51,8 @@ extern "C" int probe_bd_fwd(const float* x, const float* packed, float* y, int c
   sk.T = (int)T;
   sk.prof = prof;
   const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
-  // with_prof: 1 stamps; 2, 4, 8, 6, 14 timing-only ablations (dconv_kernels.h fwd_sk_body PROF)
+  // with_prof: 1 stamps; 2, 4, 8, 6, 14 timing-only ablations, 16 a BN-apply of the image operand
+  // (dconv_kernels.h fwd_sk_body PROF)
 #define PROBE_CASE(V)                                                                                              \
   case V:                                                                                                          \
     hipLaunchKernelGGL((k_igemm_fwd_sk2<128, kSkBN, 1, 4, 1, 4, false, kMathH3P, false, true, false, V>), grid,     \
@@ -65,6 +66,7 @@ extern "C" int probe_bd_fwd(const float* x, const float* packed, float* y, int c
     PROBE_CASE(6)
     PROBE_CASE(8)
     PROBE_CASE(14)
+    PROBE_CASE(16)
     default: return MSL_ERR_ARG;
   }
   MSL_CHECK_LAUNCH();

@@ -53,12 +53,15 @@ def timed(p, reps=20):
 
 
 t_plain, t_prof = timed(0), timed(1)
-abl = {name: round(timed(v), 1) for v, name in ((2, "no B loads"), (4, "no A DMA"), (6, "no B loads, no A DMA"),
+abl = {name: round(timed(v), 1) for v, name in ((16, "BN apply in the split (identity table)"), (2, "no B loads"), (4, "no A DMA"), (6, "no B loads, no A DMA"),
                                                 (8, "no barrier"), (14, "no loads, no DMA, no barrier"))}
 ok_plain = None
 run(0)
 torch.cuda.synchronize()
 ok_plain = torch.equal(y, y_ref)
+run(16)
+torch.cuda.synchronize()
+ok_apply = torch.equal(y, y_ref)
 prof.zero_()
 run(1)
 torch.cuda.synchronize()
@@ -67,7 +70,7 @@ steps = ph[:, 5].sum().item()
 tot = ph[:, :5].sum(0)
 names = ["wait A pieces (vmcnt)", "barrier", "frag reads + split + MFMA issue + next issue", "lgkmcnt(0)", "epilogue"]
 out = {"shape": [cin, cout, h, w, nimg, d], "workers": nw, "us_plain": round(t_plain, 1), "us_stamped": round(t_prof, 1), "us_ablations": abl,
-       "plain_output_bitexact_vs_library": ok_plain, "kstep_waves": steps,
+       "plain_output_bitexact_vs_library": ok_plain, "apply_output_bitexact_vs_library": ok_apply, "kstep_waves": steps,
        "cycles_per_kstep": {n: round(tot[i].item() / steps, 1) for i, n in enumerate(names)},
        "shares": {n: round(tot[i].item() / tot.sum().item(), 3) for i, n in enumerate(names)}}
 print(json.dumps(out))
