@@ -14,15 +14,10 @@
  *     allocator on the Python side).  The library allocates nothing; scratch
  *     comes from the caller's workspace, sized by the matching *_workspace()
  *     query, and no call leaves state that a later call reads.
- *   - Process-wide configuration: four switches select kernel FORMS, not
- *     results' meaning - msl_conv_set_f32_form, msl_conv_set_pack_form,
- *     msl_conv_set_sk_hybrid and msl_bn_set_fused.  They are process-wide
- *     atomics (not thread_local: PyTorch's autograd engine launches the
- *     backward from its own per-device thread, which must see the forms the
- *     main thread chose), read once per call on the host at launch time.
- *     Set them at start-up, before work is enqueued: a concurrent set is
- *     well defined but takes effect at an arbitrary call boundary, and a
- *     captured hipGraph keeps the forms that were current at capture.
+ *   - No process state (ABI 3): the kernel FORMS of a call - which matrix-core
+ *     form, schedule or BN kernel runs, not what the result means - come with
+ *     the call as a const msl_forms* (NULL = the defaults), read on the host
+ *     at launch time, so a captured hipGraph keeps the forms of its capture.
  *   - Work is enqueued on the given hipStream_t (passed as msl_stream_t) and
  *     is stream-ordered; no entry point synchronises the host, so every call
  *     is safe to capture in a hipGraph.
@@ -49,32 +44,38 @@ typedef void* msl_stream_t; /* a hipStream_t */
 int msl_abi_version(void);
 const char* msl_status_string(int status);
 
-/* Length (ints) of the arrival-counter array the conv forward / data-gradient calls take.
- * Reserved: the current stream-K kernels never read or write it (split tiles are summed by a
- * separate reduce launch, with no inter-workgroup signalling), so no call depends on its
- * contents; it stays in the signatures for ABI stability.  Pass a zero-filled array of this
- * length (non-NULL is checked). */
-int msl_counter_elems(void);
-
-/* Matrix-core form of the fp32 conv entry points (msl_dconv_* / msl_pconv_* without _bf16),
- * process-wide: 0 = v_mfma_f32_32x32x2_f32 (exact fmaf chain), 2 = each fp32 operand split
- * into three bf16 terms, six products per 16-deep K slice on v_mfma_f32_32x32x16_bf16 with fp32
- * accumulation (fp32-accurate), 5 = each operand tensor scaled by a power of two
- * (its absolute maximum brought to [2^14, 2^15)) and split into two fp16 terms, three products
- * per slice on v_mfma_f32_32x32x16_f16 with fp32 accumulation, the result unscaled exactly
- * (fp32-accurate: the 3xTF32 scheme at fp16's 11-bit significand; the default).  Returns MSL_ERR_ARG for
- * any other value.  Packs are form-specific (form 5 writes fp16 planes and the weights' scale):
- * repack after changing the form.  Replaces nothing in the reference (its convs are cuDNN fp32). */
-int msl_conv_set_f32_form(int form);
-int msl_conv_f32_form(void);
-/* Weight-pack kernel (process-wide; identical packed bytes either way): 1 = one LDS-transposing
- * pack+split launch per msl_*_pack call (default), 0 = element-wise gather + separate split. */
-int msl_conv_set_pack_form(int form);
-/* Schedule of the forward-form conv kernels (fwd and data gradient; process-wide; same results
- * up to the fp32 summation order of split tiles): 1 = when the output tiles outnumber the 512
- * workgroups, whole rounds of tiles run data-parallel and only the remainder is split stream-K
- * (default); 0 = pure stream-K (every tile range-split over 512 workgroups). */
-int msl_conv_set_sk_hybrid(int on);
+/* The kernel forms of a call (ABI 3: replaces ABI 2's process-wide setters msl_conv_set_f32_form,
+ * msl_conv_set_pack_form, msl_conv_set_sk_hybrid, msl_bn_set_fused and the reserved int* counters
+ * argument, which no kernel read).  Every conv, pack and BN entry point takes one; NULL = the
+ * defaults {5, 1, 1, 1}.  A bad value is MSL_ERR_ARG.
+ *   f32_form  matrix-core form of the fp32 conv entry points (msl_dconv_* / msl_pconv_* without
+ *             _bf16 / _f16) and of the packs: 0 = v_mfma_f32_32x32x2_f32 (exact fmaf chain), 2 = each
+ *             fp32 operand split into three bf16 terms, six products per 16-deep K slice on
+ *             v_mfma_f32_32x32x16_bf16 with fp32 accumulation (fp32-accurate), 5 = each operand tensor
+ *             scaled by a power of two (its absolute maximum brought to [2^14, 2^15)) and split into
+ *             two fp16 terms, three products per slice on v_mfma_f32_32x32x16_f16 with fp32
+ *             accumulation, the result unscaled exactly (fp32-accurate: the 3xTF32 scheme at fp16's
+ *             11-bit significand; the default).  Packs are form-specific (form 5 writes fp16 planes
+ *             and the weights' scale): a conv call must pass the f32_form its pack was made with; the
+ *             _f16 entry points need packs made with form 5.  Replaces nothing in the reference (its
+ *             convs are cuDNN fp32).
+ *   sk_hybrid schedule of the forward-form kernels (fwd and data gradient; same results up to the
+ *             fp32 summation order of split tiles): 1 = when the output tiles outnumber the 512
+ *             workgroups, whole rounds of tiles run data-parallel and only the remainder is split
+ *             stream-K (default); 0 = pure stream-K.
+ *   pack_form weight-pack kernel (identical packed bytes either way): 1 = one LDS-transposing
+ *             pack+split launch per pack call (default), 0 = element-wise gather + separate split.
+ *   bn_fused  BN kernel form: 1 = train-mode layers with p <= 16384 (or p <= 33792 and c >= 128) run
+ *             one fused statistics+apply launch per call (one block per channel, operands held in
+ *             registers; default), 0 = the split statistics / flat-apply launches everywhere. */
+typedef struct msl_forms {
+  int f32_form;
+  int sk_hybrid;
+  int pack_form;
+  int bn_fused;
+} msl_forms;
+int msl_forms_default(msl_forms* out);       /* writes the defaults */
+int msl_forms_check(const msl_forms* forms); /* MSL_OK (NULL included) or MSL_ERR_ARG */
 
 /* ------------------------------------------------------------------------
  * Dilated 3x3 convolution, stride 1, padding = dilation, as an FP32-MFMA
@@ -110,28 +111,28 @@ long long msl_conv_pack_blocks(int nbranch, int taps, int cin, int cout, int for
  * msl_conv_pack_blocks; block_start[njobs] = total_blocks).  Byte-identical to the per-job calls;
  * replaces the ~120 per-conv pack launches of a training step by two. */
 int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, int njobs, int taps,
-                       long long total_blocks, msl_stream_t stream);
+                       long long total_blocks, const msl_forms* forms, msl_stream_t stream);
 int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin, int cout,
-                   int for_dgrad, float* packed, msl_stream_t stream);
+                   int for_dgrad, float* packed, const msl_forms* forms, msl_stream_t stream);
 
 /* y[cout][h][w] = sum_b conv3x3(x, W_b, dil_b) (+ sum_b bias[b][cout] if bias)
  * replaces nn.Conv2d.forward at deeplab_multi.py:35 (layer3/4) and :63-65 (ASPP). */
 size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w, int nimg);
 int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                   size_t ws_bytes, msl_stream_t stream);
 
 /* dx[cin][h][w] = sum_b conv3x3^T(dy, W_b, dil_b)   (autograd of the same sites) */
 size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg);
 int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                    int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                     size_t ws_bytes, msl_stream_t stream);
 
 /* dw[b][cout][cin][3][3] (= or += when accumulate) and, if dbias != NULL,
  * dbias[b][cout] = sum_px dy (identical for both branches). */
 size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg);
 int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, const msl_forms* forms, void* ws,
                     size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
@@ -143,29 +144,29 @@ int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, in
  * Weights [cout][cin] (= [cout][cin][1][1]).
  * ---------------------------------------------------------------------- */
 long long msl_pconv_packed_elems(int cin, int cout, int for_dgrad);
-int msl_pconv_pack(const float* w, int cin, int cout, int for_dgrad, float* packed,
+int msl_pconv_pack(const float* w, int cin, int cout, int for_dgrad, float* packed, const msl_forms* forms,
                    msl_stream_t stream);
 
 /* y[cout][p] = sum_ci W[cout][ci] x[ci][p] */
 size_t msl_pconv_fwd_workspace(int cin, int cout, int p);
 int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
-                  int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+                  const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* dx[cin][p] = sum_co W[co][cin] dy[co][p] */
 size_t msl_pconv_dgrad_workspace(int cin, int cout, int p);
 int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                    int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+                    const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
 /* msl_pconv_dgrad with accumulate = 1: dx += W^T dy (dx read and written by the GEMM's own
  * epilogue / piece reduce; the bottleneck's residual gradient summed without a separate add).
  * accumulate = 0 is msl_pconv_dgrad.  Replaces autograd's grad accumulation at the block input
  * (Bottleneck.forward, deeplab_multi.py:31-48: conv1(x) and the identity residual both read x). */
 int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                        int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+                        int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* dw[cout][cin] (= or += when accumulate) = sum_p dy[cout][p] x[cin][p] */
 size_t msl_pconv_wgrad_workspace(int cin, int cout, int p);
 int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,
-                    int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream);
+                    int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * The stem and the strided glue of ResNetMulti (csrc/stem.hip), all gather forms without atomics
@@ -196,7 +197,7 @@ int msl_subsample_bwd(const float* dy, int c, int h, int w, int stride, int ho, 
                       msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
- * Operand scales of the f16x3 form (msl_conv_set_f32_form(5)).  Each GEMM operand is scaled by a
+ * Operand scales of the f16x3 form (msl_forms.f32_form 5).  Each GEMM operand is scaled by a
  * power of two derived from absolute maxima and split into two fp16 terms.  The maxima come as
  * PER-ROW partials: msl_absmax_partials writes part[r] = max |x[r][.]| for each of the `rows` rows
  * (channels) of a [rows][row_len] tensor, and msl_bn_fwd_am / msl_bn_bwd_am write the same per-
@@ -213,23 +214,23 @@ int msl_subsample_bwd(const float* dy, int c, int h, int w, int stride, int ho, 
  * ---------------------------------------------------------------------- */
 int msl_absmax_partials(const float* x, int rows, int row_len, float* part, msl_stream_t stream);
 int msl_dconv_fwd_sc(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                     int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                     int cin, int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                      size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart);
 int msl_dconv_dgrad_sc(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                       int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                       int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                        size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart);
 int msl_dconv_wgrad_sc(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                       int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
+                       int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, const msl_forms* forms, void* ws,
                        size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
                        const float* dy_part, int dy_npart);
 int msl_pconv_fwd_sc(const float* x, const float* packed, float* y, int cin, int cout, int p,
-                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                     const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
                      int x_npart);
 int msl_pconv_dgrad_acc_sc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                           int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                           int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream,
                            const float* dy_part, int dy_npart);
 int msl_pconv_wgrad_sc(const float* x, const float* dy, float* dw, int cin, int cout, int p,
-                       int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                       int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
                        int x_npart, const float* dy_part, int dy_npart);
 
 /* ------------------------------------------------------------------------
@@ -261,26 +262,26 @@ int msl_aspp_shift_gather(const float* dy, float* g, float* dbias, int nbranch, 
  * v_mfma_f32_32x32x16_bf16 with fp32 accumulation.  Same reference sites.
  * ---------------------------------------------------------------------- */
 int msl_dconv_fwd_bf16(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                       int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                       int cin, int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                        size_t ws_bytes, msl_stream_t stream);
 int msl_dconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                         int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                         int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                          size_t ws_bytes, msl_stream_t stream);
 int msl_dconv_wgrad_bf16(const float* x, const float* dy, float* dw, float* dbias, int nbranch,
-                         int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate,
+                         int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, const msl_forms* forms,
                          void* ws, size_t ws_bytes, msl_stream_t stream);
 int msl_pconv_fwd_bf16(const float* x, const float* packed, float* y, int cin, int cout, int p,
-                       int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+                       const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
 int msl_pconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout,
-                         int p, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream);
+                         int p, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
 int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, int cout, int p,
-                         int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream);
+                         int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * FP16-MFMA forms (BASELINE config 5's fp16 MFMA path): each operand tensor scaled by a power of
  * two (its absolute maximum into [2^14, 2^15)) and rounded to fp16 once - the weights at pack
  * time, as the hi planes of the f16x3 packs, so the packs must be made in the f16x3 fp32 form
- * (msl_conv_set_f32_form(5), the default; MSL_ERR_ARG otherwise) - then one
+ * (forms.f32_form 5, the default; MSL_ERR_ARG for another f32_form) - then one
  * v_mfma_f32_32x32x16_f16 per 16-deep K slice with fp32 accumulation, the result unscaled
  * exactly (M <= 64: 64-row fp16 tiles, r04; the weight gradients with fewer than 128 channels on either
  * side keep exact f32 MFMA tiles).  Operand partials as in
@@ -288,20 +289,20 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
  * accumulate flag of msl_pconv_dgrad_acc.  Same workspaces and results layout.
  * ---------------------------------------------------------------------- */
 int msl_dconv_fwd_f16(const float* x, const float* packed, const float* bias, float* y, int nbranch, int cin,
-                      int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                      int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws, size_t ws_bytes,
                       msl_stream_t stream, const float* x_part, int x_npart);
 int msl_dconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin, int cout,
-                        int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                        int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws, size_t ws_bytes,
                         msl_stream_t stream, const float* dy_part, int dy_npart);
 int msl_dconv_wgrad_f16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin, int cout,
-                        int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws, size_t ws_bytes,
+                        int h, int w, int nimg, int dil0, int dil1, int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes,
                         msl_stream_t stream, const float* x_part, int x_npart, const float* dy_part, int dy_npart);
-int msl_pconv_fwd_f16(const float* x, const float* packed, float* y, int cin, int cout, int p, int* counters,
+int msl_pconv_fwd_f16(const float* x, const float* packed, float* y, int cin, int cout, int p, const msl_forms* forms,
                       void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart);
 int msl_pconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                        int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                        int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream,
                         const float* dy_part, int dy_npart);
-int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int cout, int p, int accumulate,
+int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int cout, int p, int accumulate, const msl_forms* forms,
                         void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
                         const float* dy_part, int dy_npart);
 /* 1 if the weight gradient of this conv (taps 9: msl_dconv_wgrad*, h x w maps of nimg images;
@@ -409,7 +410,7 @@ size_t msl_bn_workspace(int c, int p, int nimg);
 int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const float* residual,
                float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
                float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
-               int update_running, float momentum, float eps, int relu, void* ws,
+               int update_running, float momentum, float eps, int relu, const msl_forms* forms, void* ws,
                size_t ws_bytes, msl_stream_t stream);
 /* dx (nullable), dres = d residual (nullable), dgamma / dbeta (nullable, = or += when
  * accumulate_params: the training step accumulates straight into the flat gradient buffer);
@@ -417,7 +418,7 @@ int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const floa
 int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gamma,
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
                float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
-               int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream);
+               int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
 /* msl_bn_fwd / msl_bn_bwd that also write absmax[c] = max |y[c][.]| (forward) or max |dx[c][.]|
  * (backward; dx required): the per-channel absmax partials (c of them) that the f16x3 conv
  * entry points (_sc) take for the tensor this BN produced - the next conv's input, or the
@@ -426,12 +427,12 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
 int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const float* residual,
                   float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
                   float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
-                  int update_running, float momentum, float eps, int relu, void* ws,
+                  int update_running, float momentum, float eps, int relu, const msl_forms* forms, void* ws,
                   size_t ws_bytes, msl_stream_t stream, float* absmax);
 int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* gamma,
                   const float* save_mean, const float* save_invstd, float* dx, float* dres,
                   float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
-                  int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx);
+                  int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx);
 /* msl_bn_bwd_am that may take y = NULL with relu for a BN WITHOUT a residual: the fused kernel
  * then recomputes the ReLU mask from x (y > 0 <=> fma(x, invstd*gamma, fma(-mean, invstd*gamma,
  * beta)) > 0, the forward's own float operations on the saved mean / invstd, so the mask is
@@ -441,16 +442,11 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
 int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const float* gamma,
                        const float* beta, const float* save_mean, const float* save_invstd, float* dx,
                        float* dres, float* dgamma, float* dbeta, int c, int p, int nimg, int training,
-                       int relu, int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream,
+                       int relu, int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream,
                        float* absmax_dx);
 /* 1 if msl_bn_fwd / msl_bn_bwd run the fused one-block-per-channel kernels for this shape (their
  * _am absmax output is then free; the split forms add a pass over the output). */
-int msl_bn_uses_fused(int c, int p, int training);
-/* BN kernel form (process-wide): 1 = train-mode layers with p <= 16384 (or p <= 33792 and
- * c >= 128) run one fused statistics+apply launch per call (one block per channel, operands held in registers), 0 =
- * the split statistics / flat-apply launches everywhere.  Returns 0, or MSL_ERR_ARG. */
-int msl_bn_set_fused(int fused);
-int msl_bn_fused(void);
+int msl_bn_uses_fused(int c, int p, int training, const msl_forms* forms);
 
 /* ------------------------------------------------------------------------
  * Training-time evaluation (tools/train_source.py:280-283 + utils/eval.py:109-118): for one

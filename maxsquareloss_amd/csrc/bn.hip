@@ -17,7 +17,6 @@
 // channels it touches).  Backward: per-channel reduce (sum g, sum g*xhat with g = dy masked by
 // y > 0 when ReLU) + flat apply (dx, d residual, dgamma, dbeta).  HBM-bound: fwd reads x twice,
 // writes y (+ reads the residual); bwd reads dy, x, y twice, writes dx (+ dres).
-#include <atomic>
 #include "msl_internal.h"
 
 namespace msl {
@@ -404,8 +403,8 @@ int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
 }
 constexpr int kBnRemaskMaxEpt = 16;  // msl_bn_bwd_am_beta's y = NULL: p <= 16 * 1024
 constexpr int kBnFusedMaxP = 33 * kBnFusedThreads;  // layer1 at 1024x512: 257x129 = 33153 px
-static std::atomic<int> g_bn_fused{1};  // msl_bn_set_fused; process-wide + atomic as dconv.hip's forms
-static bool bn_fused_enabled() { return g_bn_fused != 0; }
+// forms.bn_fused (msl_forms, per call): the fused kernels where bn_fused_shape allows them
+static bool bn_fused_enabled(const msl_forms* forms) { return forms_of(forms).bn_fused != 0; }
 // beyond 16 elements per lane only with >= 128 channels: at 64 blocks (layer1's 64-channel
 // maps) the split kernels' wider grids win the backward (profiles/r01_bn_forms.txt)
 static bool bn_fused_shape(int c, int p) {
@@ -620,16 +619,9 @@ using namespace msl;
 
 extern "C" {
 
-int msl_bn_set_fused(int fused) {
-  if (fused != 0 && fused != 1) return MSL_ERR_ARG;
-  g_bn_fused = fused;
-  return MSL_OK;
-}
-
-int msl_bn_fused(void) { return g_bn_fused; }
-
-int msl_bn_uses_fused(int c, int p, int training) {
-  return training && bn_fused_enabled() && c >= 1 && p >= 1 && bn_fused_shape(c, p) ? 1 : 0;
+int msl_bn_uses_fused(int c, int p, int training, const msl_forms* forms) {
+  if (forms_bad(forms)) return MSL_ERR_ARG;
+  return training && bn_fused_enabled(forms) && c >= 1 && p >= 1 && bn_fused_shape(c, p) ? 1 : 0;
 }
 
 size_t msl_bn_workspace(int c, int p, int nimg) {
@@ -639,17 +631,17 @@ size_t msl_bn_workspace(int c, int p, int nimg) {
 int msl_bn_fwd(const float* x, const float* gamma, const float* beta, const float* residual,
                float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
                float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
-               int update_running, float momentum, float eps, int relu, void* ws,
+               int update_running, float momentum, float eps, int relu, const msl_forms* forms, void* ws,
                size_t ws_bytes, msl_stream_t stream) {
   return msl_bn_fwd_am(x, gamma, beta, residual, y, running_mean, running_var, num_batches_tracked, save_mean,
-                       save_invstd, c, p, nimg, training, update_running, momentum, eps, relu, ws, ws_bytes, stream,
+                       save_invstd, c, p, nimg, training, update_running, momentum, eps, relu, forms, ws, ws_bytes, stream,
                        nullptr);
 }
 
 int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const float* residual,
                   float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
                   float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
-                  int update_running, float momentum, float eps, int relu, void* ws,
+                  int update_running, float momentum, float eps, int relu, const msl_forms* forms, void* ws,
                   size_t ws_bytes, msl_stream_t stream, float* absmax) {
   if (!x || !y || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
     return MSL_ERR_ARG;
@@ -660,7 +652,8 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
   if (training && ws_bytes < msl_bn_workspace(c, p, nimg)) return MSL_ERR_WORKSPACE;
   double* part = (double*)ws;
   const bool vec = al16(x) && al16(y) && (!residual || al16(residual));
-  const bool fused = training && bn_fused_enabled() && bn_fused_shape(c, p);
+  if (forms_bad(forms)) return MSL_ERR_ARG;
+  const bool fused = training && bn_fused_enabled(forms) && bn_fused_shape(c, p);
   if (training && !fused) {
     if (vec)
       hipLaunchKernelGGL(k_bn_stats<true>, dim3(R, S), dim3(256), 0, st, x, p, S, part);
@@ -705,27 +698,28 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
 int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gamma,
                const float* save_mean, const float* save_invstd, float* dx, float* dres,
                float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
-               int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream) {
+               int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream) {
   return msl_bn_bwd_am(dy, x, y, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, nimg, training, relu,
-                       accumulate_params, ws, ws_bytes, stream, nullptr);
+                       accumulate_params, forms, ws, ws_bytes, stream, nullptr);
 }
 
 int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* gamma,
                   const float* save_mean, const float* save_invstd, float* dx, float* dres,
                   float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
-                  int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
+                  int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
   if (relu && !y) return MSL_ERR_ARG;
   return msl_bn_bwd_am_beta(dy, x, y, gamma, nullptr, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, nimg,
-                            training, relu, accumulate_params, ws, ws_bytes, stream, absmax_dx);
+                            training, relu, accumulate_params, forms, ws, ws_bytes, stream, absmax_dx);
 }
 
 int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const float* gamma, const float* beta,
                        const float* save_mean, const float* save_invstd, float* dx, float* dres,
                        float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
-                       int accumulate_params, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
+                       int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
   if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
     return MSL_ERR_ARG;
-  const bool fused = training && bn_fused_enabled() && bn_fused_shape(c, p);
+  if (forms_bad(forms)) return MSL_ERR_ARG;
+  const bool fused = training && bn_fused_enabled(forms) && bn_fused_shape(c, p);
   // the mask recompute is the fused kernels' alone, up to 16 elements per lane
   if (relu && !y && !(fused && p <= kBnRemaskMaxEpt * kBnFusedThreads)) return MSL_ERR_ARG;
   if (absmax_dx && !dx) return MSL_ERR_ARG;

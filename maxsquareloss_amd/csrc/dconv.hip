@@ -22,7 +22,6 @@
 // read is a conflict-free ds_read_b32 of 32 consecutive floats), double
 // buffered, one barrier per K-step.  Small GEMMs are split along K into fp32
 // slabs that a reduce kernel sums deterministically (fixed order).
-#include <atomic>
 #include "dconv_kernels.h"
 
 namespace msl {
@@ -263,19 +262,14 @@ __global__ void __launch_bounds__(256) k_pack_split_many(const msl_pack_job* __r
 // persistent workgroups (2 per CU), so every CU gets the same number of MFMA stages whatever
 // the tile count.  The split-K tile kernel remains for an odd K-step count with M <= 32.
 constexpr int kSkBN = 128, kSkNW = 512;
-// Forward-form schedule (msl_conv_set_sk_hybrid): 1 = data-parallel rounds + stream-K remainder
-// when the tiles outnumber the workers (SkArgs), 0 = pure stream-K.  Process-wide, not per thread:
-// PyTorch's autograd engine issues the backward launches from its own per-device worker thread,
-// so a thread-local form set on the main thread would not reach them.  Atomic, so a setter racing
-// a launching thread is well defined (each launch reads a switch once).
-static std::atomic<int> g_sk_hybrid{1};
-// Matrix-core form of the fp32 entry points (msl_conv_set_f32_form): kMathF32 runs
+// The call's forms (msl_forms, r05: per call, no process state): sk_hybrid = the forward-form
+// schedule (1: data-parallel rounds + stream-K remainder when the tiles outnumber the workers,
+// SkArgs; 0: pure stream-K); f32_form = the matrix-core form of the fp32 entry points: kMathF32 runs
 // v_mfma_f32_32x32x2_f32 (an exact fmaf chain), kMathX6 the three-way bf16 split on the BF16
 // matrix cores (fp32-accurate, dconv_kernels.h; layer3 fwd 78 vs 102 us in the step, err vs fp64
 // 4e-8 vs 6e-8 relative to sum|terms|), kMathH3P the scaled two-way fp16 split (three fp16
-// MFMAs per slice; dconv_kernels.h Split2h).  Process-wide and atomic like g_sk_hybrid; packs are form-specific.
-static std::atomic<int> g_f32_form{kMathH3P};
-constexpr int kMaxCounters = 65536;  // length of the reserved counter array of the C-ABI (unused)
+// MFMAs per slice; dconv_kernels.h Split2h); packs are form-specific.
+static_assert(kMathF32 == 0 && kMathX6 == 2 && kMathH3P == 5, "msl_forms.f32_form values");
 
 struct FwdPlan {
   bool sk;
@@ -409,7 +403,7 @@ static size_t wgrad_piece_bytes(const WgradPlan& pl) { return (size_t)pl.nw * pl
 static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)pl.KS * 6 * pl.lda * 16 : 0; }
 
 // stream-K workspace: the published pieces, NW x 2 x BM*BN floats (summed by k_sk_reduce; no
-// counters, flags or other state survive a call).
+// flags or other state survive a call).
 // + (f16x3) the image's kNPart absmax partials at the end of the caller's workspace.
 constexpr size_t kPartBytes = kNPart * sizeof(float);
 // stream-K pieces, then (the BP form) the image operand's fp16 planes, then the partials at the end
@@ -487,8 +481,9 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
 template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int nimg, int dil0,
-                           int dil1, int* counters, void* ws, size_t ws_bytes, hipStream_t st,
+                           int dil1, const msl_forms* forms, void* ws, size_t ws_bytes, hipStream_t st,
                            int accum = 0, const float* img_part = nullptr, int img_npart = 0) {
+  if (forms_bad(forms)) return MSL_ERR_ARG;
   const int P = nimg * h * w;  // nimg images of h x w stacked along the pixel axis
   FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
   // The x6 form runs one K-step per stage, three stages deep (r01 tuning harness, layer3:
@@ -553,10 +548,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   a.taps = taps;
   a.slab = (long long)M * P;
   if (pl.sk) {
-    if (!counters) return MSL_ERR_ARG;
-    if ((long long)pl.tiles_m * pl.tiles_n > kMaxCounters) return MSL_ERR_SHAPE;
     SkArgs sk{};
-    sk.flags = counters;
     sk.part = (float*)ws;
     sk.tiles_m = pl.tiles_m;
     sk.tiles_n = pl.tiles_n;
@@ -568,7 +560,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
     // at least as many tiles as workers: whole rounds of tiles data-parallel, stream-K over the
     // rest (SkArgs); fewer: pure stream-K.  Every stream-K worker must own at least one iteration:
     // the piece count of a tile is the number of workgroups its iteration range touches.
-    sk.tdp = (g_sk_hybrid && tiles >= kSkNW) ? (int)(tiles / kSkNW * kSkNW) : 0;
+    sk.tdp = (forms_of(forms).sk_hybrid && tiles >= kSkNW) ? (int)(tiles / kSkNW * kSkNW) : 0;
     // Tile order (r04): m fastest when whole rounds of tiles run data-parallel (hybrid): one XCD's
     // workers then hold every m-block of a few pixel blocks, so each image block is fetched once and
     // re-read from that L2 (same box: 256 -> 1024 fwd 42.7 vs 49.8 us, 2048 -> 512 dgrad 127 vs 141,
@@ -712,10 +704,10 @@ static long long packed_elems(int nbranch, int taps, int cin, int cout, int for_
   return pack_tail_offset(packed_f32_elems(nbranch, taps, cin, cout, for_dgrad)) + kPackTail;
 }
 
-static std::atomic<int> g_pack_form{1};  // msl_conv_set_pack_form: 1 = k_pack_split, 0 = k_pack + k_split_pack
-
+// forms.pack_form: 1 = k_pack_split, 0 = k_pack + k_split_pack
 static int pack(const float* w, long long branch_stride, int nbranch, int taps, int cin, int cout,
-                int for_dgrad, float* packed, hipStream_t st) {
+                int for_dgrad, float* packed, const msl_forms* forms, hipStream_t st) {
+  if (forms_bad(forms)) return MSL_ERR_ARG;
   const int cimg = for_dgrad ? cout : cin;
   const int m = for_dgrad ? cin : cout;
   const long long total = packed_f32_elems(nbranch, taps, cin, cout, for_dgrad);
@@ -723,11 +715,11 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
   const int ncb = cdiv(cimg, kCB);
   __bf16* planes = reinterpret_cast<__bf16*>(packed + total);
   // f16x3: fp16 planes for every M (the <= 64-row 3x3 / ASPP tiles run f16x3 too since r03)
-  const bool h3 = g_f32_form == kMathH3P;
+  const bool h3 = forms_of(forms).f32_form == kMathH3P;
   float* tail = h3 ? packed + pack_tail_offset(total) : nullptr;
   // M <= 64 has no planes to split, and its 128-row padding is mostly zeros, which k_pack's
   // fully coalesced rows write faster (ASPP fwd 2048 -> 19: 5.2 vs 9.5 us)
-  if (!h3 && (g_pack_form == 0 || m <= 64)) {  // element-wise gather, then a separate split
+  if (!h3 && (forms_of(forms).pack_form == 0 || m <= 64)) {  // element-wise gather, then a separate split
     const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
     hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
                        ncb, lda, taps, total, packed);
@@ -916,16 +908,19 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
   return MSL_OK;
 }
 
+// the fp32 entry points: the kernel template of the call's f32 form
 template <typename... Args>
-static int fwd_f32(Args... args) {
-  const int form = g_f32_form.load(std::memory_order_relaxed);
+static int fwd_f32(const msl_forms* forms, Args... args) {
+  if (forms_bad(forms)) return MSL_ERR_ARG;
+  const int form = forms_of(forms).f32_form;
   if (form == kMathH3P) return launch_fwd_form<kMathH3P>(args...);
   return form == kMathX6 ? launch_fwd_form<kMathX6>(args...) : launch_fwd_form<kMathF32>(args...);
 }
 
 template <typename... Args>
-static int wgrad_f32(Args... args) {
-  const int form = g_f32_form.load(std::memory_order_relaxed);
+static int wgrad_f32(const msl_forms* forms, Args... args) {
+  if (forms_bad(forms)) return MSL_ERR_ARG;
+  const int form = forms_of(forms).f32_form;
   if (form == kMathH3P) return launch_wgrad<kMathH3P>(args...);
   return form == kMathX6 ? launch_wgrad<kMathX6>(args...) : launch_wgrad<kMathF32>(args...);
 }
@@ -938,27 +933,13 @@ extern "C" {
 
 int msl_abi_version(void) { return MSL_ABI_VERSION; }
 
-int msl_counter_elems(void) { return kMaxCounters; }
-
-int msl_conv_set_f32_form(int form) {
-  if (form != kMathF32 && form != kMathX6 && form != kMathH3P) return MSL_ERR_ARG;
-  g_f32_form = form;
+int msl_forms_default(msl_forms* out) {
+  if (!out) return MSL_ERR_ARG;
+  *out = kDefaultForms;
   return MSL_OK;
 }
 
-int msl_conv_f32_form(void) { return g_f32_form; }
-
-int msl_conv_set_sk_hybrid(int on) {
-  if (on != 0 && on != 1) return MSL_ERR_ARG;
-  g_sk_hybrid = on;
-  return MSL_OK;
-}
-
-int msl_conv_set_pack_form(int form) {
-  if (form != 0 && form != 1) return MSL_ERR_ARG;
-  g_pack_form = form;
-  return MSL_OK;
-}
+int msl_forms_check(const msl_forms* forms) { return forms_bad(forms) ? MSL_ERR_ARG : MSL_OK; }
 
 const char* msl_status_string(int status) {
   switch (status) {
@@ -976,9 +957,9 @@ long long msl_dconv_packed_elems(int nbranch, int cin, int cout, int for_dgrad) 
 }
 
 int msl_dconv_pack(const float* w, long long branch_stride, int nbranch, int cin, int cout,
-                   int for_dgrad, float* packed, msl_stream_t stream) {
+                   int for_dgrad, float* packed, const msl_forms* forms, msl_stream_t stream) {
   if (bad_dims(nbranch, cin, cout, 1, 1) || !w || !packed) return MSL_ERR_ARG;
-  return pack(w, branch_stride, nbranch, 9, cin, cout, for_dgrad, packed, as_stream(stream));
+  return pack(w, branch_stride, nbranch, 9, cin, cout, for_dgrad, packed, forms, as_stream(stream));
 }
 
 long long msl_conv_pack_blocks(int nbranch, int taps, int cin, int cout, int for_dgrad) {
@@ -990,12 +971,12 @@ long long msl_conv_pack_blocks(int nbranch, int taps, int cin, int cout, int for
 }
 
 int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, int njobs, int taps,
-                       long long total_blocks, msl_stream_t stream) {
+                       long long total_blocks, const msl_forms* forms, msl_stream_t stream) {
   if (!jobs || !block_start || njobs < 1 || total_blocks < 1 || total_blocks >= (1LL << 31) ||
-      (taps != 1 && taps != 9))
+      (taps != 1 && taps != 9) || forms_bad(forms))
     return MSL_ERR_ARG;
   hipStream_t st = as_stream(stream);
-  const int h3 = g_f32_form == kMathH3P;
+  const int h3 = forms_of(forms).f32_form == kMathH3P;
   if (h3) {  // the weights' absmax partials first (jobs with M > 64: the split packs)
     if (taps == 9)
       hipLaunchKernelGGL(k_absmax_jobs<9>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
@@ -1027,13 +1008,13 @@ size_t msl_dconv_fwd_workspace(int nbranch, int cin, int cout, int h, int w, int
 }
 
 int msl_dconv_fwd(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                   size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return fwd_f32(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1,
-                         counters, ws, ws_bytes, as_stream(stream));
+  return fwd_f32(forms, x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1,
+                         forms, ws, ws_bytes, as_stream(stream));
 }
 
 size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg) {
@@ -1043,13 +1024,13 @@ size_t msl_dconv_dgrad_workspace(int nbranch, int cin, int cout, int h, int w, i
 }
 
 int msl_dconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                    int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                     size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1,
-                         counters, ws, ws_bytes, as_stream(stream));
+  return fwd_f32(forms, dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1,
+                         forms, ws, ws_bytes, as_stream(stream));
 }
 
 size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w, int nimg) {
@@ -1059,12 +1040,12 @@ size_t msl_dconv_wgrad_workspace(int nbranch, int cin, int cout, int h, int w, i
 }
 
 int msl_dconv_wgrad(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, const msl_forms* forms, void* ws,
                     size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return wgrad_f32(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws,
+  return wgrad_f32(forms, x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws,
                       ws_bytes, as_stream(stream));
 }
 
@@ -1074,10 +1055,10 @@ long long msl_pconv_packed_elems(int cin, int cout, int for_dgrad) {
   return packed_elems(1, 1, cin, cout, for_dgrad);
 }
 
-int msl_pconv_pack(const float* w, int cin, int cout, int for_dgrad, float* packed,
+int msl_pconv_pack(const float* w, int cin, int cout, int for_dgrad, float* packed, const msl_forms* forms,
                    msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, 1) || !w || !packed) return MSL_ERR_ARG;
-  return pack(w, 0, 1, 1, cin, cout, for_dgrad, packed, as_stream(stream));
+  return pack(w, 0, 1, 1, cin, cout, for_dgrad, packed, forms, as_stream(stream));
 }
 
 size_t msl_pconv_fwd_workspace(int cin, int cout, int p) {
@@ -1086,9 +1067,9 @@ size_t msl_pconv_fwd_workspace(int cin, int cout, int p) {
 }
 
 int msl_pconv_fwd(const float* x, const float* packed, float* y, int cin, int cout, int p,
-                  int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+                  const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return fwd_f32(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws,
+  return fwd_f32(forms, x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, forms, ws,
                          ws_bytes, as_stream(stream));
 }
 
@@ -1098,19 +1079,19 @@ size_t msl_pconv_dgrad_workspace(int cin, int cout, int p) {
 }
 
 int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                    int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+                    const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters,
+  return fwd_f32(forms, dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms,
                          ws, ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                        int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+                        int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
   if (!accumulate)
-    return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
+    return fwd_f32(forms, dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms, ws, ws_bytes,
                    as_stream(stream));
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
+  return fwd_f32(forms, dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms, ws, ws_bytes,
                  as_stream(stream), 1);
 }
 
@@ -1130,63 +1111,63 @@ int msl_absmax_partials(const float* x, int rows, int row_len, float* part, msl_
 }
 
 int msl_dconv_fwd_sc(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                     int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                     int cin, int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                      size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart) {
   if (bad_parts(x_part, x_npart)) return MSL_ERR_ARG;
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return fwd_f32(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1, counters, ws, ws_bytes,
+  return fwd_f32(forms, x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1, forms, ws, ws_bytes,
                  as_stream(stream), 0, x_part, x_npart);
 }
 
 int msl_dconv_dgrad_sc(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                       int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                       int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                        size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart) {
   if (bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1, counters, ws,
+  return fwd_f32(forms, dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1, forms, ws,
                  ws_bytes, as_stream(stream), 0, dy_part, dy_npart);
 }
 
 int msl_dconv_wgrad_sc(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                       int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
+                       int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, const msl_forms* forms, void* ws,
                        size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
                        const float* dy_part, int dy_npart) {
   if (bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return wgrad_f32(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws, ws_bytes,
+  return wgrad_f32(forms, x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws, ws_bytes,
                    as_stream(stream), x_part, x_npart, dy_part, dy_npart);
 }
 
 int msl_pconv_fwd_sc(const float* x, const float* packed, float* y, int cin, int cout, int p,
-                     int* counters, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                     const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
                      int x_npart) {
   if (bad_parts(x_part, x_npart)) return MSL_ERR_ARG;
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return fwd_f32(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
+  return fwd_f32(forms, x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, forms, ws, ws_bytes,
                  as_stream(stream), 0, x_part, x_npart);
 }
 
 int msl_pconv_dgrad_acc_sc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                           int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                           int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream,
                            const float* dy_part, int dy_npart) {
   if (bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return fwd_f32(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
+  return fwd_f32(forms, dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms, ws, ws_bytes,
                  as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart);
 }
 
 int msl_pconv_wgrad_sc(const float* x, const float* dy, float* dw, int cin, int cout, int p,
-                       int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
+                       int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
                        int x_npart, const float* dy_part, int dy_npart) {
   if (bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
-  return wgrad_f32(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes, as_stream(stream),
+  return wgrad_f32(forms, x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes, as_stream(stream),
                    x_part, x_npart, dy_part, dy_npart);
 }
 
@@ -1196,9 +1177,9 @@ size_t msl_pconv_wgrad_workspace(int cin, int cout, int p) {
 }
 
 int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cout, int p,
-                    int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
+                    int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
-  return wgrad_f32(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes,
+  return wgrad_f32(forms, x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes,
                       as_stream(stream));
 }
 
@@ -1207,52 +1188,53 @@ int msl_pconv_wgrad(const float* x, const float* dy, float* dw, int cin, int cou
 // Same operands, workspaces and results layout; products in bf16 (RNE from the fp32 operands),
 // sums in fp32 (BASELINE config 5's fp16/bf16 MFMA path).
 int msl_dconv_fwd_bf16(const float* x, const float* packed, const float* bias, float* y, int nbranch,
-                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                  int cin, int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                   size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
   return launch_fwd_form<kMathBf16>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1,
-                         counters, ws, ws_bytes, as_stream(stream));
+                         forms, ws, ws_bytes, as_stream(stream));
 }
 
 int msl_dconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin,
-                    int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws,
                     size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad || !dx || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
   return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1,
-                         counters, ws, ws_bytes, as_stream(stream));
+                         forms, ws, ws_bytes, as_stream(stream));
 }
 
 int msl_dconv_wgrad_bf16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin,
-                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws,
+                    int cout, int h, int w, int nimg, int dil0, int dil1, int accumulate, const msl_forms* forms, void* ws,
                     size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !dy || !dw || dil0 < 1 ||
       (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
+  if (forms_bad(forms)) return MSL_ERR_ARG;
   return launch_wgrad<kMathBf16>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws,
                       ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_fwd_bf16(const float* x, const float* packed, float* y, int cin, int cout, int p,
-                  int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+                  const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !x || !packed || !y) return MSL_ERR_ARG;
-  return launch_fwd_form<kMathBf16>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws,
+  return launch_fwd_form<kMathBf16>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, forms, ws,
                          ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_dgrad_bf16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                    int* counters, void* ws, size_t ws_bytes, msl_stream_t stream) {
+                    const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream) {
   if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx) return MSL_ERR_ARG;
-  return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters,
+  return launch_fwd_form<kMathBf16>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms,
                          ws, ws_bytes, as_stream(stream));
 }
 
 int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, int cout, int p,
-                    int accumulate, void* ws, size_t ws_bytes, msl_stream_t stream) {
-  if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw) return MSL_ERR_ARG;
+                    int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream) {
+  if (bad_dims(1, cin, cout, 1, p) || !x || !dy || !dw || forms_bad(forms)) return MSL_ERR_ARG;
   return launch_wgrad<kMathBf16>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes,
                       as_stream(stream));
 }
@@ -1263,59 +1245,59 @@ int msl_pconv_wgrad_bf16(const float* x, const float* dy, float* dw, int cin, in
 // so packs must be made in the f16x3 fp32 form, the default), one v_mfma_f32_32x32x16_f16 per
 // 16-deep slice, fp32 sums, the result unscaled exactly.  The 64- / 32-row tiles (M <= 64) run
 // exact f32 MFMA.  Partials as in the _sc entry points ((pointer, count), NULL = computed).
-static bool f16_ready() { return g_f32_form == kMathH3P; }
+static bool f16_ready(const msl_forms* forms) { return !forms_bad(forms) && forms_of(forms).f32_form == kMathH3P; }
 
 int msl_dconv_fwd_f16(const float* x, const float* packed, const float* bias, float* y, int nbranch, int cin,
-                      int cout, int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                      int cout, int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws, size_t ws_bytes,
                       msl_stream_t stream, const float* x_part, int x_npart) {
-  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y ||
+  if (!f16_ready(forms) || bad_parts(x_part, x_npart) || bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !packed || !y ||
       dil0 < 1 || (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1, counters,
+  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, bias, nbranch, y, nbranch, 9, h, w, nimg, dil0, dil1, forms,
                                    ws, ws_bytes, as_stream(stream), 0, x_part, x_npart);
 }
 
 int msl_dconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int nbranch, int cin, int cout,
-                        int h, int w, int nimg, int dil0, int dil1, int* counters, void* ws, size_t ws_bytes,
+                        int h, int w, int nimg, int dil0, int dil1, const msl_forms* forms, void* ws, size_t ws_bytes,
                         msl_stream_t stream, const float* dy_part, int dy_npart) {
-  if (!f16_ready() || bad_parts(dy_part, dy_npart) || bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad ||
+  if (!f16_ready(forms) || bad_parts(dy_part, dy_npart) || bad_dims(nbranch, cin, cout, h, w, nimg) || !dy || !packed_dgrad ||
       !dx || dil0 < 1 || (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
   return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, nbranch, 9, h, w, nimg, dil0, dil1,
-                                   counters, ws, ws_bytes, as_stream(stream), 0, dy_part, dy_npart);
+                                   forms, ws, ws_bytes, as_stream(stream), 0, dy_part, dy_npart);
 }
 
 int msl_dconv_wgrad_f16(const float* x, const float* dy, float* dw, float* dbias, int nbranch, int cin, int cout,
-                        int h, int w, int nimg, int dil0, int dil1, int accumulate, void* ws, size_t ws_bytes,
+                        int h, int w, int nimg, int dil0, int dil1, int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes,
                         msl_stream_t stream, const float* x_part, int x_npart, const float* dy_part, int dy_npart) {
-  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart) ||
+  if (!f16_ready(forms) || bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart) ||
       bad_dims(nbranch, cin, cout, h, w, nimg) || !x || !dy || !dw || dil0 < 1 || (nbranch == 2 && dil1 < 1))
     return MSL_ERR_ARG;
   return launch_wgrad<kMathH1P>(x, dy, dw, dbias, nbranch, 9, cin, cout, h, w, nimg, dil0, dil1, accumulate, ws, ws_bytes,
                                 as_stream(stream), x_part, x_npart, dy_part, dy_npart);
 }
 
-int msl_pconv_fwd_f16(const float* x, const float* packed, float* y, int cin, int cout, int p, int* counters,
+int msl_pconv_fwd_f16(const float* x, const float* packed, float* y, int cin, int cout, int p, const msl_forms* forms,
                       void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart) {
-  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_dims(1, cin, cout, 1, p) || !x || !packed || !y)
+  if (!f16_ready(forms) || bad_parts(x_part, x_npart) || bad_dims(1, cin, cout, 1, p) || !x || !packed || !y)
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, counters, ws, ws_bytes,
+  return launch_fwd_form<kMathH1P>(x, cin, packed, cout, nullptr, 0, y, 1, 1, 1, p, 1, 0, 0, forms, ws, ws_bytes,
                                    as_stream(stream), 0, x_part, x_npart);
 }
 
 int msl_pconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
-                        int accumulate, int* counters, void* ws, size_t ws_bytes, msl_stream_t stream,
+                        int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream,
                         const float* dy_part, int dy_npart) {
-  if (!f16_ready() || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx)
+  if (!f16_ready(forms) || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx)
     return MSL_ERR_ARG;
-  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, counters, ws,
+  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms, ws,
                                    ws_bytes, as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart);
 }
 
-int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int cout, int p, int accumulate,
+int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int cout, int p, int accumulate, const msl_forms* forms,
                         void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part, int x_npart,
                         const float* dy_part, int dy_npart) {
-  if (!f16_ready() || bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) ||
+  if (!f16_ready(forms) || bad_parts(x_part, x_npart) || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) ||
       !x || !dy || !dw)
     return MSL_ERR_ARG;
   return launch_wgrad<kMathH1P>(x, dy, dw, nullptr, 1, 1, cin, cout, 1, p, 1, 0, 0, accumulate, ws, ws_bytes,

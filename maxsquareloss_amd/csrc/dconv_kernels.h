@@ -25,7 +25,7 @@ struct FwdArgs {
   int taps;           // 9 (3x3) or 1 (pointwise: dil0 = 0, so the single tap has no shift)
   long long slab;
   const void* Ax6;    // kMathX6P/PP: A split into bf16 planes [ks][plane][k half][lda][8] (k_split_pack)
-  const void* Bx6;    // kMathX6PP: B split into bf16 planes [cb][plane][k half][P][8] (k_split_act)
+  const void* Bx6;    // the BP form: the image operand's fp16 planes (k_split_img)
   int accum;          // stream-K forms: C = C_old + result (the fused residual-gradient sum)
   // kMathH3P: Ax6 holds A * sA as two fp16 planes [ks][plane][k half][lda][8]; ascale = {sA,
   // 1/sA} (written by the pack); bpart = the kNPart absmax partials of B (k_absmax)
@@ -148,8 +148,7 @@ struct Split3 {
 // matrix-core form of a conv kernel (template argument MT)
 // kMathX6P: the x6 form with the A operand (packed weights) split once per call by
 // k_split_pack instead of per read (fwd form only)
-// by k_split_pack instead of per read; kMathX6PP: both operands pre-split (k_split_act for B)
-constexpr int kMathF32 = 0, kMathBf16 = 1, kMathX6 = 2, kMathX6P = 3, kMathX6PP = 4;
+constexpr int kMathF32 = 0, kMathBf16 = 1, kMathX6 = 2, kMathX6P = 3;
 
 __device__ __forceinline__ void split3_set(Split3& s, int j, float v) {
   const __bf16 h = (__bf16)v;
@@ -334,63 +333,6 @@ __global__ void __launch_bounds__(256) k_split_pack(const float* __restrict__ A,
     out[row] = sp.hi;
     out[row + 2LL * lda] = sp.mid;
     out[row + 4LL * lda] = sp.lo;
-  }
-}
-
-// The fwd-form B operand (image [cimg][P] fp32) split into bf16 planes
-// planes[((cb*3 + q)*2 + h)*P + p][j] = term q of image[cb*16 + 8h + j][p] (0 past cimg): a tap's
-// B tile is then one 16-B DMA piece per (pixel, plane, half) - per-lane, so shifted pixels that
-// leave the image still get an out-of-range offset - and one ds_read_b128 per fragment and plane.
-__global__ void __launch_bounds__(256) k_split_act(const float* __restrict__ x, int cimg, int ncb, int P,
-                                                   __bf16* __restrict__ planes) {
-  const long long n = (long long)ncb * 2 * P;
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const int p = (int)(e % P);
-    const long long kh = e / P;
-    const int h = (int)(kh & 1), cb = (int)(kh >> 1);
-    Split3 sp;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = cb * kCB + 8 * h + j;
-      split3_set(sp, j, c < cimg ? x[(long long)c * P + p] : 0.f);
-    }
-    bf16x8* out = reinterpret_cast<bf16x8*>(planes);
-    const long long row = ((long long)(cb * 3) * 2 + h) * P + p;  // plane 0
-    out[row] = sp.hi;
-    out[row + 2LL * P] = sp.mid;
-    out[row + 4LL * P] = sp.lo;
-  }
-}
-
-// x6 stage with both operands read as pre-split bf16 planes: no split work in the loop.
-template <int G, int TM, int TN, int BM, int BN, typename F>
-__device__ __forceinline__ void mfma_stage_x6pp(const float* As, const float* Bs,
-                                                int wm, int wn, int lane, f32x16 (&acc)[TM][TN], F&& mid) {
-  const int l32 = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int kk = 0; kk < G; ++kk) {
-    const bf16x8* Ab = reinterpret_cast<const bf16x8*>(As + kk * 24 * BM);
-    const bf16x8* Bb = reinterpret_cast<const bf16x8*>(Bs + kk * 24 * BN);
-    Split3 av[TM], bv[TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = wm + i * 32 + l32;
-      av[i].hi = Ab[h * BM + m];
-      av[i].mid = Ab[(2 + h) * BM + m];
-      av[i].lo = Ab[(4 + h) * BM + m];
-    }
-#pragma unroll
-    for (int t = 0; t < TN; ++t) {
-      const int n = wn + t * 32 + l32;
-      bv[t].hi = Bb[h * BN + n];
-      bv[t].mid = Bb[(2 + h) * BN + n];
-      bv[t].lo = Bb[(4 + h) * BN + n];
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int t = 0; t < TN; ++t) acc[i][t] = mfma_x6(av[i], bv[t], acc[i][t]);
-    if (kk == 0) mid();
   }
 }
 
@@ -821,131 +763,6 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int STAGES, int WM, int WN>
-__global__ void __launch_bounds__(256) k_igemm_fwd_dma(FwdArgs a) {
-  constexpr int BK = kCB;
-  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
-  static_assert(BN % 64 == 0 && BM % 64 == 0, "tiles");
-  constexpr int A_STAGE = BK * BM, STAGE = A_STAGE + BK * BN;
-  // per wave and stage: A rows (16 B per lane: 64 lanes = 1024 floats = 1024/BM rows) + B rows
-  constexpr int A_ROWS_PER_INST = 256 / BM;                // rows of BM floats per dwordx4 instruction
-  constexpr int A_INST = BK / A_ROWS_PER_INST;             // per workgroup
-  constexpr int A_INST_W = (A_INST + 3) / 4;               // per wave
-  constexpr int B_INST = BK * (BN / 64);                   // per workgroup (one row-half each)
-  constexpr int B_INST_W = B_INST / 4;
-  constexpr int INST_W = A_INST_W + B_INST_W;
-  static_assert(A_INST % 4 == 0, "A instructions split evenly over waves");
-  __shared__ __attribute__((aligned(16))) float smem[STAGES * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = (wid / WN) * (TM * 32), wn = (wid % WN) * (TN * 32);
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int split = blockIdx.z;
-  const int s_begin = split * a.kps;
-  const int s_end = min(a.ksteps, s_begin + a.kps);
-  const int nst = s_end - s_begin;
-
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.A, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * BK * a.lda * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.B, (short)0, (int)min(0x7fffffffLL, (long long)a.cimg * a.P * 4), 0x00020000);
-
-  // this lane's pixels: one per 64-wide half of the BN tile
-  constexpr int NH = BN / 64;
-  int py[NH], px[NH];
-  bool pin[NH];
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    const int p = n0 + h * 64 + lane;
-    pin[h] = p < a.P;
-    const int pq = p / a.W;
-    px[h] = p - pq * a.W;
-    py[h] = pq % a.H;
-  }
-  const int per_b = a.ncb * a.taps;
-  constexpr unsigned OOB = 0x80000000u;
-
-  auto issue = [&](int s, int slot) {
-    float* As = smem + slot * STAGE;
-    float* Bs = As + A_STAGE;
-    const int b = s / per_b;
-    const int rem = s - b * per_b;
-    const int t = rem / a.ncb;
-    const int cb = rem - t * a.ncb;
-    const int d = b ? a.dil1 : a.dil0;
-    const int dh = (t / 3 - 1) * d, dw = (t % 3 - 1) * d;
-    // A: wave wid loads instructions wid*A_INST_W .. ; each covers A_ROWS_PER_INST rows
-#pragma unroll
-    for (int i = 0; i < A_INST_W; ++i) {
-      const int inst = wid * A_INST_W + i;
-      const int row = inst * A_ROWS_PER_INST + lane / (BM / 4);
-      const int c4 = lane % (BM / 4);
-      const unsigned off = (unsigned)((((long long)s * BK + row) * a.lda + m0 + c4 * 4) * 4);
-      dma_b128(ra, As + inst * 256, off);  // 64 lanes x 16 B = 256 floats per instruction
-    }
-    // B: instruction j of this wave -> row r = (wid*B_INST_W + j) / NH, half h
-    const int cb16 = cb * kCB;
-#pragma unroll
-    for (int j = 0; j < B_INST_W; ++j) {
-      const int inst = wid * B_INST_W + j;
-      const int r = inst / NH, h = inst % NH;
-      const int ci = cb16 + r;
-      const bool v = pin[h] && ci < a.cimg && (unsigned)(py[h] + dh) < (unsigned)a.H &&
-                     (unsigned)(px[h] + dw) < (unsigned)a.W;
-      const long long e = (long long)ci * a.P + (n0 + h * 64 + lane) + dh * a.W + dw;
-      dma_b32(rb, Bs + r * BN + h * 64, v ? (unsigned)(e * 4) : OOB);
-    }
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  // prologue: STAGES-1 stages in flight
-#pragma unroll
-  for (int k = 0; k < STAGES - 1; ++k)
-    if (k < nst) issue(s_begin + k, k);
-  for (int i = 0; i < nst; ++i) {
-    // stage i must have landed: the younger in-flight stages may stay outstanding
-    const int younger = min(STAGES - 2, nst - 1 - i);
-    if (younger >= 2) wait_vmcnt<2 * INST_W>();
-    else if (younger == 1) wait_vmcnt<INST_W>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    if (i + STAGES - 1 < nst) issue(s_begin + i + STAGES - 1, (i + STAGES - 1) % STAGES);
-    const float* As = smem + (i % STAGES) * STAGE;
-    mfma_stage<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-
-  float* C = a.C + (long long)split * a.slab;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int n = n0 + wn + j * 32 + (lane & 31);
-        if (m < a.M && n < a.P) {
-          float v = acc[i][j][r];
-          if (a.bias) {
-            float bsum = a.bias[m];
-            for (int b = 1; b < a.nbias; ++b) bsum += a.bias[b * a.M + m];
-            v += bsum;
-          }
-          C[(long long)m * a.P + n] = v;
-        }
-      }
-}
-
-
 // The forward-form image operand pre-split (variant bit 7, r03): planes[((cb*NP + q)*2 + h)*P + p] =
 // 16 B = plane q of the 8 channels cb*16 + 8h .. +7 of pixel p, scaled by the tensor's power of two
 // (0 past cimg).  NP = 2 (f16x3: hi, lo) or 1 (fp16: hi).  One thread per (cb, h, p): eight loads
@@ -993,7 +810,6 @@ __global__ void __launch_bounds__(256) k_split_img(const float* __restrict__ x, 
 // stream-K and leaves 272 this way.  tdp = 0 is pure stream-K.
 struct SkArgs {
   float* part;     // [NW][2][BM][BN] pieces of split tiles (row-major)
-  int* flags;      // unused (kept for the C-ABI's caller-owned counter array)
   int tiles_m, tiles_n, KS, NW;
   int T;           // stream-K iterations: (tiles - tdp) * KS  (T * NW < 2^31, checked by the planner)
   int tdp;         // leading tiles that run data-parallel (a multiple of the grid size)
@@ -1056,15 +872,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   static_assert(BN % 64 == 0 && BM % 32 == 0, "tiles");
   constexpr bool H1 = MT == kMathH1P;                                 // fp16: the hi plane only
   constexpr bool H3 = MT == kMathH3P || H1;                           // f16x3: two fp16 planes
-  constexpr bool APRE = MT == kMathX6P || MT == kMathX6PP || H3;  // A from pre-split planes
-  constexpr bool BPRE = MT == kMathX6PP;                            // B from pre-split bf16 planes
+  constexpr bool APRE = MT == kMathX6P || H3;  // A from pre-split planes
   constexpr int NQ = H3 ? 4 : 6;  // (plane, k half) blocks of one pre-split K-step in the pack
   constexpr int NQL = H1 ? 2 : NQ;  // of them staged (fp16 math: plane 0's two halves)
   static_assert(!APRE || BM % 64 == 0, "pre-split A: 64-row DMA pieces");
-  static_assert(!BPRE || (!PW && BN % 64 == 0), "pre-split B: 64-pixel DMA pieces");
-  static_assert(!BD || (H3 && G == 1 && WM == 1 && WN == 4 && TN == 1 && STAGES == 4 && !BPRE), "BD form");
+  static_assert(!BD || (H3 && G == 1 && WM == 1 && WN == 4 && TN == 1 && STAGES == 4), "BD form");
   constexpr int A_STAGE = APRE ? G * 4 * NQL * BM : BK * BM;
-  constexpr int STAGE = A_STAGE + (BD ? 0 : BPRE ? G * 24 * BN : BK * BN);
+  constexpr int STAGE = A_STAGE + (BD ? 0 : BK * BN);
   constexpr int A_ROWS_PER_INST = 256 / BM;
   constexpr int A_INST = APRE ? G * NQL * (BM / 64) : BK / A_ROWS_PER_INST;
   // fp16 math on 64-row tiles (r04): a K-step's A is one plane's two 1-KB pieces; each wave issues
@@ -1072,7 +886,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr bool AHALF = APRE && A_INST == 2;
   constexpr int A_INST_W = AHALF ? 1 : A_INST / 4;
   constexpr int NH = BN / 64;
-  constexpr int BG_INST_W = BPRE ? 6 * NH / 4 : PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B DMAs per wave per K-step
+  constexpr int BG_INST_W = PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B DMAs per wave per K-step
   static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
   static_assert(!BP || BD, "BP: the BD form with a pre-split image");
   constexpr int INST_W = A_INST_W + G * (BP ? (H1 ? 1 : 2) : BD ? 8 : BG_INST_W);
@@ -1110,7 +924,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       (void*)a.Ax6, (short)0, (int)min(0x7fffffffLL, (long long)a.ksteps * NQ * a.lda * 16), 0x00020000);
   const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.Bx6, (short)0,
-      (int)min(0x7fffffffLL, (long long)a.ncb * (BP ? (H1 ? 2 : 4) : 6) * a.P * 16), 0x00020000);
+      (int)min(0x7fffffffLL, (long long)a.ncb * (H1 ? 2 : 4) * a.P * 16), 0x00020000);
   constexpr unsigned OOB = 0x80000000u;
   const unsigned chan_bytes = (unsigned)a.P * 4u;
   // f16x3: B's scale from its absmax partials, A's from the pack; the result is unscaled by both
@@ -1208,7 +1022,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
           const bool v = pin[h] && (unsigned)(py[h] + dh) < (unsigned)a.H && (unsigned)(px[h] + dw) < (unsigned)a.W;
-          vrow[h] = v ? (unsigned)((n0 + h * 64 + lane + shift) * (BPRE ? 16 : 4)) : OOB;
+          vrow[h] = v ? (unsigned)((n0 + h * 64 + lane + shift) * 4) : OOB;
         }
       }
     };
@@ -1276,15 +1090,6 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
               asm volatile("v_mov_b32 %0, 0" : "=v"(bq[j]));
             else
               bq[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, vbdh, (int)(sb + j * chan_bytes), 0));
-          }
-        } else if constexpr (BPRE) {
-          // piece (plane*2 + k half, 64-pixel half): lane = pixel, 16 B = 8 channels of a plane
-#pragma unroll
-          for (int j = 0; j < BG_INST_W; ++j) {
-            const int inst = wid * BG_INST_W + j;
-            const int qh = inst / NH, h = inst % NH;  // wave-uniform
-            const unsigned rowb = (unsigned)((c_cb * 6 + qh) * a.P) * 16u;
-            dma_b128(rbx, Bs + g * 24 * BN + (qh * BN + h * 64) * 4, vrow[h] + rowb);
           }
         } else if constexpr (PW) {
           // lanes 0-31 -> row 2*inst, lanes 32-63 -> row 2*inst+1; 4 pixels per lane.  A chunk
@@ -1405,8 +1210,6 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         mfma_stage_x6<BK, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (MT == kMathX6P)
         mfma_stage_x6p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
-      else if constexpr (MT == kMathX6PP)
-        mfma_stage_x6pp<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid);
       else if constexpr (H1)
         mfma_stage_h1p<G, TM, TN, BM, BN>(As, As + A_STAGE, wm, wn, lane, acc, mid, sB);
       else if constexpr (H3)

@@ -5,7 +5,7 @@
 #include <algorithm>
 #include "../../include/msl_hip.h"
 
-#define MSL_ABI_VERSION 2
+#define MSL_ABI_VERSION 3
 
 #define MSL_CHECK_LAUNCH()                         \
   do {                                             \
@@ -37,5 +37,14 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // absmax[r] = max |t[r][0..p)| for r < c (bn.hip; stream-ordered memset + one launch, integer
 // atomicMax on the float bits: exact and order-independent).  The f16x3 convs' per-row partials.
 int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st);
+
+// The kernel forms of a call (msl_forms, include/msl_hip.h): NULL = the defaults (f16x3, the hybrid
+// stream-K schedule, one-launch packs, fused BN)
+constexpr msl_forms kDefaultForms = {5, 1, 1, 1};
+static inline const msl_forms& forms_of(const msl_forms* f) { return f ? *f : kDefaultForms; }
+static inline bool forms_bad(const msl_forms* f) {
+  return f && ((f->f32_form != 0 && f->f32_form != 2 && f->f32_form != 5) || (unsigned)f->sk_hybrid > 1u ||
+               (unsigned)f->pack_form > 1u || (unsigned)f->bn_fused > 1u);
+}
 
 }  // namespace msl

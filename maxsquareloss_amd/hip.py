@@ -22,49 +22,46 @@ SIGNATURES = {
     "msl_abi_version": (c_int, []),
     "msl_status_string": (ctypes.c_char_p, [c_int]),
     "msl_dconv_packed_elems": (c_ll, [c_int, c_int, c_int, c_int]),
-    "msl_dconv_pack": (c_int, [c_p, c_ll, c_int, c_int, c_int, c_int, c_p, c_p]),
+    "msl_forms_default": (c_int, [c_p]),
+    "msl_forms_check": (c_int, [c_p]),
+    "msl_dconv_pack": (c_int, [c_p, c_ll, c_int, c_int, c_int, c_int, c_p, c_p, c_p]),
     "msl_conv_pack_blocks": (c_ll, [c_int] * 5),
-    "msl_conv_pack_many": (c_int, [c_p, c_p, c_int, c_int, c_ll, c_p]),
+    "msl_conv_pack_many": (c_int, [c_p, c_p, c_int, c_int, c_ll, c_p, c_p]),
     "msl_dconv_fwd_workspace": (c_sz, [c_int] * 6),
-    "msl_counter_elems": (c_int, []),
-    "msl_conv_set_f32_form": (c_int, [c_int]),
-    "msl_conv_f32_form": (c_int, []),
-    "msl_conv_set_sk_hybrid": (c_int, [c_int]),
-    "msl_conv_set_pack_form": (c_int, [c_int]),
     "msl_dconv_fwd": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_dgrad_workspace": (c_sz, [c_int] * 6),
     "msl_dconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_wgrad_workspace": (c_sz, [c_int] * 6),
-    "msl_dconv_wgrad": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_sz, c_p]),
+    "msl_dconv_wgrad": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_packed_elems": (c_ll, [c_int] * 3),
-    "msl_pconv_pack": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p]),
+    "msl_pconv_pack": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
     "msl_pconv_fwd_workspace": (c_sz, [c_int] * 3),
     "msl_pconv_fwd": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_dgrad_workspace": (c_sz, [c_int] * 3),
     "msl_pconv_dgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_dgrad_acc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_wgrad_workspace": (c_sz, [c_int] * 3),
-    "msl_pconv_wgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
+    "msl_pconv_wgrad": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p]),
     "msl_absmax_partials": (c_int, [c_p, c_int, c_int, c_p, c_p]),
     "msl_dconv_fwd_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_dconv_dgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
-    "msl_dconv_wgrad_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_dconv_wgrad_sc": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
     "msl_pconv_fwd_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_dgrad_acc_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
-    "msl_pconv_wgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_pconv_wgrad_sc": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
     "msl_dconv_fwd_f16": (c_int, [c_p] * 4 + [c_int] * 8 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_dconv_dgrad_f16": (c_int, [c_p] * 3 + [c_int] * 8 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
-    "msl_dconv_wgrad_f16": (c_int, [c_p] * 4 + [c_int] * 9 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_dconv_wgrad_f16": (c_int, [c_p] * 4 + [c_int] * 9 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
     "msl_pconv_fwd_f16": (c_int, [c_p] * 3 + [c_int] * 3 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
     "msl_pconv_dgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int]),
-    "msl_pconv_wgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
+    "msl_pconv_wgrad_f16": (c_int, [c_p] * 3 + [c_int] * 4 + [c_p, c_p, c_sz, c_p, c_p, c_int, c_p, c_int]),
     "msl_conv_wgrad_split": (c_int, [c_int] * 7),
     "msl_dconv_fwd_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
     "msl_dconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 8 + [c_p, c_p, c_sz, c_p]),
-    "msl_dconv_wgrad_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_sz, c_p]),
+    "msl_dconv_wgrad_bf16": (c_int, [c_p, c_p, c_p, c_p] + [c_int] * 9 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_fwd_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
     "msl_pconv_dgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 3 + [c_p, c_p, c_sz, c_p]),
-    "msl_pconv_wgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_sz, c_p]),
+    "msl_pconv_wgrad_bf16": (c_int, [c_p, c_p, c_p] + [c_int] * 4 + [c_p, c_p, c_sz, c_p]),
     "msl_upsample_fwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p]),
     "msl_upsample_bwd_workspace": (c_sz, [c_int] * 5),
     "msl_upsample_bwd": (c_int, [c_p, c_p] + [c_int] * 5 + [c_p, c_sz, c_p]),
@@ -84,15 +81,13 @@ SIGNATURES = {
     "msl_iw_maxsquare_prob_fwd": (c_int, [c_p, c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "msl_iw_maxsquare_prob_bwd": (c_int, [c_p, c_int, c_int, c_p, c_p, c_p, c_p]),
     "msl_confusion_accumulate": (c_int, [c_p, c_p, c_int, ctypes.c_longlong, c_p, c_p, c_p]),
-    "msl_bn_set_fused": (c_int, [c_int]),
-    "msl_bn_fused": (c_int, []),
-    "msl_bn_uses_fused": (c_int, [c_int, c_int, c_int]),
+    "msl_bn_uses_fused": (c_int, [c_int, c_int, c_int, c_p]),
     "msl_bn_workspace": (c_sz, [c_int] * 3),
-    "msl_bn_fwd": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_sz, c_p]),
-    "msl_bn_bwd": (c_int, [c_p] * 10 + [c_int] * 6 + [c_p, c_sz, c_p]),
-    "msl_bn_fwd_am": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_sz, c_p, c_p]),
-    "msl_bn_bwd_am": (c_int, [c_p] * 10 + [c_int] * 6 + [c_p, c_sz, c_p, c_p]),
-    "msl_bn_bwd_am_beta": (c_int, [c_p] * 11 + [c_int] * 6 + [c_p, c_sz, c_p, c_p]),
+    "msl_bn_fwd": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_p, c_sz, c_p]),
+    "msl_bn_bwd": (c_int, [c_p] * 10 + [c_int] * 6 + [c_p, c_p, c_sz, c_p]),
+    "msl_bn_fwd_am": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_p, c_sz, c_p, c_p]),
+    "msl_bn_bwd_am": (c_int, [c_p] * 10 + [c_int] * 6 + [c_p, c_p, c_sz, c_p, c_p]),
+    "msl_bn_bwd_am_beta": (c_int, [c_p] * 11 + [c_int] * 6 + [c_p, c_p, c_sz, c_p, c_p]),
     "msl_image_transform": (c_int, [c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p, c_p]),
     "msl_label_transform": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
     "msl_im2col": (c_int, [c_p] + [c_int] * 11 + [c_p, c_p]),
@@ -111,7 +106,7 @@ SIGNATURES = {
     "msl_sgd_step_lr_dev": (c_int, [c_p, c_p, c_p, c_ll, c_p, c_f, c_f, c_f, c_p]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 
 
@@ -161,21 +156,28 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
-_COUNTERS = {}
+class Forms(ctypes.Structure):
+    """msl_forms (include/msl_hip.h): the kernel forms every conv / pack / BN call takes (ABI 3)."""
+    _fields_ = [("f32_form", c_int), ("sk_hybrid", c_int), ("pack_form", c_int), ("bn_fused", c_int)]
 
 
-def counters(device):
-    """The zero-filled counter array the conv forward / data-gradient entry points take
-    (msl_counter_elems() ints, one per device and stream).  Reserved by the C-ABI: the current
-    kernels never touch it, so no call depends on what an earlier (or aborted) call left."""
-    dev = torch.device(device)
-    idx = dev.index if dev.index is not None else torch._C._cuda_getDevice()
-    key = (idx, torch._C._cuda_getCurrentRawStream(idx))
-    buf = _COUNTERS.get(key)
-    if buf is None:
-        buf = torch.zeros(load().msl_counter_elems(), dtype=torch.int32, device=device)
-        _COUNTERS[key] = buf
-    return buf
+FORMS = Forms(5, 1, 1, 1)  # the forms this process passes: the library's defaults until set_form
+
+
+def forms():
+    """The const msl_forms* of every conv / pack / BN call: FORMS, read by the library on the host when
+    the call launches (a captured graph keeps the forms of its capture)."""
+    return ctypes.addressof(FORMS)
+
+
+def set_form(name, value):
+    """Set one field of FORMS (checked by msl_forms_check); returns the previous value."""
+    trial = Forms(*(getattr(FORMS, f) for f, _ in Forms._fields_))
+    setattr(trial, name, int(value))
+    check(load(require_gpu=False).msl_forms_check(ctypes.addressof(trial)), f"msl_forms {name}={value}")
+    prev = getattr(FORMS, name)
+    setattr(FORMS, name, int(value))
+    return prev
 
 
 def workspace(nbytes, device):

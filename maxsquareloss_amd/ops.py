@@ -33,46 +33,37 @@ def set_conv_math(math):
     CONV_MATH = math
 
 
-# Matrix-core form of the fp32 conv math, held process-wide by the library
-# (msl_conv_set_f32_form): "mfma_f32" = v_mfma_f32_32x32x2_f32, an exact fmaf chain; "bf16x6" =
+# Matrix-core form of the fp32 conv math (hip.FORMS.f32_form, passed with every conv / pack call as
+# msl_forms): "mfma_f32" = v_mfma_f32_32x32x2_f32, an exact fmaf chain; "bf16x6" =
 # each operand split into three bf16 terms, six products per 16-deep K slice on
 # v_mfma_f32_32x32x16_bf16 with fp32 sums (fp32-accurate; csrc/dconv_kernels.h Split3); "f16x3" =
 # each operand tensor scaled by a power of two and split into two fp16 terms, three products per
 # slice on v_mfma_f32_32x32x16_f16 with fp32 sums (fp32-accurate; dconv_kernels.h Split2h).
 F32_FORMS = {"mfma_f32": 0, "bf16x6": 2, "f16x3": 5}
 SPLIT_FORMS = ("bf16x6", "f16x3")  # the forms the HIP pointwise / 128-row kernels run split
-_FORM = [None]  # the library's current form code, mirrored for the pack-cache keys
 
 
 def _form_code():
-    if _FORM[0] is None:
-        _FORM[0] = hip.load(require_gpu=False).msl_conv_f32_form()
-    return _FORM[0]
+    """The f32 form code the conv / pack calls pass (packs are form-specific: it keys the pack caches)."""
+    return hip.FORMS.f32_form
 
 
 def set_f32_form(form):
     """Select the fp32 conv form; returns the previous one."""
     if form not in F32_FORMS:
         raise ValueError(f"fp32 conv form must be one of {sorted(F32_FORMS)}, got {form!r}")
-    lib = hip.load(require_gpu=False)
-    prev = lib.msl_conv_f32_form()
-    hip.check(lib.msl_conv_set_f32_form(F32_FORMS[form]), "msl_conv_set_f32_form")
-    _FORM[0] = F32_FORMS[form]  # packs are form-specific: the cache keys change with it
+    prev = hip.set_form("f32_form", F32_FORMS[form])
     return {v: k for k, v in F32_FORMS.items()}[prev]
 
 
 def set_bn_fused(fused):
-    """Select the BN kernel form (msl_bn_set_fused): True = one fused launch per train-mode BN
+    """Select the BN kernel form (msl_forms.bn_fused): True = one fused launch per train-mode BN
     call on maps of <= 16384 px (<= 33792 px with >= 128 channels); returns the previous setting."""
-    lib = hip.load(require_gpu=False)
-    prev = bool(lib.msl_bn_fused())
-    hip.check(lib.msl_bn_set_fused(int(bool(fused))), "msl_bn_set_fused")
-    return prev
+    return bool(hip.set_form("bn_fused", int(bool(fused))))
 
 
 def f32_form():
-    lib = hip.load(require_gpu=False)
-    return {v: k for k, v in F32_FORMS.items()}[lib.msl_conv_f32_form()]
+    return {v: k for k, v in F32_FORMS.items()}[hip.FORMS.f32_form]
 
 
 def _fn(lib, name, math):
@@ -257,14 +248,15 @@ class PackCache:
             s = hip.stream_ptr()
             wc = [w.detach().contiguous() for w in weights]
             if self.pointwise:
-                hip.check(lib.msl_pconv_pack(wc[0].data_ptr(), cin, cout, for_dgrad, buf.data_ptr(), s),
+                hip.check(lib.msl_pconv_pack(wc[0].data_ptr(), cin, cout, for_dgrad, buf.data_ptr(), hip.forms(), s),
                           "msl_pconv_pack")
             else:
                 # one call packs every branch (and splits the bf16x6 planes behind them)
                 stride = (wc[1].data_ptr() - wc[0].data_ptr()) // 4 if nb == 2 else 0
                 if nb == 2 and (wc[1].data_ptr() - wc[0].data_ptr()) % 4:
                     raise hip.MSLError("dconv pack: misaligned branch weights")
-                hip.check(lib.msl_dconv_pack(wc[0].data_ptr(), stride, nb, cin, cout, for_dgrad, buf.data_ptr(), s),
+                hip.check(lib.msl_dconv_pack(wc[0].data_ptr(), stride, nb, cin, cout, for_dgrad, buf.data_ptr(),
+                                             hip.forms(), s),
                           "msl_dconv_pack")
             self.buf[for_dgrad] = buf
             self.key[for_dgrad] = key
@@ -361,7 +353,8 @@ class PackBatch:
         lib = hip.load()
         s = hip.stream_ptr()
         for taps, (jt, st, n, total) in self.tables.items():
-            hip.check(lib.msl_conv_pack_many(jt.data_ptr(), st.data_ptr(), n, taps, total, s), "msl_conv_pack_many")
+            hip.check(lib.msl_conv_pack_many(jt.data_ptr(), st.data_ptr(), n, taps, total, hip.forms(), s),
+                      "msl_conv_pack_many")
         for (c, d), k in zip(jobs, keys):
             c.key[d] = k
         self.launches += 1
@@ -403,7 +396,7 @@ class _DConv3x3(Function):
         xpart = _parts(x, math, compute=_split_gemm(cout, cin))
         hip.check(_conv_call(lib, "msl_dconv_fwd", math,
                              (x.data_ptr(), packed.data_ptr(), hip.ptr(bias), y.data_ptr(), nb, cin, cout, h, w, n,
-                              dil0, dil1 if nb > 1 else 0, hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb,
+                              dil0, dil1 if nb > 1 else 0, hip.forms(), ws.data_ptr(), wsb,
                               hip.stream_ptr()), (xpart,)), "msl_dconv_fwd")
         if probe is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
@@ -432,7 +425,7 @@ class _DConv3x3(Function):
             ws = hip.workspace(wsb, x.device)
             hip.check(_conv_call(lib, "msl_dconv_dgrad", math,
                                  (gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin, cout, h, w, n, dil0, d1,
-                                  hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (gpart,)),
+                                  hip.forms(), ws.data_ptr(), wsb, s), (gpart,)),
                       "msl_dconv_dgrad")
         sink = grad_sink(weights[0]) if (nb == 1 and not has_bias and ctx.needs_input_grad[1]) else None
         wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w, n)
@@ -443,7 +436,7 @@ class _DConv3x3(Function):
                 ws = hip.workspace(wsb, x.device)
                 hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
                                      (x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w, n, dil0, 0, 1,
-                                      ws.data_ptr(), wsb, hip.stream_ptr()), (xpart, gpart)), "msl_dconv_wgrad")
+                                      hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr()), (xpart, gpart)), "msl_dconv_wgrad")
             if side is not None:
                 _keep(side, x, gy, *(q[0] for q in (xpart, gpart) if q is not None))
             fg.notify(i)
@@ -453,7 +446,7 @@ class _DConv3x3(Function):
         db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
         hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
                              (x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb, cin, cout, h, w,
-                              n, dil0, d1, 0, ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
+                              n, dil0, d1, 0, hip.forms(), ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
         dw0 = dw_all[0]
         dw1 = dw_all[1] if nb > 1 else None
         db0 = db_all[0] if has_bias else None
@@ -534,7 +527,7 @@ class _ASPPShift(Function):
         s = hip.stream_ptr()
         hip.check(_conv_call(lib, "msl_pconv_fwd", math,
                              (x.data_ptr(), packed.data_ptr(), z.data_ptr(), cin, m, p,
-                              hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (xpart,)), "msl_pconv_fwd")
+                              hip.forms(), ws.data_ptr(), wsb, s), (xpart,)), "msl_pconv_fwd")
         bias = None
         if b0 is not None:
             bias = torch.stack([b0] if nb == 1 else [b0, b1]).contiguous()
@@ -566,7 +559,7 @@ class _ASPPShift(Function):
             dx = torch.empty_like(x)
             wsb = lib.msl_pconv_dgrad_workspace(cin, m, p)
             ws = hip.workspace(wsb, x.device)
-            cnt = hip.counters(x.device).data_ptr()
+            cnt = hip.forms()
             if math == "bf16":
                 st = lib.msl_pconv_dgrad_bf16(g.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, m, p, cnt,
                                               ws.data_ptr(), wsb, s)
@@ -581,7 +574,7 @@ class _ASPPShift(Function):
             wsb = lib.msl_pconv_wgrad_workspace(cin, m, p)
             ws = hip.workspace(wsb, x.device)
             hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
-                                 (x.data_ptr(), g.data_ptr(), dwp.data_ptr(), cin, m, p, 0, ws.data_ptr(), wsb, s),
+                                 (x.data_ptr(), g.data_ptr(), dwp.data_ptr(), cin, m, p, 0, hip.forms(), ws.data_ptr(), wsb, s),
                                  (ctx.xpart, gpart)), "msl_pconv_wgrad")
             dw_all = torch.empty((nb, c, cin, 3, 3), dtype=_f32, device=x.device)
             hip.check(lib.msl_aspp_weight_grad(dwp.data_ptr(), nb, c, cin, dw_all.data_ptr(), s), "msl_aspp_weight_grad")
@@ -627,7 +620,7 @@ class _PConv(Function):
         xpart = _parts(x, math, compute=_split_gemm(cout, cin))
         hip.check(_conv_call(lib, "msl_pconv_fwd", math,
                              (x.data_ptr(), packed.data_ptr(), y.data_ptr(), cin, cout, p,
-                              hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()), (xpart,)),
+                              hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr()), (xpart,)),
                   "msl_pconv_fwd")
         ctx.save_for_backward(x, weight)
         ctx.meta = (cin, cout, p, cache, math)
@@ -656,7 +649,7 @@ class _PConv(Function):
             packed_d = cache.get([weight], cin, cout, 1)
             wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
             ws = hip.workspace(wsb, x.device)
-            cnt = hip.counters(x.device).data_ptr()
+            cnt = hip.forms()
             if math == "bf16":
                 tgt = torch.empty_like(x) if acc else dx
                 hip.check(lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), tgt.data_ptr(), cin, cout, p,
@@ -677,7 +670,7 @@ class _PConv(Function):
             ws = hip.workspace(wsb, x.device)
             hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
                                  (x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p, int(sink is not None),
-                                  ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.xpart, gpart)), "msl_pconv_wgrad")
+                                  hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.xpart, gpart)), "msl_pconv_wgrad")
         if side is not None:
             _keep(side, x, gy, *(q[0] for q in (ctx.xpart, gpart) if q is not None))
         if sink is None:
@@ -748,7 +741,7 @@ class _StemConv(Function):
         cpart = _parts(col, math, compute=_split_gemm(cout, kk))
         hip.check(_conv_call(lib, "msl_pconv_fwd", math,
                              (col.data_ptr(), packed.data_ptr(), y.data_ptr(), kk, cout, p,
-                              hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, s), (cpart,)), "msl_pconv_fwd")
+                              hip.forms(), ws.data_ptr(), wsb, s), (cpart,)), "msl_pconv_fwd")
         ctx.save_for_backward(col, weight)
         ctx.meta = (cin, h, w, n, kh, kw, stride, pad, ho, wo, cache, math)
         ctx.cpart = cpart
@@ -769,7 +762,7 @@ class _StemConv(Function):
             dcol = torch.empty_like(col)
             wsb = lib.msl_pconv_dgrad_workspace(kk, cout, p)
             ws = hip.workspace(wsb, gy.device)
-            cnt = hip.counters(gy.device).data_ptr()
+            cnt = hip.forms()
             if math == "bf16":
                 st = lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), dcol.data_ptr(), kk, cout, p, cnt,
                                               ws.data_ptr(), wsb, s)
@@ -791,7 +784,7 @@ class _StemConv(Function):
             ws = hip.workspace(wsb, gy.device)
             hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
                                  (col.data_ptr(), gy.data_ptr(), dst.data_ptr(), kk, cout, p, int(sink is not None),
-                                  ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.cpart, gpart)), "msl_pconv_wgrad")
+                                  hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.cpart, gpart)), "msl_pconv_wgrad")
         if side is not None:
             _keep(side, col, gy, *(q[0] for q in (ctx.cpart, gpart) if q is not None))
         if sink is None:
@@ -1193,18 +1186,18 @@ class _BNAct(Function):
         # the fused kernel has it in registers; after a split-form BN (stem, 64-channel layer1) a
         # conv that needs it reduces it itself (its first consumer is often an exact-f32 GEMM)
         am = torch.empty(c, dtype=_f32, device=x.device) if (
-            _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(bool(training)))) else None
+            _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(bool(training)), hip.forms())) else None
         hip.check(lib.msl_bn_fwd_am(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
                                     hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
                                     save_mean.data_ptr(), save_invstd.data_ptr(), c, p, n, int(bool(training)),
-                                    int(update), float(momentum), float(eps), int(bool(relu)), ws.data_ptr(), wsb,
+                                    int(update), float(momentum), float(eps), int(bool(relu)), hip.forms(), ws.data_ptr(), wsb,
                                     hip.stream_ptr(), hip.ptr(am)), "msl_bn_fwd")
         if am is not None:
             _tag_absmax(y, am)
         # ReLU without a residual under the fused kernels (p <= 16384): the backward recomputes the
         # mask from x (msl_bn_bwd_am_beta, y = NULL) instead of reading y
         remask = (bool(relu) and residual is None and p <= 16384
-                  and bool(lib.msl_bn_uses_fused(c, p, int(bool(training)))))
+                  and bool(lib.msl_bn_uses_fused(c, p, int(bool(training)), hip.forms())))
         ctx.save_for_backward(x, weight, y if (relu and not remask) else None, save_mean, save_invstd)
         ctx.bias = bias
         ctx.meta = (c, p, n, bool(training), bool(relu))
@@ -1233,11 +1226,11 @@ class _BNAct(Function):
         ws = hip.workspace(wsb, x.device)
         # f16x3: the per-channel absmax of dx, the gradient the conv before this BN reads twice
         am = torch.empty(c, dtype=_f32, device=x.device) if (
-            dx is not None and _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(training))) else None
+            dx is not None and _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(training), hip.forms())) else None
         hip.check(lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight),
                                          hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(),
                                          hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n,
-                                         int(training), int(relu), int(direct), ws.data_ptr(), wsb,
+                                         int(training), int(relu), int(direct), hip.forms(), ws.data_ptr(), wsb,
                                          hip.stream_ptr(), hip.ptr(am)), "msl_bn_bwd")
         if am is not None:
             _tag_absmax(dx, am)

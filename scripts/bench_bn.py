@@ -42,7 +42,7 @@ def main():
     args = ap.parse_args()
     lib = hip.load()
     if args.unfused:
-        lib.msl_bn_set_fused(0)
+        hip.set_form("bn_fused", 0)
     p = args.hw[0] * args.hw[1]
     n = args.nimg
     s = hip.stream_ptr()
@@ -64,18 +64,20 @@ def main():
         def fwd():
             hip.check(lib.msl_bn_fwd_am(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), hip.ptr(r), y.data_ptr(),
                                         rm.data_ptr(), rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, n, 1,
-                                        1, 0.1, 1e-5, int(relu), ws.data_ptr(), wsb, s, fa.data_ptr()), "fwd")
+                                        1, 0.1, 1e-5, int(relu), hip.forms(), ws.data_ptr(), wsb, s,
+                                        fa.data_ptr()), "fwd")
 
         def bwd(with_y):
             def f():
                 hip.check(lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), y.data_ptr() if with_y else None,
                                                  gamma.data_ptr(), beta.data_ptr(), sm.data_ptr(), si.data_ptr(),
                                                  dx.data_ptr(), hip.ptr(dres), dg.data_ptr(), db.data_ptr(), c, p, n,
-                                                 1, int(relu), 0, ws.data_ptr(), wsb, s, ba.data_ptr()), "bwd")
+                                                 1, int(relu), 0, hip.forms(), ws.data_ptr(), wsb, s,
+                                                 ba.data_ptr()), "bwd")
             return f
 
         mb = c * n * p * 4 / 1e6
-        rec = {"c": c, "res": res, "relu": relu, "p": p, "nimg": n, "fused": lib.msl_bn_uses_fused(c, p, 1)}
+        rec = {"c": c, "res": res, "relu": relu, "p": p, "nimg": n, "fused": lib.msl_bn_uses_fused(c, p, 1, hip.forms())}
         t = timed(fwd, args.reps)
         rec["fwd_us"] = round(t, 2)
         rec["fwd_TBps"] = round(mb * (3 if res else 2) / t, 3)

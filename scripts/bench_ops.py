@@ -44,7 +44,7 @@ def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W, nimg=1):
     lib = hip.load()
     s = hip.stream_ptr()
     p = h * w * nimg
-    cnt = hip.counters(x.device).data_ptr()
+    cnt = hip.forms()
     cache = ops.PackCache(pointwise=(k == 1))
     xpart = ops._parts(x)
     gpart = ops._parts(gy)
@@ -61,7 +61,7 @@ def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W, nimg=1):
         dgr = lambda: hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), pd.data_ptr(), dx.data_ptr(), cin, cout, p,  # noqa: E731
                                                            0, cnt, wsd.data_ptr(), wsd.numel(), s, *ops._pp(gpart)), "dgrad")
         wgr = lambda: hip.check(lib.msl_pconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), cin, cout, p, 0,  # noqa: E731
-                                                       wsw.data_ptr(), wsw.numel(), s, *ops._pp(xpart),
+                                                       cnt, wsw.data_ptr(), wsw.numel(), s, *ops._pp(xpart),
                                                        *ops._pp(gpart)), "wgrad")
         ref = lambda xx, ww: F.conv2d(xx, ww)  # noqa: E731
     else:
@@ -76,7 +76,7 @@ def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W, nimg=1):
                                                        w, nimg, d, 0, cnt, wsd.data_ptr(), wsd.numel(), s,
                                                        *ops._pp(gpart)), "dgrad")
         wgr = lambda: hip.check(lib.msl_dconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), None, 1, cin,  # noqa: E731
-                                                       cout, h, w, nimg, d, 0, 0, wsw.data_ptr(), wsw.numel(), s,
+                                                       cout, h, w, nimg, d, 0, 0, cnt, wsw.data_ptr(), wsw.numel(), s,
                                                        *ops._pp(xpart), *ops._pp(gpart)), "wgrad")
         ref = lambda xx, ww: F.conv2d(xx, ww, padding=d, dilation=d)  # noqa: E731
     flops = 2.0 * cin * cout * k * k * p  # p counts every image

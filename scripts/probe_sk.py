@@ -27,7 +27,7 @@ wsb = lib.msl_dconv_fwd_workspace(1, cin, cout, h, w, nimg)
 ws = hip.workspace(wsb, "cuda")
 y_ref = torch.empty(1, cout, nimg, h, w, device="cuda")
 hip.check(lib.msl_dconv_fwd_sc(x.data_ptr(), packed.data_ptr(), None, y_ref.data_ptr(), 1, cin, cout, h, w, nimg, d, 0,
-                               hip.counters(x.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr(), *ops._pp(xpart)),
+                               hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr(), *ops._pp(xpart)),
           "ref")
 nw = so.probe_workers(cin, cout, h, w, nimg)
 prof = torch.zeros(nw * 4 * 8, dtype=torch.int64, device="cuda")

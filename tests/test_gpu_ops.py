@@ -5,6 +5,7 @@ against an fp64 CPU conv (the kernels are exact fp32 FMA chains, only the
 summation order differs); upsample forward bit-exact vs torch-CPU; losses
 1e-5 relative; class histograms bit-exact.
 """
+import ctypes
 import numpy as np
 import pytest
 import torch
@@ -536,20 +537,18 @@ def test_pack_forms_identical(kind, nb, cin, cout, for_dgrad):
     total = lib.msl_dconv_packed_elems(nb, cin, cout, for_dgrad) if kind == "d" else \
         lib.msl_pconv_packed_elems(cin, cout, for_dgrad)
     bufs = []
-    try:
-        for form in (0, 1):
-            assert lib.msl_conv_set_pack_form(form) == 0
-            buf = torch.full((total,), float("nan"), device=DEV)
-            if kind == "d":
-                st = lib.msl_dconv_pack(w.data_ptr(), cout * cin * 9, nb, cin, cout, for_dgrad, buf.data_ptr(),
-                                        hip.stream_ptr())
-            else:
-                st = lib.msl_pconv_pack(w.data_ptr(), cin, cout, for_dgrad, buf.data_ptr(), hip.stream_ptr())
-            assert st == 0
-            bufs.append(buf)
-        torch.cuda.synchronize()
-    finally:
-        lib.msl_conv_set_pack_form(1)
+    for form in (0, 1):
+        fm = hip.Forms(hip.FORMS.f32_form, 1, form, 1)  # the call's own forms (ABI 3), not the process's
+        buf = torch.full((total,), float("nan"), device=DEV)
+        if kind == "d":
+            st = lib.msl_dconv_pack(w.data_ptr(), cout * cin * 9, nb, cin, cout, for_dgrad, buf.data_ptr(),
+                                    ctypes.addressof(fm), hip.stream_ptr())
+        else:
+            st = lib.msl_pconv_pack(w.data_ptr(), cin, cout, for_dgrad, buf.data_ptr(), ctypes.addressof(fm),
+                                    hip.stream_ptr())
+        assert st == 0
+        bufs.append(buf)
+    torch.cuda.synchronize()
     assert torch.equal(bufs[0].view(torch.int32), bufs[1].view(torch.int32))
 
 
@@ -669,7 +668,7 @@ def test_pconv_dgrad_accumulate(cin, cout, h, w, f32_form):
     wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
     ws = hip.workspace(wsb, dx.device)
     assert lib.msl_pconv_dgrad_acc(gy.to(DEV).data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, 1,
-                                   hip.counters(dx.device).data_ptr(), ws.data_ptr(), wsb, hip.stream_ptr()) == 0
+                                   hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr()) == 0
     torch.cuda.synchronize()
     assert _rel(dx, ref) < 1e-5
 
@@ -703,10 +702,9 @@ def test_bottleneck_fused_residual_grad(f32_form, monkeypatch):
 def test_sk_hybrid_schedule(cin, cout, h, w, f32_form):
     """Forward-form schedule: data-parallel rounds + a stream-K remainder (default; 528 / 1056
     tiles leave 16 / 32 split tiles, 2048 x 8192 is exactly 1024 whole tiles and launches no
-    reduce) and pure stream-K (msl_conv_set_sk_hybrid(0)) both match fp64, forward and data
+    reduce) and pure stream-K (msl_forms.sk_hybrid 0) both match fp64, forward and data
     gradient."""
     from maxsquareloss_amd import hip
-    lib = hip.load()
     g = torch.Generator().manual_seed(cin + 11 * cout)
     x = torch.randn(1, cin, h, w, generator=g)
     wt = torch.randn(cout, cin, 1, 1, generator=g) * 0.05
@@ -717,7 +715,7 @@ def test_sk_hybrid_schedule(cin, cout, h, w, f32_form):
     outs = []
     try:
         for hybrid in (1, 0):
-            assert lib.msl_conv_set_sk_hybrid(hybrid) == 0
+            hip.set_form("sk_hybrid", hybrid)
             xg = x.to(DEV).requires_grad_()
             wg = wt.to(DEV).requires_grad_()
             y = ops.pconv(xg, wg, ops.PackCache(pointwise=True))
@@ -727,11 +725,12 @@ def test_sk_hybrid_schedule(cin, cout, h, w, f32_form):
             assert _rel(xg.grad, xr.grad) < 1e-5, hybrid
             outs.append((y.detach(), xg.grad))
     finally:
-        lib.msl_conv_set_sk_hybrid(1)
+        hip.set_form("sk_hybrid", 1)
     # the two schedules differ only in the fp32 summation order of split tiles
     assert _rel(outs[0][0], outs[1][0].double()) < 4e-6
     assert _rel(outs[0][1], outs[1][1].double()) < 4e-6
-    assert lib.msl_conv_set_sk_hybrid(2) != 0
+    with pytest.raises(hip.MSLError):
+        hip.set_form("sk_hybrid", 2)
 
 
 @pytest.mark.parametrize("cin,cout,h,w", [(256, 1024, 65, 129), (512, 2048, 17, 33), (128, 512, 33, 65),
@@ -755,8 +754,8 @@ def test_pconv_wgrad_accumulate_both_orientations(cin, cout, h, w, form):
         xd, gd, dw = x.to(DEV), gy.to(DEV), dw0.to(DEV)
         wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
         ws = hip.workspace(wsb, xd.device)
-        assert lib.msl_pconv_wgrad(xd.data_ptr(), gd.data_ptr(), dw.data_ptr(), cin, cout, p, 1, ws.data_ptr(), wsb,
-                                   hip.stream_ptr()) == 0
+        assert lib.msl_pconv_wgrad(xd.data_ptr(), gd.data_ptr(), dw.data_ptr(), cin, cout, p, 1, hip.forms(),
+                                   ws.data_ptr(), wsb, hip.stream_ptr()) == 0
         torch.cuda.synchronize()
         assert _rel(dw, ref) < 1e-5
         if form == "f16x3":
@@ -765,8 +764,8 @@ def test_pconv_wgrad_accumulate_both_orientations(cin, cout, h, w, form):
                 assert lib.msl_absmax_partials(t.data_ptr(), rows, p, q.data_ptr(), hip.stream_ptr()) == 0
             assert torch.equal(xp.cpu(), x.abs().amax(1)) and torch.equal(gp.cpu(), gy.abs().amax(1))  # per row
             dw2 = dw0.to(DEV)
-            assert lib.msl_pconv_wgrad_sc(xd.data_ptr(), gd.data_ptr(), dw2.data_ptr(), cin, cout, p, 1, ws.data_ptr(),
-                                          wsb, hip.stream_ptr(), xp.data_ptr(), cin, gp.data_ptr(), cout) == 0
+            assert lib.msl_pconv_wgrad_sc(xd.data_ptr(), gd.data_ptr(), dw2.data_ptr(), cin, cout, p, 1, hip.forms(),
+                                          ws.data_ptr(), wsb, hip.stream_ptr(), xp.data_ptr(), cin, gp.data_ptr(), cout) == 0
             torch.cuda.synchronize()
             assert torch.equal(dw2, dw)
     finally:
@@ -894,11 +893,11 @@ def test_bn_absmax_outputs(c, h, w, res, relu, fused):
             dg, db = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
             fa, ba = torch.full((c,), -1.0, device=DEV), torch.full((c,), -1.0, device=DEV)
             fargs = (x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), hip.ptr(r), y.data_ptr(), rm.data_ptr(),
-                     rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, 1, 1, 1, 0.1, 1e-5, int(relu), ws.data_ptr(),
-                     wsb, s)
+                     rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, 1, 1, 1, 0.1, 1e-5, int(relu), hip.forms(),
+                     ws.data_ptr(), wsb, s)
             bargs = (gy.data_ptr(), x.data_ptr(), y.data_ptr(), gamma.data_ptr(), sm.data_ptr(), si.data_ptr(),
-                     dx.data_ptr(), dres.data_ptr(), dg.data_ptr(), db.data_ptr(), c, p, 1, 1, int(relu), 0, ws.data_ptr(),
-                     wsb, s)
+                     dx.data_ptr(), dres.data_ptr(), dg.data_ptr(), db.data_ptr(), c, p, 1, 1, int(relu), 0, hip.forms(),
+                     ws.data_ptr(), wsb, s)
             if am:
                 assert lib.msl_bn_fwd_am(*fargs, fa.data_ptr()) == 0
                 assert lib.msl_bn_bwd_am(*bargs, ba.data_ptr()) == 0
@@ -945,15 +944,15 @@ def test_bn_bwd_relu_mask_recompute(c, h, w, nimg):
         sm, si = torch.empty(c * nimg, device=DEV), torch.empty(c * nimg, device=DEV)
         assert lib.msl_bn_fwd(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), None, y.data_ptr(), rm.data_ptr(),
                               rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, nimg, 1, 1, 0.1, 1e-5, 1,
-                              ws.data_ptr(), wsb, s) == 0
-        assert lib.msl_bn_uses_fused(c, p, 1) == 1
+                              hip.forms(), ws.data_ptr(), wsb, s) == 0
+        assert lib.msl_bn_uses_fused(c, p, 1, hip.forms()) == 1
         outs = []
         for remask in (False, True):
             dx = torch.empty_like(x)
             dg, db, am = (torch.empty(c, device=DEV) for _ in range(3))
             args = (gy.data_ptr(), x.data_ptr(), None if remask else y.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                     sm.data_ptr(), si.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(), c, p, nimg, 1, 1, 0,
-                    ws.data_ptr(), wsb, s, am.data_ptr())
+                    hip.forms(), ws.data_ptr(), wsb, s, am.data_ptr())
             assert lib.msl_bn_bwd_am_beta(*args) == 0
             torch.cuda.synchronize()
             outs.append((dx, dg, db, am))
@@ -962,18 +961,18 @@ def test_bn_bwd_relu_mask_recompute(c, h, w, nimg):
             assert torch.equal(a, b)
         # refusals: the split forms read y; msl_bn_bwd_am always needs it
         assert lib.msl_bn_bwd_am(gy.data_ptr(), x.data_ptr(), None, gamma.data_ptr(), sm.data_ptr(), si.data_ptr(),
-                                 dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(), c, p, nimg, 1, 1, 0, ws.data_ptr(),
-                                 wsb, s, None) == -3
+                                 dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(), c, p, nimg, 1, 1, 0, hip.forms(),
+                                 ws.data_ptr(), wsb, s, None) == -3
         big = 129 * 257  # fused, but the 33-element form keeps reading y (checked before any launch)
-        assert lib.msl_bn_uses_fused(256, big, 1) == 1
+        assert lib.msl_bn_uses_fused(256, big, 1, hip.forms()) == 1
         assert lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), None, gamma.data_ptr(), beta.data_ptr(),
                                       sm.data_ptr(), si.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(),
-                                      256, big, 1, 1, 1, 0, ws.data_ptr(), lib.msl_bn_workspace(256, big, 1), s,
+                                      256, big, 1, 1, 1, 0, hip.forms(), ws.data_ptr(), lib.msl_bn_workspace(256, big, 1), s,
                                       None) == -3
         ops.set_bn_fused(False)
         assert lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), None, gamma.data_ptr(), beta.data_ptr(),
                                       sm.data_ptr(), si.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(),
-                                      c, p, nimg, 1, 1, 0, ws.data_ptr(), wsb, s, None) == -3
+                                      c, p, nimg, 1, 1, 0, hip.forms(), ws.data_ptr(), wsb, s, None) == -3
     finally:
         ops.set_bn_fused(prev)
 

@@ -1,4 +1,5 @@
 """CPU tests of the host side: the C-ABI library, the model/optimizer plumbing and DP exchange."""
+import ctypes
 import json
 import os
 import re
@@ -62,16 +63,30 @@ def test_pure_host_entry_points():
     off = np.zeros(8, np.int64)
     n = lib.msl_sgd_plan(numels.ctypes.data, 4, ent.ctypes.data, off.ctypes.data, 8)
     assert n == 4 and list(ent[:4]) == [0, 1, 2, 2] and list(off[:4]) == [0, 0, 0, be]
-    # matrix-core form of the fp32 convs: f16x3 (5) by default, f32 MFMA (0) and bf16x6 (2)
-    # selectable, others refused
-    assert lib.msl_conv_f32_form() == 5
-    assert lib.msl_conv_set_f32_form(1) == -3 and lib.msl_conv_set_f32_form(7) == -3
-    assert lib.msl_conv_set_f32_form(0) == 0 and lib.msl_conv_f32_form() == 0
-    assert lib.msl_conv_set_f32_form(2) == 0 and lib.msl_conv_f32_form() == 2
-    assert lib.msl_conv_set_f32_form(5) == 0 and lib.msl_conv_f32_form() == 5
-    assert lib.msl_bn_fused() == 1 and lib.msl_bn_set_fused(2) == -3
-    assert lib.msl_bn_set_fused(0) == 0 and lib.msl_bn_fused() == 0
-    assert lib.msl_bn_set_fused(1) == 0 and lib.msl_bn_fused() == 1
+    # the per-call kernel forms (ABI 3, msl_forms): defaults f16x3 (5), hybrid schedule, one-launch
+    # packs, fused BN; f32 MFMA (0) and bf16x6 (2) selectable, other values refused; NULL = defaults
+    d = hip.Forms()
+    assert lib.msl_forms_default(ctypes.addressof(d)) == 0
+    assert (d.f32_form, d.sk_hybrid, d.pack_form, d.bn_fused) == (5, 1, 1, 1)
+    assert [(f, getattr(hip.FORMS, f)) for f, _ in hip.Forms._fields_] == [(f, getattr(d, f)) for f, _ in d._fields_]
+    assert lib.msl_forms_check(None) == 0
+    for field, good, bad in (("f32_form", (0, 2, 5), (1, 7, -1)), ("sk_hybrid", (0, 1), (2,)),
+                             ("pack_form", (0, 1), (2,)), ("bn_fused", (0, 1), (2, -1))):
+        for v in good + bad:
+            t = hip.Forms(5, 1, 1, 1)
+            setattr(t, field, v)
+            assert lib.msl_forms_check(ctypes.addressof(t)) == (0 if v in good else -3), (field, v)
+    t = hip.Forms(5, 1, 1, 2)
+    assert lib.msl_bn_uses_fused(256, 8385, 1, ctypes.addressof(t)) == -3
+    assert lib.msl_bn_uses_fused(256, 8385, 1, None) == 1
+    t.bn_fused = 0
+    assert lib.msl_bn_uses_fused(256, 8385, 1, ctypes.addressof(t)) == 0
+    # hip.set_form checks before it sets and returns the previous value
+    assert hip.set_form("sk_hybrid", 0) == 1 and hip.FORMS.sk_hybrid == 0
+    assert hip.set_form("sk_hybrid", 1) == 0
+    with pytest.raises(hip.MSLError):
+        hip.set_form("f32_form", 3)
+    assert hip.FORMS.f32_form == 5
 
 
 def test_compute_calls_fail_loudly_without_gpu():
