@@ -312,7 +312,8 @@ def test_config5_fp16_loss_curve():
             env.check(f"{phase} {k} RMS over {len(dg)} iterations", float(np.sqrt((dg ** 2).mean())),
                       float(np.sqrt((de ** 2).mean())), 1e-3 + sl.max())
             for i, (d, s) in enumerate(zip(dg, sl)):
-                env.check(f"{phase} it{i + (n_sync if free else 0)} {k}", d, 0.0, 0.0, bar=3 * de.max() + 1e-3 + s)
+                env.check(f"{phase} it{i + (n_sync if free else 0)} {k} (emulation: this iteration's)", d, de[i], 0.0,
+                          bar=3 * de.max() + 1e-3 + s)
         env.done()
     finally:
         ops.set_conv_math("fp32")
