@@ -447,6 +447,23 @@ int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const fl
 /* 1 if msl_bn_fwd / msl_bn_bwd run the fused one-block-per-channel kernels for this shape (their
  * _am absmax output is then free; the split forms add a pass over the output). */
 int msl_bn_uses_fused(int c, int p, int training, const msl_forms* forms);
+/* The ReLU mask as bits (r05): msl_bn_fwd_mask is msl_bn_fwd_am that also writes y > 0 of every
+ * pixel to relu_mask (bit e % 64 of word [row][e / 64], rows c * nimg + image, cdiv(p, 64) words per
+ * row: msl_bn_relu_mask_bytes); msl_bn_bwd_mask is msl_bn_bwd_am_beta with relu_mask in place of y,
+ * the same mask bit for bit.  For the residual BN + ReLU of a bottleneck (deeplab_multi.py:45-47)
+ * the backward then reads 1 bit per pixel instead of the 4-byte block output.  Both need relu and
+ * msl_bn_uses_fused(c, p, training, forms) (else MSL_ERR_ARG). */
+size_t msl_bn_relu_mask_bytes(int c, int p, int nimg);
+int msl_bn_fwd_mask(const float* x, const float* gamma, const float* beta, const float* residual,
+                    float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
+                    float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
+                    int update_running, float momentum, float eps, int relu, const msl_forms* forms, void* ws,
+                    size_t ws_bytes, msl_stream_t stream, float* absmax, uint64_t* relu_mask);
+int msl_bn_bwd_mask(const float* dy, const float* x, const uint64_t* relu_mask, const float* gamma,
+                    const float* beta, const float* save_mean, const float* save_invstd, float* dx, float* dres,
+                    float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
+                    int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream,
+                    float* absmax_dx);
 
 /* ------------------------------------------------------------------------
  * Training-time evaluation (tools/train_source.py:280-283 + utils/eval.py:109-118): for one

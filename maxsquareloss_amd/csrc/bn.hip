@@ -104,6 +104,7 @@ struct BnArgs {
   int C, NI, P, S, chunk, relu, training, update_running;  // C channels, NI images, P pixels per image
   float eps, momentum;
   float* absmax;  // [C] max |y| per channel (msl_bn_fwd_am: the next conv's f16x3 partials) or null
+  unsigned long long* mask;  // msl_bn_fwd_mask: y > 0 as bits, [row][cdiv(P, 64)] words (fused form) or null
 };
 
 // Batch statistics of row r (channel r / NI of image r % NI) from the fp64 partial sums.
@@ -225,6 +226,7 @@ struct BnBwdArgs {
   double* part;
   int C, NI, P, S, chunk, relu, training, accumulate;
   float* absmax;  // [C] max |dx| per channel (msl_bn_bwd_am) or null
+  const unsigned long long* mask;  // msl_bn_bwd_mask: the forward's y > 0 bits (fused form) instead of y
 };
 
 template <bool VEC>
@@ -504,17 +506,31 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
 #pragma unroll
     for (int j = 0; j < EPT; ++j) rv[j] = 0.f;
   }
+  // r05: with a.mask, y > 0 of each wave's 64 consecutive pixels as one 64-bit word (a ballot): the
+  // residual BN's backward then reads 1 bit per pixel for its ReLU mask instead of the 4-byte y
+  // (lane j of the wave keeps block j's word, and the EPT words leave in one masked store after the loop)
+  unsigned long long* mrow = a.mask ? a.mask + (long long)r * cdiv(P, 64) : nullptr;
+  unsigned long long myword = 0;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = j * kBnFusedThreads + t;
+    bool pos = false;
     if (e < P) {
       float v = __fmaf_rn(xv[j], alpha, bsh);
       v += rv[j];
       v = a.relu ? fmaxf(v, 0.f) : v;
       bn_st(ry, vo, j, v);
       am = fmaxf(am, fabsf(v));
+      pos = v > 0.f;
+    }
+    if (mrow) {
+      const unsigned long long bits = __ballot(pos);
+      if ((t & 63) == j) myword = bits;
     }
   }
+  static_assert(EPT <= 64, "one mask word per lane");
+  if (mrow && (t & 63) < EPT && (t & 63) * kBnFusedThreads + (t & ~63) < P)
+    mrow[(t & 63) * (kBnFusedThreads / 64) + (t >> 6)] = myword;
   }  // images
   if (a.absmax) {
     __shared__ float redm[kBnFusedThreads / 64];
@@ -544,7 +560,17 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
     xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
   }
   const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
-  if (a.relu && a.y) {
+  if (a.relu && a.mask) {  // the forward's y > 0 bits: one 8-byte word per wave and element block
+    const unsigned long long* mrow = a.mask + (long long)r * cdiv(P, 64);
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = j * kBnFusedThreads + t;
+      if (j * kBnFusedThreads + (t & ~63) < P) {  // wave-uniform: the word exists
+        const unsigned long long bits = mrow[j * (kBnFusedThreads / 64) + (t >> 6)];
+        if (e < P && !((bits >> (t & 63)) & 1ull)) g[j] = 0.f;
+      }
+    }
+  } else if (a.relu && a.y) {
     const __amdgpu_buffer_rsrc_t ryy = bn_row(a.y + base, P);
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
@@ -643,6 +669,21 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
                   float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
                   int update_running, float momentum, float eps, int relu, const msl_forms* forms, void* ws,
                   size_t ws_bytes, msl_stream_t stream, float* absmax) {
+  return msl_bn_fwd_mask(x, gamma, beta, residual, y, running_mean, running_var, num_batches_tracked, save_mean,
+                         save_invstd, c, p, nimg, training, update_running, momentum, eps, relu, forms, ws, ws_bytes,
+                         stream, absmax, nullptr);
+}
+
+size_t msl_bn_relu_mask_bytes(int c, int p, int nimg) {
+  if (c < 1 || p < 1 || nimg < 1) return 0;
+  return (size_t)c * nimg * cdiv(p, 64) * sizeof(uint64_t);
+}
+
+int msl_bn_fwd_mask(const float* x, const float* gamma, const float* beta, const float* residual,
+                    float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
+                    float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
+                    int update_running, float momentum, float eps, int relu, const msl_forms* forms, void* ws,
+                    size_t ws_bytes, msl_stream_t stream, float* absmax, uint64_t* relu_mask) {
   if (!x || !y || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
     return MSL_ERR_ARG;
   if ((!training || update_running) && (!running_mean || !running_var)) return MSL_ERR_ARG;
@@ -654,6 +695,7 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
   const bool vec = al16(x) && al16(y) && (!residual || al16(residual));
   if (forms_bad(forms)) return MSL_ERR_ARG;
   const bool fused = training && bn_fused_enabled(forms) && bn_fused_shape(c, p);
+  if (relu_mask && !(fused && relu)) return MSL_ERR_ARG;  // the bits come from the fused kernels
   if (training && !fused) {
     if (vec)
       hipLaunchKernelGGL(k_bn_stats<true>, dim3(R, S), dim3(256), 0, st, x, p, S, part);
@@ -684,6 +726,7 @@ int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const f
   a.eps = eps;
   a.momentum = momentum;
   a.absmax = absmax;
+  a.mask = reinterpret_cast<unsigned long long*>(relu_mask);
   if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>, c, p, st, a);
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec)
@@ -712,16 +755,17 @@ int msl_bn_bwd_am(const float* dy, const float* x, const float* y, const float* 
                             training, relu, accumulate_params, forms, ws, ws_bytes, stream, absmax_dx);
 }
 
-int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const float* gamma, const float* beta,
-                       const float* save_mean, const float* save_invstd, float* dx, float* dres,
-                       float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
-                       int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
+static int bn_bwd(const float* dy, const float* x, const float* y, const uint64_t* relu_mask, const float* gamma,
+                  const float* beta, const float* save_mean, const float* save_invstd, float* dx, float* dres,
+                  float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu, int accumulate_params,
+                  const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
   if (!dy || !x || !save_mean || !save_invstd || c < 1 || p < 1 || nimg < 1 || (long long)c * nimg >= (1LL << 31))
     return MSL_ERR_ARG;
   if (forms_bad(forms)) return MSL_ERR_ARG;
   const bool fused = training && bn_fused_enabled(forms) && bn_fused_shape(c, p);
+  if (relu_mask && !(fused && relu)) return MSL_ERR_ARG;  // the bits are read by the fused kernels
   // the mask recompute is the fused kernels' alone, up to 16 elements per lane
-  if (relu && !y && !(fused && p <= kBnRemaskMaxEpt * kBnFusedThreads)) return MSL_ERR_ARG;
+  if (relu && !y && !relu_mask && !(fused && p <= kBnRemaskMaxEpt * kBnFusedThreads)) return MSL_ERR_ARG;
   if (absmax_dx && !dx) return MSL_ERR_ARG;
   if (ws_bytes < msl_bn_workspace(c, p, nimg)) return MSL_ERR_WORKSPACE;
   hipStream_t st = as_stream(stream);
@@ -749,6 +793,7 @@ int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const fl
   a.training = training;
   a.accumulate = accumulate_params;
   a.absmax = absmax_dx;
+  a.mask = reinterpret_cast<const unsigned long long*>(relu_mask);
   if (fused)
     return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
@@ -765,6 +810,24 @@ int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const fl
   MSL_CHECK_LAUNCH();
   if (absmax_dx) return absmax_rows(dx, c, nimg * p, absmax_dx, st);  // the split forms: a pass over dx
   return MSL_OK;
+}
+
+int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const float* gamma, const float* beta,
+                       const float* save_mean, const float* save_invstd, float* dx, float* dres,
+                       float* dgamma, float* dbeta, int c, int p, int nimg, int training, int relu,
+                       int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream,
+                       float* absmax_dx) {
+  return bn_bwd(dy, x, y, nullptr, gamma, beta, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, nimg, training,
+                relu, accumulate_params, forms, ws, ws_bytes, stream, absmax_dx);
+}
+
+int msl_bn_bwd_mask(const float* dy, const float* x, const uint64_t* relu_mask, const float* gamma, const float* beta,
+                    const float* save_mean, const float* save_invstd, float* dx, float* dres, float* dgamma,
+                    float* dbeta, int c, int p, int nimg, int training, int relu, int accumulate_params,
+                    const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, float* absmax_dx) {
+  if (!relu_mask || !relu) return MSL_ERR_ARG;
+  return bn_bwd(dy, x, nullptr, relu_mask, gamma, beta, save_mean, save_invstd, dx, dres, dgamma, dbeta, c, p, nimg,
+                training, relu, accumulate_params, forms, ws, ws_bytes, stream, absmax_dx);
 }
 
 }  // extern "C"

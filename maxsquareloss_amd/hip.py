@@ -88,6 +88,9 @@ SIGNATURES = {
     "msl_bn_fwd_am": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_p, c_sz, c_p, c_p]),
     "msl_bn_bwd_am": (c_int, [c_p] * 10 + [c_int] * 6 + [c_p, c_p, c_sz, c_p, c_p]),
     "msl_bn_bwd_am_beta": (c_int, [c_p] * 11 + [c_int] * 6 + [c_p, c_p, c_sz, c_p, c_p]),
+    "msl_bn_relu_mask_bytes": (c_sz, [c_int] * 3),
+    "msl_bn_fwd_mask": (c_int, [c_p] * 10 + [c_int] * 5 + [c_f, c_f, c_int, c_p, c_p, c_sz, c_p, c_p, c_p]),
+    "msl_bn_bwd_mask": (c_int, [c_p] * 11 + [c_int] * 6 + [c_p, c_p, c_sz, c_p, c_p]),
     "msl_image_transform": (c_int, [c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p, c_p]),
     "msl_label_transform": (c_int, [c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
     "msl_im2col": (c_int, [c_p] + [c_int] * 11 + [c_p, c_p]),

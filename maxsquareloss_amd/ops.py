@@ -1164,6 +1164,12 @@ def iw_maxsquare_prob(prob, label, ratio):
 
 
 # --------------------------------------------------------------------------- batch norm (+ReLU, +residual)
+# r05: the residual BN + ReLU (each bottleneck's bn3, deeplab_multi.py:45-47) keeps its ReLU mask as bits
+# for the backward (msl_bn_fwd_mask / msl_bn_bwd_mask) instead of re-reading the block output; the same
+# mask bit for bit (tests/test_gpu_ops.py test_bn_relu_mask_bits).  False: the backward reads y.
+BN_MASK_BITS = True
+
+
 class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, training, momentum,
@@ -1185,20 +1191,26 @@ class _BNAct(Function):
         # f16x3: the per-channel absmax of y for the convs that read it (their operand scales), where
         # the fused kernel has it in registers; after a split-form BN (stem, 64-channel layer1) a
         # conv that needs it reduces it itself (its first consumer is often an exact-f32 GEMM)
-        am = torch.empty(c, dtype=_f32, device=x.device) if (
-            _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(bool(training)), hip.forms())) else None
-        hip.check(lib.msl_bn_fwd_am(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
-                                    hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
-                                    save_mean.data_ptr(), save_invstd.data_ptr(), c, p, n, int(bool(training)),
-                                    int(update), float(momentum), float(eps), int(bool(relu)), hip.forms(), ws.data_ptr(), wsb,
-                                    hip.stream_ptr(), hip.ptr(am)), "msl_bn_fwd")
+        fused = bool(lib.msl_bn_uses_fused(c, p, int(bool(training)), hip.forms()))
+        am = torch.empty(c, dtype=_f32, device=x.device) if (_h3(CONV_MATH) and fused) else None
+        # r05: a residual BN + ReLU under the fused kernels writes the ReLU mask as bits (msl_bn_fwd_mask),
+        # so its backward reads 1 bit per pixel instead of y (msl_bn_bwd_mask)
+        bits = None
+        if relu and residual is not None and fused and BN_MASK_BITS:
+            bits = torch.empty(lib.msl_bn_relu_mask_bytes(c, p, n) // 8, dtype=torch.int64, device=x.device)
+        hip.check(lib.msl_bn_fwd_mask(x.data_ptr(), hip.ptr(weight), hip.ptr(bias), hip.ptr(residual), y.data_ptr(),
+                                      hip.ptr(running_mean), hip.ptr(running_var), hip.ptr(num_batches),
+                                      save_mean.data_ptr(), save_invstd.data_ptr(), c, p, n, int(bool(training)),
+                                      int(update), float(momentum), float(eps), int(bool(relu)), hip.forms(),
+                                      ws.data_ptr(), wsb, hip.stream_ptr(), hip.ptr(am), hip.ptr(bits)), "msl_bn_fwd")
         if am is not None:
             _tag_absmax(y, am)
         # ReLU without a residual under the fused kernels (p <= 16384): the backward recomputes the
         # mask from x (msl_bn_bwd_am_beta, y = NULL) instead of reading y
-        remask = (bool(relu) and residual is None and p <= 16384
-                  and bool(lib.msl_bn_uses_fused(c, p, int(bool(training)), hip.forms())))
-        ctx.save_for_backward(x, weight, y if (relu and not remask) else None, save_mean, save_invstd)
+        remask = (bool(relu) and residual is None and p <= 16384 and fused)
+        ctx.bits = bits
+        ctx.save_for_backward(x, weight, y if (relu and not remask and bits is None) else None, save_mean,
+                              save_invstd)
         ctx.bias = bias
         ctx.meta = (c, p, n, bool(training), bool(relu))
         ctx.hold = hold
@@ -1227,11 +1239,18 @@ class _BNAct(Function):
         # f16x3: the per-channel absmax of dx, the gradient the conv before this BN reads twice
         am = torch.empty(c, dtype=_f32, device=x.device) if (
             dx is not None and _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(training), hip.forms())) else None
-        hip.check(lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight),
-                                         hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(),
-                                         hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n,
-                                         int(training), int(relu), int(direct), hip.forms(), ws.data_ptr(), wsb,
-                                         hip.stream_ptr(), hip.ptr(am)), "msl_bn_bwd")
+        if ctx.bits is not None:
+            st = lib.msl_bn_bwd_mask(gy.data_ptr(), x.data_ptr(), ctx.bits.data_ptr(), hip.ptr(weight),
+                                     hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(), hip.ptr(dx),
+                                     hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n, int(training), int(relu),
+                                     int(direct), hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr(), hip.ptr(am))
+        else:
+            st = lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight),
+                                        hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(),
+                                        hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n,
+                                        int(training), int(relu), int(direct), hip.forms(), ws.data_ptr(), wsb,
+                                        hip.stream_ptr(), hip.ptr(am))
+        hip.check(st, "msl_bn_bwd")
         if am is not None:
             _tag_absmax(dx, am)
         if direct:

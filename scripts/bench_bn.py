@@ -47,7 +47,7 @@ def main():
     n = args.nimg
     s = hip.stream_ptr()
     for c, res, relu in [(128, False, True), (256, False, True), (512, False, True), (1024, True, True),
-                         (1024, False, False), (2048, True, True)]:
+                         (1024, False, False), (2048, True, True), (512, True, True)]:
         g = torch.Generator().manual_seed(c)
         x = (torch.randn(c, n * p, generator=g) * 3 + 1).to(DEV)
         r = torch.randn(c, n * p, generator=g).to(DEV) if res else None
@@ -84,6 +84,22 @@ def main():
         t = timed(bwd(True), args.reps)
         rec["bwd_us"] = round(t, 2)
         rec["bwd_TBps"] = round(mb * ((3 if relu else 2) + (2 if res else 1)) / t, 3)
+        if relu and res and not args.unfused:  # r05: the ReLU mask as bits (msl_bn_fwd_mask / msl_bn_bwd_mask)
+            bits = torch.empty(lib.msl_bn_relu_mask_bytes(c, p, n) // 8, dtype=torch.int64, device=DEV)
+
+            def fwdm():
+                hip.check(lib.msl_bn_fwd_mask(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), hip.ptr(r), y.data_ptr(),
+                                              rm.data_ptr(), rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p,
+                                              n, 1, 1, 0.1, 1e-5, int(relu), hip.forms(), ws.data_ptr(), wsb, s,
+                                              fa.data_ptr(), bits.data_ptr()), "fwd_mask")
+
+            def bwdm():
+                hip.check(lib.msl_bn_bwd_mask(gy.data_ptr(), x.data_ptr(), bits.data_ptr(), gamma.data_ptr(),
+                                              beta.data_ptr(), sm.data_ptr(), si.data_ptr(), dx.data_ptr(),
+                                              hip.ptr(dres), dg.data_ptr(), db.data_ptr(), c, p, n, 1, int(relu), 0,
+                                              hip.forms(), ws.data_ptr(), wsb, s, ba.data_ptr()), "bwd_mask")
+            rec["fwd_mask_us"] = round(timed(fwdm, args.reps), 2)
+            rec["bwd_mask_us"] = round(timed(bwdm, args.reps), 2)
         if relu and not res and not args.unfused:
             t = timed(bwd(False), args.reps)
             rec["bwd_remask_us"] = round(t, 2)

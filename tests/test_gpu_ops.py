@@ -977,6 +977,75 @@ def test_bn_bwd_relu_mask_recompute(c, h, w, nimg):
         ops.set_bn_fused(prev)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,h,w,nimg", [(1024, 65, 129, 2), (256, 129, 257, 2), (512, 65, 129, 1), (2048, 17, 33, 2)])
+def test_bn_relu_mask_bits(c, h, w, nimg):
+    """msl_bn_fwd_mask / msl_bn_bwd_mask (r05): the residual BN + ReLU writes y > 0 as bits (bit e % 64 of
+    word [row][e / 64]) and its backward reads them instead of y - the same y / statistics / dx / dres /
+    dgamma / dbeta / absmax bytes as msl_bn_fwd_am + msl_bn_bwd_am_beta reading y, incl. pre-activations
+    that are exactly 0, the 33-element form (layer1's 33153 px) and a tail word; refused without relu or
+    under the split kernels."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    g = torch.Generator().manual_seed(c + 7 * nimg)
+    p = h * w
+    x = torch.randn(c, nimg, p, generator=g) * 3 + 1
+    x[:, :, : p // 3] = x[:, :, :1]  # a third of each row at the mean: pre-activation = beta + residual
+    x = x.reshape(c, nimg * p).to(DEV)
+    res = torch.randn(c, nimg * p, generator=g)
+    res[::2, : p // 3] = 0.0
+    res = res.to(DEV)
+    gamma = (torch.rand(c, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(c, generator=g)
+    beta[::2] = 0.0
+    beta = beta.to(DEV)
+    gy = torch.randn(c, nimg * p, generator=g).to(DEV)
+    wsb = lib.msl_bn_workspace(c, p, nimg)
+    ws = hip.workspace(wsb, x.device)
+    s = hip.stream_ptr()
+    nw = (p + 63) // 64
+    assert lib.msl_bn_relu_mask_bytes(c, p, nimg) == c * nimg * nw * 8
+    assert lib.msl_bn_uses_fused(c, p, 1, hip.forms()) == 1
+    outs = []
+    for use_bits in (False, True):
+        rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+        y = torch.empty_like(x)
+        sm, si = torch.empty(c * nimg, device=DEV), torch.empty(c * nimg, device=DEV)
+        fa, ba = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+        bits = torch.full((c * nimg * nw,), -1, dtype=torch.int64, device=DEV)
+        fargs = (x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), res.data_ptr(), y.data_ptr(), rm.data_ptr(),
+                 rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, nimg, 1, 1, 0.1, 1e-5, 1, hip.forms(),
+                 ws.data_ptr(), wsb, s, fa.data_ptr())
+        assert (lib.msl_bn_fwd_mask(*fargs, bits.data_ptr()) if use_bits else lib.msl_bn_fwd_am(*fargs)) == 0
+        dx, dres = torch.empty_like(x), torch.empty_like(x)
+        dg, db = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+        tail = (gamma.data_ptr(), beta.data_ptr(), sm.data_ptr(), si.data_ptr(), dx.data_ptr(), dres.data_ptr(),
+                dg.data_ptr(), db.data_ptr(), c, p, nimg, 1, 1, 0, hip.forms(), ws.data_ptr(), wsb, s, ba.data_ptr())
+        if use_bits:
+            assert lib.msl_bn_bwd_mask(gy.data_ptr(), x.data_ptr(), bits.data_ptr(), *tail) == 0
+        else:
+            assert lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), y.data_ptr(), *tail) == 0
+        torch.cuda.synchronize()
+        outs.append((y, sm, si, rm, rv, fa, dx, dres, dg, db, ba))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    y = outs[1][0]
+    assert 0.2 < (y == 0).float().mean().item() < 0.8  # the mask matters
+    pos = (y > 0).reshape(c * nimg, p).cpu().numpy()
+    pos = np.pad(pos, ((0, 0), (0, nw * 64 - p)))
+    want = np.packbits(pos, axis=-1, bitorder="little").view("<u8").reshape(-1)
+    assert np.array_equal(bits.cpu().numpy().view("<u8"), want)
+    # refusals: bits need relu and the fused kernels
+    args_norelu = list(fargs[:17]) + [0] + list(fargs[18:])
+    assert lib.msl_bn_fwd_mask(*args_norelu, bits.data_ptr()) == -3
+    prev = ops.set_bn_fused(False)
+    try:
+        assert lib.msl_bn_fwd_mask(*fargs, bits.data_ptr()) == -3
+        assert lib.msl_bn_bwd_mask(gy.data_ptr(), x.data_ptr(), bits.data_ptr(), *tail) == -3
+    finally:
+        ops.set_bn_fused(prev)
+
+
 # ---------------------------------------------------------------------------- stem / maxpool / stride 2
 @pytest.mark.parametrize("h,w", [(64, 128), (33, 47), (512, 1024)])
 def test_stem_conv_fwd_bwd(h, w, f32_form):
