@@ -15,7 +15,6 @@ extern "C" int probe_bd_fwd(const float* x, const float* packed, float* y, int c
   pl.G = 1;
   pl.bk = kCB;
   pl.kps = pl.ksteps;
-  if (ws_bytes < fwd_ws_bytes(pl, cout, P, cin, 9)) return MSL_ERR_WORKSPACE;
   FwdArgs a{};
   a.A = packed;
   a.B = x;
@@ -43,14 +42,16 @@ extern "C" int probe_bd_fwd(const float* x, const float* packed, float* y, int c
   sk.tiles_n = pl.tiles_n;
   sk.KS = pl.kps;
   const long long tiles = (long long)pl.tiles_m * pl.tiles_n;
-  sk.tdp = tiles >= kSkNW ? (int)(tiles / kSkNW * kSkNW) : 0;
+  const int nwk = kSkNW;
+  if (ws_bytes < (size_t)nwk * 2 * 128 * kSkBN * 4) return MSL_ERR_WORKSPACE;
+  sk.tdp = tiles >= nwk ? (int)(tiles / nwk * nwk) : 0;
   sk.gm = sk.tdp > 0 ? pl.tiles_m : 1;
   const long long T = (tiles - sk.tdp) * sk.KS;
-  sk.NW = (int)std::min<long long>(kSkNW, T);
+  sk.NW = (int)std::min<long long>(nwk, T);
   if (sk.tdp > 0) sk.NW = (int)std::max<long long>(1, std::min<long long>(sk.NW, T / 8));
   sk.T = (int)T;
   sk.prof = prof;
-  const dim3 grid(sk.tdp > 0 ? kSkNW : sk.NW), block(256);
+  const dim3 grid(sk.tdp > 0 ? nwk : sk.NW), block(256);
   // with_prof: 1 stamps; 2, 4, 8, 6, 14 timing-only ablations, 16 a BN-apply of the image operand
   // (dconv_kernels.h fwd_sk_body PROF)
 #define PROBE_CASE(V)                                                                                              \
@@ -67,6 +68,7 @@ extern "C" int probe_bd_fwd(const float* x, const float* packed, float* y, int c
     PROBE_CASE(8)
     PROBE_CASE(14)
     PROBE_CASE(16)
+
     default: return MSL_ERR_ARG;
   }
   MSL_CHECK_LAUNCH();

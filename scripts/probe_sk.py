@@ -23,7 +23,7 @@ wt = (torch.randn(cout, cin, 3, 3, generator=g) * 0.02).cuda()
 cache = ops.PackCache()
 packed = cache.get([wt], cin, cout, 0)
 xpart = ops._parts(x)
-wsb = lib.msl_dconv_fwd_workspace(1, cin, cout, h, w, nimg)
+wsb = max(lib.msl_dconv_fwd_workspace(1, cin, cout, h, w, nimg), 768 * 2 * 128 * 128 * 4 + 4096)
 ws = hip.workspace(wsb, "cuda")
 y_ref = torch.empty(1, cout, nimg, h, w, device="cuda")
 hip.check(lib.msl_dconv_fwd_sc(x.data_ptr(), packed.data_ptr(), None, y_ref.data_ptr(), 1, cin, cout, h, w, nimg, d, 0,
