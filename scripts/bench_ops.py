@@ -101,7 +101,8 @@ def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W, nimg=1):
 
 SHAPES = [("aspp6 2048->19", 2048, 19, 3, 6), ("layer1 3x3", 64, 64, 3, 1), ("layer3 3x3 d2", 256, 256, 3, 2), ("layer4 3x3 d4", 512, 512, 3, 4), ("layer2 3x3", 128, 128, 3, 1),
           ("1x1 256->1024", 256, 1024, 1, 0), ("1x1 1024->256", 1024, 256, 1, 0), ("1x1 2048->512", 2048, 512, 1, 0),
-          ("1x1 512->2048", 512, 2048, 1, 0), ("1x1 256->64", 256, 64, 1, 0), ("1x1 64->256", 64, 256, 1, 0)]
+          ("1x1 512->2048", 512, 2048, 1, 0), ("1x1 256->64", 256, 64, 1, 0), ("1x1 64->256", 64, 256, 1, 0),
+          ("aspp shift 2048->342", 2048, 342, 1, 0)]
 
 
 def main():
