@@ -48,6 +48,8 @@ class DilatedConv3x3(nn.Conv2d):
 # Bottleneck blocks with an identity residual let conv1's data-gradient GEMM sum in the residual's
 # gradient (ops.ResidualGrad) instead of autograd's separate add; False restores the add (tests).
 FUSE_RESIDUAL_GRAD = True
+# r05: a downsample block's conv1 also sums the downsample conv's data gradient (no accumulation kernel)
+FUSE_DOWNSAMPLE_GRAD = True
 
 
 class PointwiseConv(nn.Conv2d):
@@ -58,10 +60,10 @@ class PointwiseConv(nn.Conv2d):
         super().__init__(in_channels, out_channels, kernel_size=1, stride=stride, bias=False)
         self._pack = ops.PackCache(pointwise=True)
 
-    def forward(self, x, residual_grad=None, presampled=False):
+    def forward(self, x, residual_grad=None, presampled=False, grad_to=None):
         if self.stride[0] != 1 and not presampled:
             x = ops.subsample(x, self.stride[0])
-        return ops.pconv(x, self.weight, self._pack, residual_grad)
+        return ops.pconv(x, self.weight, self._pack, residual_grad, grad_to)
 
 
 class StemConv(nn.Conv2d):
@@ -107,18 +109,23 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         # identity residual: its gradient is summed into x's gradient by conv1's data-gradient
-        # GEMM (ops.ResidualGrad) rather than by autograd's accumulation kernel
-        fuse = FUSE_RESIDUAL_GRAD and self.downsample is None and torch.is_grad_enabled()
+        # GEMM (ops.ResidualGrad) rather than by autograd's accumulation kernel; r05: likewise the
+        # downsample conv's data gradient (both read xs)
+        fuse = (FUSE_RESIDUAL_GRAD and torch.is_grad_enabled() and
+                (self.downsample is None or FUSE_DOWNSAMPLE_GRAD))
         hold = ops.ResidualGrad() if fuse else None
         # a strided block (layer2.0): conv1 and the downsample read one shared x[:, :, ::s, ::s]
         xs = ops.subsample(x, self.stride) if self.stride != 1 else x
         out = ops.bn_act(self.bn1, self.conv1(xs, hold, presampled=True), relu=True)
         out = ops.bn_act(self.bn2, self.conv2(out), relu=True)
-        residual = x.detach() if fuse else x
         if self.downsample is not None:
-            residual = ops.bn_act(self.downsample[1], self.downsample[0](xs, presampled=True))
+            residual = ops.bn_act(self.downsample[1], self.downsample[0](xs, presampled=True, grad_to=hold))
+            hold_bn3 = None
+        else:
+            residual = x.detach() if fuse else x
+            hold_bn3 = hold
         # bn3 + residual add + ReLU in one kernel (deeplab_multi.py:38-46)
-        return ops.bn_act(self.bn3, self.conv3(out), residual=residual, relu=True, residual_grad=hold)
+        return ops.bn_act(self.bn3, self.conv3(out), residual=residual, relu=True, residual_grad=hold_bn3)
 
 
 class Classifier_Module(nn.Module):

@@ -603,7 +603,7 @@ class _PConv(Function):
     No library GEMM: every call is deterministic (fixed summation order)."""
 
     @staticmethod
-    def forward(ctx, x, weight, cache, hold=None):
+    def forward(ctx, x, weight, cache, hold=None, grad_to=None):
         x = _check_act(x, "pconv", images=True)
         cout, cin = weight.shape[0], weight.shape[1]
         if weight.shape[2:] != (1, 1) or x.size(1) != cin:
@@ -626,6 +626,7 @@ class _PConv(Function):
         ctx.meta = (cin, cout, p, cache, math)
         ctx.xpart = xpart
         ctx.hold = hold
+        ctx.grad_to = grad_to
         return y
 
     @staticmethod
@@ -641,6 +642,8 @@ class _PConv(Function):
         gpart = _parts(gy, math, compute=_split_gemm(cin, cout))
         if ctx.needs_input_grad[0]:
             acc = 0
+            if hold is not None:
+                hold.consumed = True
             if hold is not None and hold.g is not None:
                 dx, hold.g = hold.g, None
                 acc = 1
@@ -660,8 +663,13 @@ class _PConv(Function):
                 fn = lib.msl_pconv_dgrad_f16 if math == "fp16" else lib.msl_pconv_dgrad_acc_sc
                 hip.check(fn(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, acc, cnt,
                              ws.data_ptr(), wsb, s, *_pp(gpart)), "msl_pconv_dgrad")
+        # a downsample conv (r05): its data gradient goes to the ResidualGrad that the block's conv1 sums
+        # into its own (msl_pconv_dgrad_acc) - unless conv1's backward already ran, then autograd adds it
+        to = ctx.grad_to
+        if dx is not None and to is not None and not to.consumed:
+            to.g, dx = dx, None
         if not ctx.needs_input_grad[1]:
-            return dx, None, None, None
+            return dx, None, None, None, None
         sink = grad_sink(weight)
         dst = sink[0] if sink is not None else torch.empty_like(weight)
         wsb = lib.msl_pconv_wgrad_workspace(cin, cout, p)
@@ -674,16 +682,18 @@ class _PConv(Function):
         if side is not None:
             _keep(side, x, gy, *(q[0] for q in (ctx.xpart, gpart) if q is not None))
         if sink is None:
-            return dx, dst, None, None
+            return dx, dst, None, None, None
         sink[1].notify(sink[2])
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
-def pconv(x, weight, cache, residual_grad=None):
+def pconv(x, weight, cache, residual_grad=None, grad_to=None):
     """1x1, stride-1, bias-free conv (Bottleneck.conv1/conv3, downsample: deeplab_multi.py:13,20,96-99).
-    `residual_grad` (a ResidualGrad also given to the block's bn_act): its gradient is added into
-    this conv's input gradient by the data-gradient GEMM."""
-    return _PConv.apply(x, weight, cache, residual_grad)
+    `residual_grad` (a ResidualGrad also given to the block's bn_act or downsample conv): its gradient
+    is added into this conv's input gradient by the data-gradient GEMM.  `grad_to` (the downsample
+    conv of a block, r05): this conv's input gradient is handed to that ResidualGrad instead of to
+    autograd, so the block's conv1 sums it (no separate accumulation kernel)."""
+    return _PConv.apply(x, weight, cache, residual_grad, grad_to)
 
 
 conv1x1 = pconv
@@ -696,10 +706,11 @@ class ResidualGrad:
     gradient GEMM (msl_pconv_dgrad_acc) instead of autograd's separate accumulation kernel
     (deeplab_multi.py:31-48: x feeds conv1 and the residual)."""
 
-    __slots__ = ("g",)
+    __slots__ = ("g", "consumed")
 
     def __init__(self):
         self.g = None
+        self.consumed = False  # the summing conv's backward ran (a later producer hands to autograd)
 
 
 # --------------------------------------------------------------------------- stem, maxpool, stride-2 glue

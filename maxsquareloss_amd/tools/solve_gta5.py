@@ -314,6 +314,9 @@ def add_UDA_train_args(arg_parser):
     a("--graph", type=str2bool, default=False,
       help="replay each iteration after the first as one captured hipGraph (single process; not in the "
            "reference, whose loop is eager)")
+    a("--dp_exchange", type=str2bool, default=False,
+      help="run the data-parallel gradient exchange (RCCL process group + GradReducer) even at one rank, "
+           "where the all-reduce is the identity: the multi-GPU code path on one GPU (not in the reference)")
     return arg_parser
 
 

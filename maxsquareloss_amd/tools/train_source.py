@@ -63,7 +63,8 @@ class Trainer:
             raise RuntimeError("the MI355X trainer needs a GPU (no CPU fallback)")
         torch.cuda.set_device(self.local_rank)
         self.device = torch.device("cuda", self.local_rank)
-        if self.world > 1 and not dist.is_initialized():
+        dp = self.world > 1 or bool(getattr(args, "dp_exchange", False))
+        if dp and not dist.is_initialized():
             dist.init_process_group("nccl", device_id=self.device)
         self.train_id = train_id
         self.logger = logger or logging.getLogger(__name__)
@@ -85,7 +86,7 @@ class Trainer:
             raise NotImplementedError("only --optim SGD (the reference default) is on the MI355X path")
         self.optimizer = SGD(lr=self.args.lr, params=self.params, momentum=self.args.momentum,
                              weight_decay=self.args.weight_decay)
-        self.reducer = GradReducer(self.optimizer) if self.world > 1 else None
+        self.reducer = GradReducer(self.optimizer, always=self.world == 1) if dp else None
         self.packer = ops.PackBatch(self.model)  # every weight pack of a step in two launches
 
         h, w = self.args.crop_size[1], self.args.crop_size[0]

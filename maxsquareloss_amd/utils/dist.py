@@ -40,11 +40,13 @@ import torch.distributed as dist
 
 
 class GradReducer:
-    def __init__(self, optimizer, bucket_cap_mb=25.0, process_group=None):
+    def __init__(self, optimizer, bucket_cap_mb=25.0, process_group=None, always=False):
         self.opt = optimizer
         self.flat = optimizer.grads
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # always: launch the collectives at one rank too (--dp_exchange: the RCCL path on one GPU)
+        self.always = bool(always) and dist.is_initialized()
         self.cap = int(bucket_cap_mb * 1024 * 1024 / 4)
         self.set_breaks([])
         self.live = None        # bool mask of parameters that receive gradients
@@ -79,7 +81,7 @@ class GradReducer:
 
     def _launch(self, b):
         a, e = self._elem_range(b)
-        if self.world > 1:
+        if self.world > 1 or self.always:
             from .. import ops
             ops.wgrad_join(self.flat.flat.device)  # the bucket's weight gradients may be on the side stream
             self.works.append(dist.all_reduce(self.flat.flat[a:e], group=self.pg, async_op=True))

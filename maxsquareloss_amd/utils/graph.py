@@ -25,6 +25,7 @@ segment 1, launches the exchange of the gradients it finished on RCCL's stream, 
 meanwhile, launches the rest and joins it, then replays the update.  Those captures use the
 thread-local capture mode, so RCCL's / gloo's own threads may keep calling the HIP runtime meanwhile.
 """
+import gc
 import torch
 
 
@@ -112,6 +113,12 @@ class GraphedStep:
         owners = [self.tr] + [m for m in vars(self.tr).values() if isinstance(m, torch.nn.Module)]
         before = [{k: v for k, v in vars(o).items() if isinstance(v, torch.Tensor)} for o in owners]
         mode = "thread_local" if dp else "global"
+        # no Python garbage collection while a stream captures: a collected CUDA graph or event of an
+        # earlier trainer (reference cycles) would call the runtime from its destructor, which a capturing
+        # stream forbids (hipErrorStreamCaptureUnsupported, an abort; found on RCCL, r05).  torch.cuda.graph
+        # collects once on entry.
+        gc_was = gc.isenabled()
+        gc.disable()
         try:
             if dp:
                 red.deferred = True
@@ -129,6 +136,8 @@ class GraphedStep:
                 with torch.cuda.graph(self.graph_update, stream=s, capture_error_mode=mode):
                     self.update()
         finally:
+            if gc_was:
+                gc.enable()
             opt.lr_dev = None  # eager steps outside the graph keep passing the rates by value
             if dp:
                 red.deferred = False

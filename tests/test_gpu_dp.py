@@ -15,8 +15,10 @@ Every kernel of the step is deterministic (no library kernel since r03), so the
 exchange is checked exactly: each bucket against the launch-time snapshots of both
 ranks' local gradients.
 """
+import gc
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -274,6 +276,97 @@ def test_graphed_dp_step_matches_eager_dp():
         assert np.array_equal(pe, pg), (r, int((pe != pg).sum()))
     for graph in (False, True):
         assert np.array_equal(got[0][graph][1], got[1][graph][1]), graph
+
+
+def _rccl_worker(port, q):
+    """One rank on the GPU with an RCCL ("nccl") process group and the exchange forced on (--dp_exchange)
+    against the same run without a process group: the captured, segmented DP step on the real collective
+    library (the all-reduce at one rank is the identity)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+        import torch.distributed as dist
+        from maxsquareloss_amd.tools.solve_gta5 import UDATrainer, build_parser
+        from maxsquareloss_amd.tools.train_source import init_args
+        from maxsquareloss_amd.utils.synthetic import synthetic_image, synthetic_labels
+        out, log = {}, []
+
+        def mark(m):
+            print(f"[rccl worker] {m}", file=sys.stderr, flush=True)
+
+        for dp in (False, True):
+            mark(f"trainer dp={dp}")
+            argv = ["--crop_size", f"{W},{H}", "--target_crop_size", f"{W},{H}", "--imagenet_pretrained", "False",
+                    "--save_dir", "", "--target_mode", "IW_maxsquare", "--multi", "True", "--lambda_target", "0.09",
+                    "--iter_max", "1000", "--graph", "True", "--dp_exchange", str(dp)]
+            args, _, _ = init_args(build_parser().parse_args(argv))
+            tr = UDATrainer(args, cuda=True)
+            mark("trainer built")
+            assert (tr.reducer is not None) == dp and dist.is_initialized() == dp
+            if dp:
+                assert dist.get_backend() == "nccl" and tr.reducer.always
+            losses = []
+            for it in range(4):
+                if dp and it == 3:
+                    red = tr.reducer
+                    red._launch = (lambda f: lambda b: (log.append(b), f(b))[1])(red._launch)
+                    works = []
+                    import torch.distributed as d2
+                    orig = d2.all_reduce
+                    d2.all_reduce = lambda *a, **k: works.append(1) or orig(*a, **k)
+                tr.uda_step(synthetic_image(H, W, it).cuda(), synthetic_labels(H, W, 19, it).cuda(),
+                            synthetic_image(H, W, 500 + it).cuda())
+                torch.cuda.synchronize()
+                mark(f"iteration {it} done")
+                if dp and it == 3:
+                    d2.all_reduce = orig
+                    assert len(works) == len(log) > 0, (len(works), log)
+                losses.append((tr.loss_val.item(), tr.loss_target.item(), tr.loss_target_2.item()))
+            if dp:
+                assert tr._graphed is not None and len(tr._graphed.graphs) == 1 + len(tr.model.split_segments())
+                assert log == [b for b in range(len(tr.reducer.bounds)) if tr.reducer.has_live[b]], log
+            out[dp] = (losses, torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).cpu().numpy())
+            del tr
+            gc.collect()
+        dist.destroy_process_group()
+        q.put(("ok", out))
+    except Exception as e:
+        import traceback
+        q.put(("error", traceback.format_exc() + repr(e)))
+        raise
+
+
+def test_rccl_world1_graphed_dp_matches_single_gpu():
+    """RCCL on the hardware (r05): the segmented, graph-captured DP step with a real "nccl" (RCCL)
+    process group at one rank (--dp_exchange: every live bucket all-reduced between the segment replays,
+    counted) gives the same losses and parameters bit for bit as the single-GPU step without a process
+    group, over 4 UDA iterations.  (Two ranks need two GPUs for RCCL; the 2-rank exchange itself is
+    tested on gloo above.)"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        import queue
+        import time
+        deadline = time.time() + 300
+        while True:  # a worker that dies (an abort in the runtime) fails the test instead of hanging it
+            try:
+                status, got = q.get(timeout=5)
+                break
+            except queue.Empty:
+                assert p.is_alive(), f"RCCL worker died, exit code {p.exitcode}"
+                assert time.time() < deadline, "RCCL worker timed out"
+        assert status == "ok", got
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    finally:
+        if p.is_alive():
+            p.kill()
+            p.join(timeout=10)
+    (l0, p0), (l1, p1) = got[False], got[True]
+    assert l0 == l1, (l0, l1)
+    assert np.array_equal(p0, p1), int((p0 != p1).sum())
 
 
 def _cfg2_worker(rank, world, port, q, outdir):

@@ -673,14 +673,26 @@ def test_pconv_dgrad_accumulate(cin, cout, h, w, f32_form):
     assert _rel(dx, ref) < 1e-5
 
 
-def test_bottleneck_fused_residual_grad(f32_form, monkeypatch):
+@pytest.mark.parametrize("kind", ["identity", "downsample", "downsample_s2"])
+def test_bottleneck_fused_residual_grad(f32_form, monkeypatch, kind):
     """Bottleneck with an identity residual: the residual's gradient summed into x's gradient by
-    conv1's data-gradient GEMM (ops.ResidualGrad) equals autograd's separate accumulation."""
+    conv1's data-gradient GEMM (ops.ResidualGrad) equals autograd's separate accumulation; r05: likewise
+    a block with a downsample conv (layer1.0 / layer3.0, and layer2.0's stride 2), whose data gradient
+    conv1's GEMM sums instead of autograd."""
+    from torch import nn
     from maxsquareloss_amd.graphs.models import deeplab_multi as dm
     torch.manual_seed(3)
-    blk = dm.Bottleneck(1024, 256, dilation=2).to(DEV).train()
-    x = (torch.randn(1, 1024, 17, 33) * 2).to(DEV)
-    gy = torch.randn(1, 1024, 17, 33).to(DEV)
+    if kind == "identity":
+        blk, cin, cout, hw, ho = dm.Bottleneck(1024, 256, dilation=2), 1024, 1024, (17, 33), (17, 33)
+    else:
+        s = 2 if kind == "downsample_s2" else 1
+        ds = nn.Sequential(dm.conv1x1(512, 1024, s), nn.BatchNorm2d(1024, affine=dm.affine_par))
+        blk, cin, cout = dm.Bottleneck(512, 256, stride=s, dilation=1, downsample=ds), 512, 1024
+        hw = (33, 65) if s == 2 else (17, 33)
+        ho = ((hw[0] + 1) // 2, (hw[1] + 1) // 2) if s == 2 else hw
+    blk = blk.to(DEV).train()
+    x = (torch.randn(1, cin, *hw) * 2).to(DEV)
+    gy = torch.randn(1, cout, *ho).to(DEV)
     out = {}
     for fused in (True, False):
         monkeypatch.setattr(dm, "FUSE_RESIDUAL_GRAD", fused)
