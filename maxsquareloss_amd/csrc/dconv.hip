@@ -400,7 +400,8 @@ static WgradPlan plan_wgrad(int nbranch, int taps, int cin, int cout, int P, boo
 }
 
 static size_t wgrad_piece_bytes(const WgradPlan& pl) { return (size_t)pl.nw * pl.slots * pl.bm * pl.bn * sizeof(float); }
-static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)pl.KS * 6 * pl.lda * 16 : 0; }
+// (+ two K-steps: k_wgrad_x6's loads one stage ahead read up to K-step KS + 1, unused)
+static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)(pl.KS + 2) * 6 * pl.lda * 16 : 0; }
 
 // stream-K workspace: the published pieces, NW x 2 x BM*BN floats (summed by k_sk_reduce; no
 // flags or other state survive a call).

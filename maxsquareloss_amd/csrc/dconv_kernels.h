@@ -1030,10 +1030,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     float bdq[4][8];  // BD: the register ring of B values (K-step i in slot i % 4)
     float bdv[4];     // PROF & 16: the ring's pixel validity (+inf / 0) and channel blocks
     int bdc[4];
-    auto issue = [&](int s, int slot, float (&bq)[8], float& bv, int& bc) {
+    // part 1: stage s's A pieces into LDS slot `slot`; part 2: its B operand (ring entry bq, or LDS),
+    // advancing the cursor; 3: both
+    auto issue = [&](int s, int slot, float (&bq)[8], float& bv, int& bc, int part = 3) {
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
-      if constexpr (AHALF) {
+      if (!(part & 1)) {
+      } else if constexpr (AHALF) {
         // piece wid / 2 (= the k half of plane 0), rows 32 * (wid & 1) .. +31: the lanes of that half
         const int qh = wid >> 1;
         if ((lane >> 5) == (wid & 1))
@@ -1058,7 +1061,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         }
       }
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
+      for (int g = 0; g < G && (part & 2); ++g) {
         const int cb16 = c_cb * kCB;
         if constexpr (BP) {
           // the pre-split planes: 16 B per plane of this lane's pixel (hi, then lo)
@@ -1142,8 +1145,10 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // complete in every wave's LDS pieces, and every wave has read slot i - 1's fragments, at step
       // i - 2), issue stage i + 3 into that slot and ring entry, read + split K-step i + 1's fragments,
       // and issue K-step i's MFMAs from the fragments read the step before
-      // K-step i: wait until its A pieces landed, barrier (the A slot refilled next was read by every
-      // wave at i - 1), issue K-step i + 3 into the ring entry and slot K-step i - 1 freed, compute.
+      // K-step i: wait until its A pieces landed, issue K-step i + 3's B loads into the ring entry
+      // K-step i - 1 freed, barrier (the A slot refilled next was read by every wave at i - 1), compute
+      // with K-step i + 3's A pieces issued into that slot after the MFMAs (r05: B ahead of the barrier,
+      // -17 us on the ASPP classifier's forward, profiles/r05_bd_bsplit_ab.txt).
       // The count leaves only the two younger stages' LDS-DMA pieces in flight, not their B loads:
       // an LDS-DMA may land after register loads issued behind it (r04: with the B loads counted too -
       // vmcnt(2 * INST_W) - a wave now and then read a stage's A slot before another wave's DMA piece
@@ -1154,10 +1159,15 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         if constexpr (PROF & 1) t0 = sk_stamp();
         wait_vmcnt<2 * A_INST_W>();
         if constexpr (PROF & 1) t1 = sk_stamp();
+        // K-step i + 3's B loads right after the wait (their ring entry was read by this wave at i - 1;
+        // no other wave is involved), before the barrier: the wait at i + 1 forces all but its four
+        // youngest loads, so what it forces was issued a whole K-step earlier rather than after this
+        // step's MFMAs.  The A pieces still go after the barrier (their LDS slot is shared).
+        issue(k_a + i + STAGES - 1, 0, nxt, nxtv, nxtc, 2);
         if constexpr (!(PROF & 8)) __builtin_amdgcn_s_barrier();
         if constexpr (PROF & 1) t2 = sk_stamp();
         const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
-        auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt, nxtv, nxtc); };
+        auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt, nxtv, nxtc, 1); };
         if constexpr (BP) {
           mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
         } else if constexpr ((PROF & 16) != 0) {
@@ -2150,6 +2160,9 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
     // leaves the younger loads in flight: A for the next K-step and the next stage's B stay in
     // flight during the MFMAs.  (With the loads conditional, the compiler drained the queue -
     // vmcnt(0) - before every stage's first MFMA, waiting for the B loads just issued, r04.)
+    // (r05: A a whole stage ahead in two more register sets was slower - 236 VGPRs, layer4 +15 us.)
+    // The prefetch past a tile's last K-step reads up to two K-steps beyond the planes (the K-step
+    // rides in the soffset, outside the range check): wgrad_planes_bytes reserves them.
     int ks = k_a;  // the K-step computed next
     for (int s = 0; 2 * s < nst; ++s) {
       const char* Bs = smem + (s & 1) * STAGEB;
