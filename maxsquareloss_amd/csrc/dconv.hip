@@ -414,11 +414,14 @@ static size_t fwd_piece_bytes(const FwdPlan& pl) {
 }
 static size_t img_planes_bytes(int cimg, int P) { return align_up((size_t)cdiv(cimg, kCB) * kCB * P * 4, 256); }
 // The f16x3 / fp16 forward-form GEMMs that read their image operand pre-split (k_split_img, BP form):
-// the 3x3 ones with M >= 512 (profiles/r03_bp_ab.txt)
-static bool bp_form(int taps, int M, bool small_f16) { return taps == 9 && M >= 512 && !small_f16; }
+// the 3x3 ones with M >= 512 (profiles/r03_bp_ab.txt); fp16 math (one plane: a quarter of the loads'
+// instructions, half their bytes) from M >= 128 (r05)
+static bool bp_form(int taps, int M, bool small_f16, bool h1 = false) {
+  return taps == 9 && !small_f16 && (M >= 512 || (h1 && M >= 128));
+}
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P, int cimg, int taps) {
   // the planes only where the BP form can run (the stem / pointwise calls reserved them too)
-  if (pl.sk) return fwd_piece_bytes(pl) + (bp_form(taps, M, false) ? img_planes_bytes(cimg, P) : 0) + kPartBytes;
+  if (pl.sk) return fwd_piece_bytes(pl) + (bp_form(taps, M, false, true) ? img_planes_bytes(cimg, P) : 0) + kPartBytes;
   return (pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0) + kPartBytes;
 }
 static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials block from the end
@@ -606,7 +609,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // the layer4 3x3 GEMMs (M = 512: the split pass is shared by 4 row blocks and 9 taps), fwd
         // 162 vs 174 us, dgrad 172 vs 185; loses where the pass is a large share (pointwise 39 vs
         // 31 us, layer2 34 vs 31, ASPP 144 vs 135) - profiles/r03_bp_ab.txt
-        const bool bp = bp_form(taps, M, small_f16);
+        const bool bp = bp_form(taps, M, small_f16, MT == kMathH1P);
         if (bp) {
           f16x8* planes = reinterpret_cast<f16x8*>((char*)ws + fwd_piece_bytes(pl));
           const long long n = (long long)a.ncb * 2 * P;
