@@ -423,7 +423,8 @@ int msl_bn_bwd(const float* dy, const float* x, const float* y, const float* gam
  * (backward; dx required): the per-channel absmax partials (c of them) that the f16x3 conv
  * entry points (_sc) take for the tensor this BN produced - the next conv's input, or the
  * gradient of the conv before it - so those GEMMs need no absmax pass of their own.  The fused
- * kernels reduce it in registers; the split forms add one pass over the output. */
+ * kernels reduce it in registers, the split forms in their apply kernel (r05; before: a pass of its
+ * own over the output). */
 int msl_bn_fwd_am(const float* x, const float* gamma, const float* beta, const float* residual,
                   float* y, float* running_mean, float* running_var, long long* num_batches_tracked,
                   float* save_mean, float* save_invstd, int c, int p, int nimg, int training,
@@ -444,8 +445,8 @@ int msl_bn_bwd_am_beta(const float* dy, const float* x, const float* y, const fl
                        float* dres, float* dgamma, float* dbeta, int c, int p, int nimg, int training,
                        int relu, int accumulate_params, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream,
                        float* absmax_dx);
-/* 1 if msl_bn_fwd / msl_bn_bwd run the fused one-block-per-channel kernels for this shape (their
- * _am absmax output is then free; the split forms add a pass over the output). */
+/* 1 if msl_bn_fwd / msl_bn_bwd run the fused one-block-per-channel kernels for this shape (else the
+ * split stats / reduce + flat apply kernels). */
 int msl_bn_uses_fused(int c, int p, int training, const msl_forms* forms);
 /* The ReLU mask as bits (r05): msl_bn_fwd_mask is msl_bn_fwd_am that also writes y > 0 of every
  * pixel to relu_mask (bit e % 64 of word [row][e / 64], rows c * nimg + image, cdiv(p, 64) words per

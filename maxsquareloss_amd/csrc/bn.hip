@@ -60,11 +60,14 @@ __device__ __forceinline__ void visit_range(long long e0, long long e1, F4&& f4,
   for (long long e = a1 + threadIdx.x; e < e1; e += 256) f1(e);
 }
 
+// zero_am (the flat apply's absmax output, or null): zeroed here, one launch ahead of its atomicMax
 template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_stats(const float* __restrict__ x, int P, int S,
-                                                   double* __restrict__ part) {
+                                                   double* __restrict__ part, float* __restrict__ zero_am = nullptr,
+                                                   int NI = 1) {
   __shared__ double red[8];
   const int c = blockIdx.x, s = blockIdx.y;
+  if (zero_am && s == 0 && threadIdx.x == 0 && c % NI == 0) zero_am[c / NI] = 0.f;
   const long long base = (long long)c * P;
   const double shift = (double)x[base];
   const int chunk = cdiv(P, S);
@@ -143,6 +146,27 @@ __device__ __forceinline__ void bn_running_update(const BnArgs& a, int c, float 
   a.running_var[c] = running_blend(a.running_var[c], m, unbiased);
 }
 
+// The flat apply kernels' absmax output (r05): each thread keeps the max |v| of the row it is in (its
+// elements come in increasing order, so the row only advances) and folds it into the block's per-row
+// LDS maxima when the row changes; the block then folds those into absmax[channel] with an integer
+// atomicMax on the float bits (|v| >= 0 orders as its bits; zeroed by the launch before).  Replaces a
+// pass of its own over the output (absmax_rows) for the next conv's f16x3 / fp16 operand scale.
+struct RowMax {
+  int k = -1;
+  float m = 0.f;
+  __device__ __forceinline__ void add(unsigned* lds, int row, float v) {
+    if (row != k) {
+      flush(lds);
+      k = row;
+      m = 0.f;
+    }
+    m = fmaxf(m, fabsf(v));
+  }
+  __device__ __forceinline__ void flush(unsigned* lds) {
+    if (k >= 0) atomicMax(lds + k, __float_as_uint(m));
+  }
+};
+
 // Flat apply: block b covers elements [b*chunk, (b+1)*chunk) of the [C*NI][P] tensor (possibly
 // several rows).  Each block derives the (alpha, beta') of the rows it touches from the fp64
 // partial sums; the block holding a row's first element also publishes its saved statistics, and
@@ -150,12 +174,14 @@ __device__ __forceinline__ void bn_running_update(const BnArgs& a, int c, float 
 template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_apply(BnArgs a) {
   __shared__ float coef[2][256];
+  __shared__ unsigned rmax[256];
   const long long N = (long long)a.C * a.NI * a.P;
   const long long start = (long long)blockIdx.x * a.chunk;
   const long long end = min(N, start + a.chunk);
   const int c0 = (int)(start / a.P);
   const int nch = (int)((end - 1) / a.P) - c0 + 1;
   if ((int)threadIdx.x < nch) {
+    rmax[threadIdx.x] = 0u;
     const int r = c0 + threadIdx.x;  // row = (channel, image)
     const int c = r / a.NI;
     const bool owner = (long long)r * a.P >= start;  // this block holds the row's first element
@@ -187,12 +213,15 @@ __global__ void __launch_bounds__(256) k_bn_apply(BnArgs a) {
   }
   __syncthreads();
   const long long cbound = (long long)(c0 + 1) * a.P;  // first element of channel c0+1
+  RowMax rm;
   auto one = [&](long long e, float xv, float rv) {
     int k = 0;
     if (e >= cbound) k = (int)(e / a.P) - c0;
     float v = xv * coef[0][k] + coef[1][k];
     v += rv;
-    return a.relu ? fmaxf(v, 0.f) : v;
+    v = a.relu ? fmaxf(v, 0.f) : v;
+    if (a.absmax) rm.add(rmax, k, v);
+    return v;
   };
   visit_range<VEC>(
       start, end,
@@ -209,6 +238,11 @@ __global__ void __launch_bounds__(256) k_bn_apply(BnArgs a) {
         reinterpret_cast<float4*>(a.y)[i] = o;
       },
       [&](long long e) { a.y[e] = one(e, a.x[e], a.residual ? a.residual[e] : 0.f); });
+  if (a.absmax) {
+    rm.flush(rmax);
+    __syncthreads();
+    if ((int)threadIdx.x < nch) atomicMax(reinterpret_cast<unsigned*>(a.absmax) + (c0 + threadIdx.x) / a.NI, rmax[threadIdx.x]);
+  }
 }
 
 struct BnBwdArgs {
@@ -233,6 +267,8 @@ template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_bwd_reduce(BnBwdArgs a) {
   __shared__ double red[8];
   const int c = blockIdx.x, s = blockIdx.y;
+  // (c: the row; the apply launch after this one folds max |dx| into absmax[row / NI])
+  if (a.absmax && s == 0 && threadIdx.x == 0 && c % a.NI == 0) a.absmax[c / a.NI] = 0.f;
   const long long base = (long long)c * a.P;
   const float mean = a.save_mean[c], invstd = a.save_invstd[c];
   const int chunk = cdiv(a.P, a.S);
@@ -264,6 +300,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(BnBwdArgs a) {
 template <bool VEC>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
   __shared__ float coef[5][256];
+  __shared__ unsigned rmax[256];
   const long long N = (long long)a.C * a.NI * a.P;
   const long long start = (long long)blockIdx.x * a.chunk;
   const long long end = min(N, start + a.chunk);
@@ -277,6 +314,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
     }
   };
   if ((int)threadIdx.x < nch) {
+    rmax[threadIdx.x] = 0u;
     const int r = c0 + threadIdx.x;  // row = (channel, image)
     const int c = r / a.NI;
     double sg, sgx;
@@ -305,6 +343,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
   }
   __syncthreads();
   const long long cbound = (long long)(c0 + 1) * a.P;
+  RowMax rm;
   // returns the masked upstream gradient g; dx through the reference's formula
   auto one = [&](long long e, float g, float yv, float xv, float& dxv) {
     int k = 0;
@@ -312,6 +351,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
     if (a.relu && !(yv > 0.f)) g = 0.f;
     const float xh = (xv - coef[3][k]) * coef[4][k];
     dxv = (g - coef[1][k] - xh * coef[2][k]) * coef[0][k];
+    if (a.absmax) rm.add(rmax, k, dxv);
     return g;
   };
   visit_range<VEC>(
@@ -336,6 +376,11 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(BnBwdArgs a) {
         if (a.dres) a.dres[e] = gm;
         if (a.dx) a.dx[e] = d;
       });
+  if (a.absmax) {
+    rm.flush(rmax);
+    __syncthreads();
+    if ((int)threadIdx.x < nch) atomicMax(reinterpret_cast<unsigned*>(a.absmax) + (c0 + threadIdx.x) / a.NI, rmax[threadIdx.x]);
+  }
 }
 
 // ---------------------------------------------------------------- fused one-block-per-channel form
@@ -698,9 +743,12 @@ int msl_bn_fwd_mask(const float* x, const float* gamma, const float* beta, const
   if (relu_mask && !(fused && relu)) return MSL_ERR_ARG;  // the bits come from the fused kernels
   if (training && !fused) {
     if (vec)
-      hipLaunchKernelGGL(k_bn_stats<true>, dim3(R, S), dim3(256), 0, st, x, p, S, part);
+      hipLaunchKernelGGL(k_bn_stats<true>, dim3(R, S), dim3(256), 0, st, x, p, S, part, absmax, nimg);
     else
-      hipLaunchKernelGGL(k_bn_stats<false>, dim3(R, S), dim3(256), 0, st, x, p, S, part);
+      hipLaunchKernelGGL(k_bn_stats<false>, dim3(R, S), dim3(256), 0, st, x, p, S, part, absmax, nimg);
+    MSL_CHECK_LAUNCH();
+  } else if (!fused && absmax) {
+    hipLaunchKernelGGL(k_zero_rows, dim3(cdiv(c, 256)), dim3(256), 0, st, absmax, c);
     MSL_CHECK_LAUNCH();
   }
   BnArgs a;
@@ -733,8 +781,7 @@ int msl_bn_fwd_mask(const float* x, const float* gamma, const float* beta, const
     hipLaunchKernelGGL(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(k_bn_apply<false>, dim3(blocks), dim3(256), 0, st, a);
-  MSL_CHECK_LAUNCH();
-  if (absmax) return absmax_rows(y, c, nimg * p, absmax, st);  // the split forms: a pass of its own over y
+  MSL_CHECK_LAUNCH();  // (absmax: folded in by k_bn_apply, zeroed by the launch before)
   return MSL_OK;
 }
 
@@ -807,8 +854,7 @@ static int bn_bwd(const float* dy, const float* x, const float* y, const uint64_
     MSL_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_bn_bwd_apply<false>, dim3(blocks), dim3(256), 0, st, a);
   }
-  MSL_CHECK_LAUNCH();
-  if (absmax_dx) return absmax_rows(dx, c, nimg * p, absmax_dx, st);  // the split forms: a pass over dx
+  MSL_CHECK_LAUNCH();  // (absmax_dx: folded in by k_bn_bwd_apply, zeroed by k_bn_bwd_reduce)
   return MSL_OK;
 }
 

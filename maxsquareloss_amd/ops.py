@@ -1199,11 +1199,11 @@ class _BNAct(Function):
         wsb = lib.msl_bn_workspace(c, p, n)
         ws = hip.workspace(wsb, x.device)
         update = bool(training) and running_mean is not None
-        # f16x3: the per-channel absmax of y for the convs that read it (their operand scales), where
-        # the fused kernel has it in registers; after a split-form BN (stem, 64-channel layer1) a
-        # conv that needs it reduces it itself (its first consumer is often an exact-f32 GEMM)
+        # f16x3 / fp16: the per-channel absmax of y for the convs that read it (their operand scales):
+        # from registers in the fused kernel, folded into the flat apply otherwise (r05: the big layer1
+        # maps of configs 4 / 5 no longer pay a pass of their own)
         fused = bool(lib.msl_bn_uses_fused(c, p, int(bool(training)), hip.forms()))
-        am = torch.empty(c, dtype=_f32, device=x.device) if (_h3(CONV_MATH) and fused) else None
+        am = torch.empty(c, dtype=_f32, device=x.device) if _h3(CONV_MATH) else None
         # r05: a residual BN + ReLU under the fused kernels writes the ReLU mask as bits (msl_bn_fwd_mask),
         # so its backward reads 1 bit per pixel instead of y (msl_bn_bwd_mask)
         bits = None
@@ -1247,9 +1247,8 @@ class _BNAct(Function):
             dbeta = torch.empty(c, dtype=_f32, device=x.device) if nig[2] else None
         wsb = lib.msl_bn_workspace(c, p, n)
         ws = hip.workspace(wsb, x.device)
-        # f16x3: the per-channel absmax of dx, the gradient the conv before this BN reads twice
-        am = torch.empty(c, dtype=_f32, device=x.device) if (
-            dx is not None and _h3(CONV_MATH) and lib.msl_bn_uses_fused(c, p, int(training), hip.forms())) else None
+        # f16x3 / fp16: the per-channel absmax of dx, the gradient the conv before this BN reads twice
+        am = torch.empty(c, dtype=_f32, device=x.device) if (dx is not None and _h3(CONV_MATH)) else None
         if ctx.bits is not None:
             st = lib.msl_bn_bwd_mask(gy.data_ptr(), x.data_ptr(), ctx.bits.data_ptr(), hip.ptr(weight),
                                      hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(), hip.ptr(dx),

@@ -928,6 +928,45 @@ def test_bn_absmax_outputs(c, h, w, res, relu, fused):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("training", [1, 0])
+@pytest.mark.parametrize("c,h,w,nimg", [(64, 161, 321, 2), (256, 33, 65, 2), (3, 7, 5, 3)])
+def test_bn_absmax_split_forms_images(c, h, w, nimg, training):
+    """The split BN kernels' absmax (r05: folded into the flat apply kernels, zeroed by the stats /
+    reduce launch or, in eval mode, by a zeroing launch): max |y| / |dx| over every image of the
+    channel ([C][NI][P]), blocks that cross rows and channels included, exactly; stale values in the
+    output buffer are overwritten."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    prev = ops.set_bn_fused(False)
+    try:
+        g = torch.Generator().manual_seed(c + h + nimg)
+        p = h * w
+        x = (torch.randn(c, nimg, p, generator=g) * 3 + 1).to(DEV)
+        gamma = (torch.rand(c, generator=g) + 0.5).to(DEV)
+        beta = torch.randn(c, generator=g).to(DEV)
+        gy = torch.randn(c, nimg, p, generator=g).to(DEV)
+        wsb = lib.msl_bn_workspace(c, p, nimg)
+        ws = hip.workspace(wsb, x.device)
+        s = hip.stream_ptr()
+        rm, rv = torch.randn(c, generator=g).to(DEV), (torch.rand(c, generator=g) + 0.5).to(DEV)
+        y, sm, si = torch.empty_like(x), torch.empty(c * nimg, device=DEV), torch.empty(c * nimg, device=DEV)
+        dx = torch.empty_like(x)
+        dg, db = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+        fa, ba = torch.full((c,), 1e30, device=DEV), torch.full((c,), 1e30, device=DEV)  # stale
+        assert lib.msl_bn_fwd_am(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), None, y.data_ptr(), rm.data_ptr(),
+                                 rv.data_ptr(), None, sm.data_ptr(), si.data_ptr(), c, p, nimg, training, 0, 0.1,
+                                 1e-5, 0, hip.forms(), ws.data_ptr(), wsb, s, fa.data_ptr()) == 0
+        assert lib.msl_bn_bwd_am(gy.data_ptr(), x.data_ptr(), y.data_ptr(), gamma.data_ptr(), sm.data_ptr(),
+                                 si.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(), c, p, nimg,
+                                 training, 0, 0, hip.forms(), ws.data_ptr(), wsb, s, ba.data_ptr()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(fa, y.abs().reshape(c, -1).amax(dim=1))
+        assert torch.equal(ba, dx.abs().reshape(c, -1).amax(dim=1))
+    finally:
+        ops.set_bn_fused(prev)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("c,h,w,nimg", [(256, 65, 129, 2), (512, 65, 129, 1), (128, 33, 65, 2), (2048, 17, 33, 2)])
 def test_bn_bwd_relu_mask_recompute(c, h, w, nimg):
     """msl_bn_bwd_am_beta with y = NULL (the fused kernel recomputes the ReLU mask from x, beta and the
