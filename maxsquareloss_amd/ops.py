@@ -749,7 +749,14 @@ class _StemConv(Function):
         # the bf16 / fp16 conv maths keep the stem (the raw image, values ~1e2; 2.5 GFLOP per image) in
         # the fp32 form: 8 significant bits there cost 3-4 % of the target loss after one update
         math = "fp32" if CONV_MATH in ("bf16", "fp16") else CONV_MATH
-        cpart = _parts(col, math, compute=_split_gemm(cout, kk))
+        # f16x3: the column matrix holds the image's values and padding zeros only, and with windows
+        # that overlap (stride <= kernel) and reach both borders every pixel is in one: max |col| =
+        # max |x|, so the GEMM's operand scale comes from the 3-channel image (r05: a 12-MB pass instead
+        # of one over the 147 x P columns, 30-120 us).  The scale is a power of two of that maximum,
+        # the same bits either way; the stem's weight gradient (64 x 147, exact-f32 tiles) reads none.
+        cover = (stride <= min(kh, kw) and pad < min(kh, kw) and (ho - 1) * stride - pad + kh >= h and
+                 (wo - 1) * stride - pad + kw >= w)
+        cpart = _parts(x, math) if cover else _parts(col, math, compute=_split_gemm(cout, kk))
         hip.check(_conv_call(lib, "msl_pconv_fwd", math,
                              (col.data_ptr(), packed.data_ptr(), y.data_ptr(), kk, cout, p,
                               hip.forms(), ws.data_ptr(), wsb, s), (cpart,)), "msl_pconv_fwd")

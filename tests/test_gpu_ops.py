@@ -1120,6 +1120,39 @@ def test_stem_conv_fwd_bwd(h, w, f32_form):
     assert _rel(wg.grad, wr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("h,w,nimg", [(64, 128, 1), (33, 47, 2), (512, 1024, 2)])
+def test_stem_image_partials_same_bits(h, w, nimg):
+    """r05: the stem GEMM takes its f16x3 operand scale from the image's absmax partials (max |col| =
+    max |x|: every pixel lies in a window) - the same output bits as the column matrix's own partials."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    prev = ops.set_f32_form("f16x3")
+    try:
+        g = torch.Generator().manual_seed(h * w + nimg)
+        x = (torch.randn(1, 3, nimg, h, w, generator=g) * 50).to(DEV)
+        wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.01).to(DEV)
+        cache = ops.PackCache(pointwise=True)
+        y = ops.stem_conv(x, wt, 2, 3, cache)
+        ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        p = ho * wo * nimg
+        s = hip.stream_ptr()
+        col = torch.empty(1, 147, nimg, ho, wo, device=DEV)
+        assert lib.msl_im2col(x.data_ptr(), 3, h, w, nimg, 7, 7, 2, 3, 1, ho, wo, col.data_ptr(), s) == 0
+        part = torch.empty(147, device=DEV)
+        assert lib.msl_absmax_partials(col.data_ptr(), 147, p, part.data_ptr(), s) == 0
+        yc = torch.empty_like(y)
+        wsb = lib.msl_pconv_fwd_workspace(147, 64, p)
+        ws = hip.workspace(wsb, DEV)
+        packed = cache.get([wt.contiguous()], 147, 64, 0)
+        assert lib.msl_pconv_fwd_sc(col.data_ptr(), packed.data_ptr(), yc.data_ptr(), 147, 64, p, hip.forms(),
+                                    ws.data_ptr(), wsb, s, part.data_ptr(), 147) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(part.max(), x.abs().max())
+        assert torch.equal(y, yc)
+    finally:
+        ops.set_f32_form(prev)
+
+
 @pytest.mark.parametrize("c,h,w,ceil", [(64, 256, 512, True), (5, 17, 33, True), (3, 16, 16, True),
                                         (4, 15, 20, False), (2, 7, 9, True)])
 def test_maxpool_bit_exact(c, h, w, ceil):
