@@ -1956,21 +1956,30 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       hi = min(hi, 16);
       return hi > lo ? ((1u << hi) - (1u << lo)) : 0u;
     };
+    // an unshifted tap (every pointwise gradient, the 3x3 centre tap): every pixel valid, no cursor
+    // (r05: ~25 fewer scalar instructions per stage there)
+    const bool unshifted = shift == 0;
     auto kmask = [&]() -> unsigned {  // valid pixels of K-step ld_ks; advances the cursor
       unsigned m16 = 0;
       if (ld_ks < k_b) {
-        const int L1 = a.W - cx;  // pixels of the K-step left in row cy
-        const int cy1 = cy + 1 == a.H ? 0 : cy + 1;  // the next row (of the next image after the last)
-        if ((unsigned)(cy + dh) < (unsigned)a.H) m16 |= seg(clo - cx, min(L1, chi - cx));
-        if ((unsigned)(cy1 + dh) < (unsigned)a.H) m16 |= seg(L1 + clo, L1 + chi);
+        if (unshifted) {
+          m16 = 0xffffu;
+        } else {
+          const int L1 = a.W - cx;  // pixels of the K-step left in row cy
+          const int cy1 = cy + 1 == a.H ? 0 : cy + 1;  // the next row (of the next image after the last)
+          if ((unsigned)(cy + dh) < (unsigned)a.H) m16 |= seg(clo - cx, min(L1, chi - cx));
+          if ((unsigned)(cy1 + dh) < (unsigned)a.H) m16 |= seg(L1 + clo, L1 + chi);
+        }
         const int left = a.P - ld_ks * kWx6BK;  // none past the last pixel
         if (left < kWx6BK) m16 &= (1u << max(left, 0)) - 1u;
       }
       ++ld_ks;
-      cx += kWx6BK;
-      if (cx >= a.W) {
-        cx -= a.W;
-        if (++cy == a.H) cy = 0;
+      if (!unshifted) {
+        cx += kWx6BK;
+        if (cx >= a.W) {
+          cx -= a.W;
+          if (++cy == a.H) cy = 0;
+        }
       }
       return m16;
     };
@@ -1983,6 +1992,14 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
           sXr[i] = n < a.N ? pow2_scale(a.bpart[n], iv) : 1.f;
         }
       }
+    }
+    // per-row element offsets of this thread's four X rows at K-step 0 (+ the tap shift); a row past N
+    // gets a sentinel that stays below -4 for every K-step (int32: N * P < 2^29, launch_wgrad)
+    int rbase[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nr = (tid >> 3) + 32 * i;
+      rbase[i] = n0 + nr < a.N ? (n0 + nr) * a.P + 4 * cc + shift : (int)0xC0000000;
     }
     float rbv[16];
     unsigned rmb = 0, rsh = 0;
@@ -2000,17 +2017,11 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       sho = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int nr = (tid >> 3) + 32 * i;
-        const long long e = (long long)(n0 + nr) * a.P + ks0 * kWx6BK + 4 * cc + shift;
-        unsigned off = OOB;
-        if (n0 + nr < a.N) {
-          if (e >= 0) {
-            off = (unsigned)e * 4u;
-          } else if (e > -4) {
-            off = 0u;
-            sho |= (unsigned)(-e) << (8 * i);
-          }
-        }
+        // branch-free (r05: the 64-bit form with nested conditions compiled to exec-mask branches,
+        // ~15 instructions per row)
+        const int e = rbase[i] + ks0 * kWx6BK;
+        const unsigned off = e >= 0 ? (unsigned)e * 4u : (e > -4 ? 0u : OOB);
+        sho |= (e < 0 && e > -4 ? (unsigned)(-e) : 0u) << (8 * i);
         union { u32x4 u; float f[4]; } c;
         c.u = __builtin_amdgcn_raw_buffer_load_b128(rB, off, 0, 0);
 #pragma unroll
