@@ -2046,8 +2046,10 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
           }
         }
       }
+      if (__builtin_amdgcn_ballot_w64(mbv != 0xfu) != 0) {  // (r05: most waves' chunks are all valid)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) rbv[q] = (mbv >> (q & 3)) & 1u ? rbv[q] : 0.f;
+        for (int q = 0; q < 16; ++q) rbv[q] = (mbv >> (q & 3)) & 1u ? rbv[q] : 0.f;
+      }
       if constexpr (H1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
