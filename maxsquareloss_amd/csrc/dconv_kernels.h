@@ -1,6 +1,8 @@
 // Implicit-GEMM kernel templates for the dilated 3x3 conv (design notes in dconv.hip).
 // Included by dconv.hip (libmsl_hip.so).
 #pragma once
+#include <type_traits>
+
 #include "msl_internal.h"
 
 namespace msl {
@@ -196,6 +198,35 @@ __device__ __forceinline__ void split2h_set(Split2h& s, int j, float v) {  // v 
   s.lo[j] = (_Float16)(v - (float)h);
 }
 
+// The f16x3 split of a pair (x0, x1) under the power-of-two scale s, packed: hi = fp16(x s),
+// lo = fp16(x s - hi), two halves per register - the same values as the plain C form (x s is exact, so
+// the fused product of v_fma_mix is too), in 4 VALU per pair: the compiler's form also rebuilt hi
+// through an fp32 multiply and a pack beside the v_fma_mix that feeds lo (r05).
+__device__ __forceinline__ void split2_mix(float x0, float x1, float s, unsigned& hi, unsigned& lo) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(x0), "v"(x1), "v"(s));
+}
+
+// split2h_set of eight values v[j] * sc (sc a power of two) through split2_mix: 2 VALU per value instead
+// of the compiler's 3 (fp32 products, a pack, the hi plane widened back for the remainder) - r05
+__device__ __forceinline__ void split2h_scaled(Split2h& out, const float (&v)[8], float sc) {
+  union { unsigned u[4]; f16x8 h; } hi, lo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) split2_mix(v[2 * q], v[2 * q + 1], sc, hi.u[q], lo.u[q]);
+  out.hi = hi.h;
+  out.lo = lo.h;
+}
+
+// the plain image-operand map of the BD stage (x -> x * s): split through split2h_scaled
+struct ScaleXf {
+  float s;
+  __device__ __forceinline__ float operator()(int, float v) const { return v * s; }
+};
+
 __device__ __forceinline__ f32x16 mfma_h3(const Split2h& a, const Split2h& b, f32x16 c) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.lo, b.hi, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.lo, c, 0, 0, 0);
@@ -389,6 +420,7 @@ __device__ __forceinline__ void mfma_stage_h3p(const float* As, const float* Bs,
     for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
     // every LDS read of the K-step issues before the B split's VALU work
     __builtin_amdgcn_sched_barrier(0);
+    // (the plain C split here: split2h_scaled made the big pointwise GEMMs 3-4 % slower, r05)
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -470,8 +502,12 @@ __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane,
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (std::is_same_v<std::decay_t<X>, ScaleXf>) {
+      split2h_scaled(bv, braw, xf.s);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) split2h_set(bv, j, xf(j, braw[j]));
+      for (int j = 0; j < 8; ++j) split2h_set(bv, j, xf(j, braw[j]));
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bv.hi, acc[i][0], 0, 0, 0);
 #pragma unroll
@@ -1180,7 +1216,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
               As, wm, lane, acc, mid,
               [&](int j, float v) { return __builtin_amdgcn_fmed3f(fmaf(v, al[j], be[j]), 0.f, vm); }, cur);
         } else {
-          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, [&](int, float v) { return v * sB; }, cur);
+          mfma_stage_hd<TM, BM, H1>(As, wm, lane, acc, mid, ScaleXf{sB}, cur);
         }
         if constexpr (PROF & 1) t3 = sk_stamp();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2062,17 +2098,12 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       } else if constexpr (H3) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          f16x4 hi, lo;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float v = rbv[4 * i + j] * sXr[i];
-            const _Float16 h = (_Float16)v;
-            hi[j] = h;
-            lo[j] = (_Float16)(v - (float)h);
-          }
+          uint2 hi, lo;
+          split2_mix(rbv[4 * i], rbv[4 * i + 1], sXr[i], hi.x, lo.x);
+          split2_mix(rbv[4 * i + 2], rbv[4 * i + 3], sXr[i], hi.y, lo.y);
           char* dst = base + i * 32 * 16;
-          *reinterpret_cast<f16x4*>(dst) = hi;
-          *reinterpret_cast<f16x4*>(dst + 2 * RB) = lo;
+          *reinterpret_cast<uint2*>(dst) = hi;
+          *reinterpret_cast<uint2*>(dst + 2 * RB) = lo;
         }
         return;
       }
