@@ -871,12 +871,12 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
       a.anpart = an;
       a.bnpart = bn;
       a.rowscale = (an == cout && bn == cin) ? 1 : 0;
-      hipLaunchKernelGGL(k_split_rows<MT>, dim3(pl.lda / 32, cdiv(pl.KS, 16)), dim3(256), 0, st, dy, cout, P,
+      hipLaunchKernelGGL(k_split_rows<MT>, dim3(pl.lda / kSplitRowsR, cdiv(pl.KS, 16)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, ap, an, a.rowscale);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL((k_wgrad_x6<MT>), grid, block, 0, st, a);
     } else {
-      hipLaunchKernelGGL(k_split_rows<kMathX6>, dim3(pl.lda / 32, cdiv(pl.KS, 16)), dim3(256), 0, st, dy, cout, P,
+      hipLaunchKernelGGL(k_split_rows<kMathX6>, dim3(pl.lda / kSplitRowsR, cdiv(pl.KS, 16)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, (const float*)nullptr, 0);
       MSL_CHECK_LAUNCH();
       hipLaunchKernelGGL(k_wgrad_x6<kMathX6>, grid, block, 0, st, a);

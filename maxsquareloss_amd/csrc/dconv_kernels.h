@@ -1830,17 +1830,20 @@ __global__ void __launch_bounds__(256) k_wsk_reduce_wide(WskArgs a) {
 constexpr int kWx6BK = 16;
 
 // planes[((ks*3 + q)*2 + h)*lda + m][j] = term q of src[m][ks*16 + 8h + j] (0 past P or M).
-// Block = 32 rows x 16 K-steps (256 pixels).  Each wave loads 8 rows, 16 B per lane and row (4 pixels:
-// one coalesced 1-KB run per row and load; the r03 form's dword loads moved 256 B per instruction and ran
-// at 3.3 TB/s), splits them and stores the 16-bit terms to LDS as [plane][row][pixel] rows padded to
-// 528 B; the block then writes every (K-step, plane, half) as 32 consecutive rows of 16-B vectors
-// (ds_read_b128 at a 528-B stride: conflict-free).  grid = (lda / 32, ceil(KS / 16)).
+// Block = R = kSplitRowsR rows x 16 K-steps (256 pixels).  Each wave loads R / 4 rows, 16 B per lane and
+// row (4 pixels: one coalesced 1-KB run per row and load; the r03 form's dword loads moved 256 B per
+// instruction and ran at 3.3 TB/s), splits them and stores the 16-bit terms to LDS as [plane][row][pixel]
+// rows padded to 528 B; the block then writes every (K-step, plane, half) as R consecutive rows of 16-B
+// vectors (ds_read_b128 at a 528-B stride: conflict-free).  grid = (lda / R, ceil(KS / 16)).
 // MT = kMathH3P: two fp16 planes of src * s, s = pow2_scale of src's absmax partials `part`.
+// r05: R = 16 instead of 32 (twice the blocks, half the LDS each: more of them resident, so one block's
+// load round trip overlaps another's transpose and stores)
+constexpr int kSplitRowsR = 16;
 template <int MT = kMathX6>
 __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ src, int M, int P, int KS, int lda,
                                                      bf16x8* __restrict__ planes, const float* __restrict__ part,
                                                      int npart, int rowscale = 0) {
-  constexpr int R = 32, PX = 256, LDP = PX + 8;  // rows, pixels per block; LDS row stride in 16-bit terms
+  constexpr int R = kSplitRowsR, PX = 256, LDP = PX + 8;  // rows, pixels per block; LDS row stride (16-bit terms)
   constexpr int KB = PX / kWx6BK;                // K-steps per block
   constexpr bool F16 = MT == kMathH3P || MT == kMathH1P;
   constexpr int NP = MT == kMathH1P ? 1 : F16 ? 2 : 3;
