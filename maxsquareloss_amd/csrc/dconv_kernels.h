@@ -2054,13 +2054,19 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       const unsigned mb = (m32 >> (4 * cc)) & 0xfu;
       mbo = mb;
       sho = 0;
+      // a run that starts before X: only X's row 0 (tile n0 = 0, this thread's first row with
+      // tid < 8) at the first K-steps of a negative shift - a wave-uniform test (r05: computed per row
+      // and stage, it cost ~20 VALU per stage)
+      if (n0 == 0 && ks0 * kWx6BK + shift < 0) {
+        const int e0 = rbase[0] + ks0 * kWx6BK;
+        sho = e0 < 0 && e0 > -4 ? (unsigned)(-e0) : 0u;
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         // branch-free (r05: the 64-bit form with nested conditions compiled to exec-mask branches,
         // ~15 instructions per row)
         const int e = rbase[i] + ks0 * kWx6BK;
         const unsigned off = e >= 0 ? (unsigned)e * 4u : (e > -4 ? 0u : OOB);
-        sho |= (e < 0 && e > -4 ? (unsigned)(-e) : 0u) << (8 * i);
         union { u32x4 u; float f[4]; } c;
         c.u = __builtin_amdgcn_raw_buffer_load_b128(rB, off, 0, 0);
 #pragma unroll
