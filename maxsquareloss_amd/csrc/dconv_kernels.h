@@ -2050,7 +2050,8 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
     // place there (sho: the shift per row, one byte each); one further before is masked whole.
     auto loadB = [&](float (&rv)[16], unsigned& mbo, unsigned& sho) {
       const int ks0 = ld_ks;
-      const unsigned m32 = kmask() | (kmask() << 16);
+      const unsigned mk0 = kmask();  // (sequenced: both calls advance the cursor)
+      const unsigned m32 = mk0 | (kmask() << 16);
       const unsigned mb = (m32 >> (4 * cc)) & 0xfu;
       mbo = mb;
       sho = 0;
