@@ -1917,6 +1917,10 @@ __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ sr
   }
 }
 
+// k_wgrad_x6's per-segment border-mask table (K-steps): a segment up to this long reads its masks from
+// LDS, computed by all threads at the segment's start, instead of the per-stage scalar cursor (r05)
+constexpr int kWxMaskTab = 2048;
+
 // MT = kMathH3P (f16x3): dY (the pre-split operand) as two fp16 planes scaled by k_split_rows<H3>,
 // X scaled by its own pow2_scale (absmax partials bpart) and split into two fp16 planes; the
 // pieces are unscaled by both before they are stored.
@@ -1931,7 +1935,9 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
   constexpr int STAGEB = 2 * KVB;     // two K-steps
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGEB];  // 48.75 KB (x6): the only LDS object
+  // + (r05) the segment's border-mask table: 16 bits per K-step, kWxMaskTab K-steps
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGEB + kWxMaskTab * 2];  // the only LDS object
+  unsigned short* const mtab = reinterpret_cast<unsigned short*>(smem + 2 * STAGEB);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2048,10 +2054,19 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
     // applied when the values are split (storeB), so nothing waits for the loads here; a run that
     // starts 1-3 pixels before X (row 0, negative shift) is loaded from X's start and shifted into
     // place there (sho: the shift per row, one byte each); one further before is masked whole.
+    // the segment's masks from the LDS table (built below, before the prologue) when it fits: two
+    // K-steps per 32-bit read at a wave-uniform address; else the scalar cursor
+    const bool use_tab = nst + 3 <= kWxMaskTab;
     auto loadB = [&](float (&rv)[16], unsigned& mbo, unsigned& sho) {
       const int ks0 = ld_ks;
-      const unsigned mk0 = kmask();  // (sequenced: both calls advance the cursor)
-      const unsigned m32 = mk0 | (kmask() << 16);
+      unsigned m32;
+      if (use_tab) {
+        m32 = *reinterpret_cast<const unsigned*>(mtab + (ks0 - k_a));  // (ks0 - k_a even)
+        ld_ks += 2;
+      } else {
+        const unsigned mk0 = kmask();  // (sequenced: both calls advance the cursor)
+        m32 = mk0 | (kmask() << 16);
+      }
       const unsigned mb = (m32 >> (4 * cc)) & 0xfu;
       mbo = mb;
       sho = 0;
@@ -2205,6 +2220,31 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     __syncthreads();  // the previous segment's LDS reads are complete in every wave
+    if (use_tab) {
+      // mask of K-step k_a + kc, as kmask computes it (0 past the segment's end, past P or outside the
+      // image), one per thread at a time; kc up to nst + 2 (the loads issued past the end)
+      for (int kc = tid; kc < nst + 3; kc += blockDim.x) {
+        unsigned m16 = 0;
+        if (kc < nst) {
+          const int ks = k_a + kc;
+          if (unshifted) {
+            m16 = 0xffffu;
+          } else {
+            const int p = ks * kWx6BK;
+            const int q = p / a.W;
+            const int x = p - q * a.W, y = q % a.H;
+            const int L1 = a.W - x;
+            const int y1 = y + 1 == a.H ? 0 : y + 1;
+            if ((unsigned)(y + dh) < (unsigned)a.H) m16 |= seg(clo - x, min(L1, chi - x));
+            if ((unsigned)(y1 + dh) < (unsigned)a.H) m16 |= seg(L1 + clo, L1 + chi);
+          }
+          const int left = a.P - ks * kWx6BK;
+          if (left < kWx6BK) m16 &= (1u << max(left, 0)) - 1u;
+        }
+        mtab[kc] = (unsigned short)m16;
+      }
+      __syncthreads();
+    }
     loadB(rbv, rmb, rsh);
     loadA(A0, k_a);
     storeB(0, rbv, rmb, rsh);
