@@ -21,7 +21,7 @@
  *   - Work is enqueued on the given hipStream_t (passed as msl_stream_t) and
  *     is stream-ordered; no entry point synchronises the host, so every call
  *     is safe to capture in a hipGraph.
- *   - Return value: 0 = MSL_OK, < 0 = argument / shape / workspace error
+ *   - Return value: 0 = MSL_OK, < 0 = argument / shape / workspace / launch-bound error
  *     (see msl_status_string), > 0 = the hipError_t of a failed launch.
  */
 #ifndef MSL_HIP_H
@@ -40,6 +40,8 @@ typedef void* msl_stream_t; /* a hipStream_t */
 #define MSL_ERR_SHAPE (-1)
 #define MSL_ERR_WORKSPACE (-2)
 #define MSL_ERR_ARG (-3)
+/* a launch whose block exceeds the kernel's __launch_bounds__: refused on the host, before the launch (r06) */
+#define MSL_ERR_LAUNCH (-4)
 
 int msl_abi_version(void);
 const char* msl_status_string(int status);
@@ -525,6 +527,12 @@ int msl_sgd_step(const msl_sgd_entry* entries, const int32_t* block_entry,
 int msl_sgd_step_lr_dev(const msl_sgd_entry* entries, const int32_t* block_entry,
                         const long long* block_offset, long long n_blocks, const float* lr_dev,
                         float momentum, float weight_decay, float grad_scale, msl_stream_t stream);
+
+/* Diagnostics (r06): the launch guard every entry point runs before each kernel launch (MSL_ERR_LAUNCH
+ * when a block exceeds the kernel's __launch_bounds__).  Launches a 256-thread-bound probe kernel with
+ * `threads` threads writing out[t] = t: MSL_OK (and out[0 .. threads) written) for 1 <= threads <= 256,
+ * MSL_ERR_LAUNCH (nothing launched, out untouched) above.  Replaces nothing in the reference. */
+int msl_launch_guard_probe(int threads, float* out, msl_stream_t stream);
 
 #ifdef __cplusplus
 }

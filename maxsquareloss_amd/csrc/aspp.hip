@@ -122,7 +122,7 @@ int msl_aspp_weight_layout(const float* w, long long branch_stride, int nbranch,
                            msl_stream_t stream) {
   if (!w || !wp || nbranch < 1 || nbranch > 2 || c < 1 || cin < 1) return MSL_ERR_ARG;
   const long long n = 9LL * nbranch * c * cin;
-  hipLaunchKernelGGL(k_aspp_weight_layout, dim3((unsigned)std::min<long long>(cdiv(n, 256), 4096)), dim3(256), 0,
+  MSL_LAUNCH(k_aspp_weight_layout, dim3((unsigned)std::min<long long>(cdiv(n, 256), 4096)), dim3(256), 0,
                      as_stream(stream), w, branch_stride, 9 * nbranch, c, cin, wp);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -131,7 +131,7 @@ int msl_aspp_weight_layout(const float* w, long long branch_stride, int nbranch,
 int msl_aspp_weight_grad(const float* dwp, int nbranch, int c, int cin, float* dw, msl_stream_t stream) {
   if (!dwp || !dw || nbranch < 1 || nbranch > 2 || c < 1 || cin < 1) return MSL_ERR_ARG;
   const long long n = 9LL * nbranch * c * cin;
-  hipLaunchKernelGGL(k_aspp_weight_grad, dim3((unsigned)std::min<long long>(cdiv(n, 256), 4096)), dim3(256), 0,
+  MSL_LAUNCH(k_aspp_weight_grad, dim3((unsigned)std::min<long long>(cdiv(n, 256), 4096)), dim3(256), 0,
                      as_stream(stream), dwp, 9 * nbranch, c, cin, dw);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -141,7 +141,7 @@ int msl_aspp_shift_add(const float* z, const float* bias, float* y, int nbranch,
                        int dil0, int dil1, msl_stream_t stream) {
   if (!z || !y || aspp_bad(nbranch, c, h, w, nimg, dil0, dil1)) return MSL_ERR_ARG;
   const int P = nimg * h * w;
-  hipLaunchKernelGGL(k_aspp_shift_add, dim3(cdiv(P, 256), c), dim3(256), 0, as_stream(stream), z, bias, y,
+  MSL_LAUNCH(k_aspp_shift_add, dim3(cdiv(P, 256), c), dim3(256), 0, as_stream(stream), z, bias, y,
                      9 * nbranch, c, h, w, P, dil0, dil1);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -152,11 +152,11 @@ int msl_aspp_shift_gather(const float* dy, float* g, float* dbias, int nbranch, 
   if (!dy || !g || aspp_bad(nbranch, c, h, w, nimg, dil0, dil1)) return MSL_ERR_ARG;
   const int P = nimg * h * w;
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(k_aspp_shift_gather, dim3(cdiv(P, 256), 9 * nbranch * c), dim3(256), 0, st, dy, g, c, h, w, P,
+  MSL_LAUNCH(k_aspp_shift_gather, dim3(cdiv(P, 256), 9 * nbranch * c), dim3(256), 0, st, dy, g, c, h, w, P,
                      dil0, dil1);
   MSL_CHECK_LAUNCH();
   if (dbias) {
-    hipLaunchKernelGGL(k_aspp_bias_grad, dim3(c), dim3(256), 0, st, dy, P, dbias, c, nbranch);
+    MSL_LAUNCH(k_aspp_bias_grad, dim3(c), dim3(256), 0, st, dy, P, dbias, c, nbranch);
     MSL_CHECK_LAUNCH();
   }
   return MSL_OK;

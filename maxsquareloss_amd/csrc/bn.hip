@@ -442,9 +442,9 @@ __global__ void __launch_bounds__(256) k_zero_rows(float* __restrict__ v, int n)
 // or garbage maxima (up to 1e38) in the partials, i.e. wrong f16x3 operand scales (r03 pair-mode
 // graph test).  Kernel nodes keep the stream order.
 int absmax_rows(const float* t, int c, int p, float* absmax, hipStream_t st) {
-  hipLaunchKernelGGL(k_zero_rows, dim3(cdiv(c, 256)), dim3(256), 0, st, absmax, c);
+  MSL_LAUNCH(k_zero_rows, dim3(cdiv(c, 256)), dim3(256), 0, st, absmax, c);
   MSL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_absmax_rows, dim3(c, cdiv(p, kAbsChunk)), dim3(256), 0, st, t, p, absmax);
+  MSL_LAUNCH(k_absmax_rows, dim3(c, cdiv(p, kAbsChunk)), dim3(256), 0, st, t, p, absmax);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
@@ -677,7 +677,7 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
 template <typename K, typename A>
 static int bn_launch_fused(K k4, K k9, K k16, K k33, int c, int p, hipStream_t st, const A& a) {
   K k = p <= 4 * kBnFusedThreads ? k4 : p <= 9 * kBnFusedThreads ? k9 : p <= 16 * kBnFusedThreads ? k16 : k33;
-  hipLaunchKernelGGL(k, dim3(c), dim3(kBnFusedThreads), 0, st, a);
+  MSL_LAUNCH(k, dim3(c), dim3(kBnFusedThreads), 0, st, a);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
@@ -743,12 +743,12 @@ int msl_bn_fwd_mask(const float* x, const float* gamma, const float* beta, const
   if (relu_mask && !(fused && relu)) return MSL_ERR_ARG;  // the bits come from the fused kernels
   if (training && !fused) {
     if (vec)
-      hipLaunchKernelGGL(k_bn_stats<true>, dim3(R, S), dim3(256), 0, st, x, p, S, part, absmax, nimg);
+      MSL_LAUNCH(k_bn_stats<true>, dim3(R, S), dim3(256), 0, st, x, p, S, part, absmax, nimg);
     else
-      hipLaunchKernelGGL(k_bn_stats<false>, dim3(R, S), dim3(256), 0, st, x, p, S, part, absmax, nimg);
+      MSL_LAUNCH(k_bn_stats<false>, dim3(R, S), dim3(256), 0, st, x, p, S, part, absmax, nimg);
     MSL_CHECK_LAUNCH();
   } else if (!fused && absmax) {
-    hipLaunchKernelGGL(k_zero_rows, dim3(cdiv(c, 256)), dim3(256), 0, st, absmax, c);
+    MSL_LAUNCH(k_zero_rows, dim3(cdiv(c, 256)), dim3(256), 0, st, absmax, c);
     MSL_CHECK_LAUNCH();
   }
   BnArgs a;
@@ -778,9 +778,9 @@ int msl_bn_fwd_mask(const float* x, const float* gamma, const float* beta, const
   if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>, c, p, st, a);
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec)
-    hipLaunchKernelGGL(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
+    MSL_LAUNCH(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(k_bn_apply<false>, dim3(blocks), dim3(256), 0, st, a);
+    MSL_LAUNCH(k_bn_apply<false>, dim3(blocks), dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();  // (absmax: folded in by k_bn_apply, zeroed by the launch before)
   return MSL_OK;
 }
@@ -846,13 +846,13 @@ static int bn_bwd(const float* dy, const float* x, const float* y, const uint64_
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec) {
-    hipLaunchKernelGGL(k_bn_bwd_reduce<true>, dim3(R, S), dim3(256), 0, st, a);
+    MSL_LAUNCH(k_bn_bwd_reduce<true>, dim3(R, S), dim3(256), 0, st, a);
     MSL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_bwd_apply<true>, dim3(blocks), dim3(256), 0, st, a);
+    MSL_LAUNCH(k_bn_bwd_apply<true>, dim3(blocks), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(R, S), dim3(256), 0, st, a);
+    MSL_LAUNCH(k_bn_bwd_reduce<false>, dim3(R, S), dim3(256), 0, st, a);
     MSL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_bwd_apply<false>, dim3(blocks), dim3(256), 0, st, a);
+    MSL_LAUNCH(k_bn_bwd_apply<false>, dim3(blocks), dim3(256), 0, st, a);
   }
   MSL_CHECK_LAUNCH();  // (absmax_dx: folded in by k_bn_bwd_apply, zeroed by k_bn_bwd_reduce)
   return MSL_OK;

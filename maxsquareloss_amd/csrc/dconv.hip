@@ -23,6 +23,7 @@
 // buffered, one barrier per K-step.  Small GEMMs are split along K into fp32
 // slabs that a reduce kernel sums deterministically (fixed order).
 #include "dconv_kernels.h"
+#include "dconv_w1.h"
 
 namespace msl {
 
@@ -43,6 +44,9 @@ __global__ void __launch_bounds__(256) k_reduce_slabs(const float* __restrict__ 
     out[i] = accumulate ? out[i] + v : v;
   }
 }
+
+// msl_launch_guard_probe's kernel: out[t] = t (a 256-thread bound, like most of the library's kernels)
+__global__ void __launch_bounds__(256) k_guard_probe(float* __restrict__ out) { out[threadIdx.x] = (float)threadIdx.x; }
 
 // dbias[b][m] (=|+=) sum_p dy[m][p], same value for every branch b.
 __global__ void __launch_bounds__(256) k_bias_grad(const float* __restrict__ dy, int P,
@@ -416,8 +420,36 @@ static size_t img_planes_bytes(int cimg, int P) { return align_up((size_t)cdiv(c
 // The f16x3 / fp16 forward-form GEMMs that read their image operand pre-split (k_split_img, BP form):
 // the 3x3 ones with M >= 512 (profiles/r03_bp_ab.txt); fp16 math (one plane: a quarter of the loads'
 // instructions, half their bytes) from M >= 128 (r05)
+// r06: the 3x3 GEMMs with M >= kBqMinM read the pre-split image in the 2 x 2 wave layout (BQ: 64 rows x 64
+// pixels per wave, half the A-fragment LDS reads per MFMA of the 1 x 4 layout, no split in the loop)
+constexpr int kBqMinM = 1 << 30;
+static bool bq_form(int taps, int M, bool small_f16) { return taps == 9 && !small_f16 && M >= kBqMinM; }
+// r06: the 3x3 f16x3 / fp16 GEMMs with 128-row tiles run the W1 form (dconv_w1.h)
+constexpr int kW1MinM = 1 << 30;
+static bool w1_form(int taps, int M, bool small_f16) { return taps == 9 && !small_f16 && M >= kW1MinM; }
+
+// The stream-K schedule of a forward-form launch over at most nw_max workers (see launch_fwd_form)
+static SkArgs plan_sk(int tiles_m, int tiles_n, int KS, int nw_max, int hybrid, float* part) {
+  SkArgs sk{};
+  sk.part = part;
+  sk.tiles_m = tiles_m;
+  sk.tiles_n = tiles_n;
+  sk.KS = KS;
+  const long long tiles = (long long)tiles_m * tiles_n;
+  sk.tdp = (hybrid && tiles >= nw_max) ? (int)(tiles / nw_max * nw_max) : 0;
+  sk.gm = sk.tdp > 0 ? tiles_m : 1;
+  const long long T = (tiles - sk.tdp) * KS;
+  sk.NW = (int)std::min<long long>(nw_max, T);
+  constexpr long long kSkMinIt = 8;
+  if (sk.tdp > 0) sk.NW = (int)std::max<long long>(1, std::min<long long>(sk.NW, T / kSkMinIt));
+  sk.T = (int)T;
+  return sk;
+}
+static bool w1_form(int taps, int M, bool small_f16);
 static bool bp_form(int taps, int M, bool small_f16, bool h1 = false) {
-  return taps == 9 && !small_f16 && (M >= 512 || (h1 && M >= 128));
+  // (the W1 form reads only the pre-split planes)
+  return taps == 9 && !small_f16 &&
+         (M >= 512 || (h1 && M >= 128) || bq_form(taps, M, small_f16) || w1_form(taps, M, small_f16));
 }
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P, int cimg, int taps) {
   // the planes only where the BP form can run (the stem / pointwise calls reserved them too)
@@ -430,24 +462,32 @@ static float* ws_partials(void* ws, size_t ws_bytes, int k) {  // k-th partials 
 
 // The forward-form kernel, plain or with the accumulate epilogue (a template form of its own)
 template <int BM, int G, int ST, int WM, int WN, int MT, bool PW = false>
-static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk,
+static int launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a, const SkArgs& sk,
                       bool bp = false) {
   if constexpr (MT == kMathH3P || MT == kMathH1P) {  // held to two waves per SIMD (k_igemm_fwd_sk2)
+    if constexpr (!PW && BM == 128 && G == 1 && ST == 4 && WM == 2 && WN == 2) {
+      // the 2 x 2 pre-split form (BQ, r06): 3x3 GEMMs only, never accumulating
+      if (bp && !accum) {
+        MSL_LAUNCH((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true, true>), grid, block, 0, st,
+                           a, sk);
+        return MSL_OK;
+      }
+    }
     if constexpr (!PW && (BM == 128 || BM == 64) && G == 1 && ST == 4 && WM == 1 && WN == 4) {
       // (accumulating BD / BP forms at 64 rows only: the pointwise M <= 64 data gradients; no 3x3 call
       // accumulates, and the 128-row accumulating 3x3 forms are not instantiated)
       if (bp) {  // the image operand pre-split by k_split_img (never for the pointwise kernels: no BP / BD form)
         if constexpr (BM == 64) {
           if (accum) {
-            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0,
+            MSL_LAUNCH((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true, true>), grid, block, 0,
                                st, a, sk);
-            return;
+            return MSL_OK;
           }
         }
         if (!accum) {
-          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true, true>), grid, block, 0,
+          MSL_LAUNCH((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true, true>), grid, block, 0,
                              st, a, sk);
-          return;
+          return MSL_OK;
         }
       }
       // the image operand straight to registers (BD form) for the shifted 3x3 rows (dword pieces);
@@ -458,28 +498,29 @@ static void launch_sk(int accum, dim3 grid, dim3 block, hipStream_t st, const Fw
       if (a.cimg % kCB == 0) {
         if constexpr (BM == 64) {
           if (accum) {
-            hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a,
+            MSL_LAUNCH((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true, true>), grid, block, 0, st, a,
                                sk);
-            return;
+            return MSL_OK;
           }
         }
         if (!accum) {
-          hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true>), grid, block, 0, st, a,
+          MSL_LAUNCH((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false, true>), grid, block, 0, st, a,
                              sk);
-          return;
+          return MSL_OK;
         }
       }
     }
     if (accum)
-      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true>), grid, block, 0, st, a, sk);
+      MSL_LAUNCH((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, true>), grid, block, 0, st, a, sk);
     else
-      hipLaunchKernelGGL((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false>), grid, block, 0, st, a, sk);
+      MSL_LAUNCH((k_igemm_fwd_sk2<BM, kSkBN, G, ST, WM, WN, PW, MT, false>), grid, block, 0, st, a, sk);
   } else {
     if (accum)
-      hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
+      MSL_LAUNCH((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, true>), grid, block, 0, st, a, sk);
     else
-      hipLaunchKernelGGL((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, false>), grid, block, 0, st, a, sk);
+      MSL_LAUNCH((k_igemm_fwd_sk<BM, kSkBN, G, ST, WM, WN, false, MT, false>), grid, block, 0, st, a, sk);
   }
+  return MSL_OK;
 }
 
 template <int MT>
@@ -599,7 +640,7 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
           a.bnpart = img_npart;
         } else {
           float* part = ws_partials(ws, ws_bytes, 1);
-          hipLaunchKernelGGL(k_absmax, dim3(kNPart), block, 0, st, img, (long long)cimg * P, 0LL, 1, part);
+          MSL_LAUNCH(k_absmax, dim3(kNPart), block, 0, st, img, (long long)cimg * P, 0LL, 1, part);
           MSL_CHECK_LAUNCH();
           a.bpart = part;
           a.bnpart = kNPart;
@@ -615,11 +656,26 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
           const long long n = (long long)a.ncb * 2 * P;
           const dim3 sgrid((unsigned)std::min<long long>(cdiv(n, 256), 8192));
           if constexpr (MT == kMathH1P)
-            hipLaunchKernelGGL(k_split_img<1>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
+            MSL_LAUNCH(k_split_img<1>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
           else
-            hipLaunchKernelGGL(k_split_img<2>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
+            MSL_LAUNCH(k_split_img<2>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
           MSL_CHECK_LAUNCH();
           a.Bx6 = planes;
+        }
+        if (w1_form(taps, M, small_f16) && !accum) {
+          // the W1 form (r06, dconv_w1.h): 128 x 256 tiles at one wave per SIMD, 256 stream-K workers
+          const long long tiles1 = (long long)pl.tiles_m * cdiv(P, kW1BN);
+          if (tiles1 * sk.KS * kW1NW >= (1LL << 31)) return MSL_ERR_SHAPE;
+          const SkArgs s1 = plan_sk(pl.tiles_m, cdiv(P, kW1BN), sk.KS, kW1NW, forms_of(forms).sk_hybrid, (float*)ws);
+          static_assert((size_t)kW1NW * 2 * kW1BM * kW1BN <= (size_t)kSkNW * 2 * 128 * kSkBN, "W1 pieces fit");
+          const dim3 g1(s1.tdp > 0 ? kW1NW : s1.NW);
+          MSL_LAUNCH((k_igemm_fwd_w1<MT>), g1, block, 0, st, a, s1);
+          MSL_CHECK_LAUNCH();
+          if (s1.T > 0)
+            MSL_LAUNCH((k_sk_reduce<kW1BM, kW1BN>), dim3(kW1BM * kW1BN / 1024, (unsigned)(tiles1 - s1.tdp)), block, 0,
+                       st, a, s1);
+          MSL_CHECK_LAUNCH();
+          return MSL_OK;
         }
         // pointwise: B rows are unshifted, so they move as dwordx4 (4 pixels per lane: 2 DMAs per
         // wave and K-step instead of 8 dword ones): 1-4 us per call on the wide 1x1 GEMMs
@@ -628,47 +684,49 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // (2 x 2 waves split each column twice); step 40.5 vs 40.9 ms on one box
         // (profiles/r02_f16x3_waves.txt)
         if (small_f16) {
-          launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp);
+          MSL_TRY(launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp));
         } else if (taps == 1 && dil0 == 0) {
           if constexpr (MT == kMathH1P) {
             if (pw2)
-              launch_sk<128, 2, 3, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
+              MSL_TRY(launch_sk<128, 2, 3, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp));
             else
-              launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
+              MSL_TRY(launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp));
           } else {
-            launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp);
+            MSL_TRY(launch_sk<128, 1, 4, 1, 4, MT, true>(accum, grid, block, st, a, sk, bp));
           }
+        } else if (bp && !accum && bq_form(taps, M, small_f16)) {
+          MSL_TRY(launch_sk<128, 1, 4, 2, 2, MT>(accum, grid, block, st, a, sk, bp));
+        } else {
+          MSL_TRY(launch_sk<128, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp));
         }
-        else
-          launch_sk<128, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp);
       } else {
-        launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk);
+        MSL_TRY(launch_sk<128, 1, 4, 2, 2, kMathX6P>(accum, grid, block, st, a, sk));
       }
       MSL_CHECK_LAUNCH();
       if (reduce) {
         if (small_f16)
-          hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
+          MSL_LAUNCH((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
         else
-          hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
+          MSL_LAUNCH((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
       }
     } else if (pl.bm == 128) {
       if (pl.G == 2)
-        launch_sk<128, 2, 2, 2, 2, MB>(accum, grid, block, st, a, sk);
+        MSL_TRY(launch_sk<128, 2, 2, 2, 2, MB>(accum, grid, block, st, a, sk));
       else
-        launch_sk<128, 1, 3, 2, 2, MB>(accum, grid, block, st, a, sk);
+        MSL_TRY(launch_sk<128, 1, 3, 2, 2, MB>(accum, grid, block, st, a, sk));
       MSL_CHECK_LAUNCH();
-      if (reduce) hipLaunchKernelGGL((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
+      if (reduce) MSL_LAUNCH((k_sk_reduce<128, kSkBN>), rgrid, block, 0, st, a, sk);
     } else if (pl.bm == 64) {
       if (pl.G == 2)
-        launch_sk<64, 2, 2, 2, 2, MS>(accum, grid, block, st, a, sk);
+        MSL_TRY(launch_sk<64, 2, 2, 2, 2, MS>(accum, grid, block, st, a, sk));
       else
-        launch_sk<64, 1, 3, 2, 2, MS>(accum, grid, block, st, a, sk);
+        MSL_TRY(launch_sk<64, 1, 3, 2, 2, MS>(accum, grid, block, st, a, sk));
       MSL_CHECK_LAUNCH();
-      if (reduce) hipLaunchKernelGGL((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
+      if (reduce) MSL_LAUNCH((k_sk_reduce<64, kSkBN>), rgrid, block, 0, st, a, sk);
     } else {
-      launch_sk<32, 2, 2, 1, 4, MS>(accum, grid, block, st, a, sk);
+      MSL_TRY(launch_sk<32, 2, 2, 1, 4, MS>(accum, grid, block, st, a, sk));
       MSL_CHECK_LAUNCH();
-      if (reduce) hipLaunchKernelGGL((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
+      if (reduce) MSL_LAUNCH((k_sk_reduce<32, kSkBN>), rgrid, block, 0, st, a, sk);
     }
     MSL_CHECK_LAUNCH();
     return MSL_OK;
@@ -676,12 +734,12 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   // the split-K tile kernel (odd K-step count, M <= 32) has no bf16 form; x6 runs it in exact f32
   if (MT == kMathBf16 || accum) return MSL_ERR_SHAPE;
   dim3 grid(pl.tiles_n, pl.tiles_m, pl.S);
-  hipLaunchKernelGGL((k_igemm_fwd<64, 128, 16, 2, 2>), grid, dim3(256), 0, st, a);
+  MSL_LAUNCH((k_igemm_fwd<64, 128, 16, 2, 2>), grid, dim3(256), 0, st, a);
   MSL_CHECK_LAUNCH();
   if (pl.S > 1) {
     const long long n = (long long)M * P;
     const int blocks = (int)std::min<long long>(cdiv(n, 256), 4096);
-    hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, (const float*)ws, pl.S, n,
+    MSL_LAUNCH(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, (const float*)ws, pl.S, n,
                        out, 0, bias, nbias, M, P);
     MSL_CHECK_LAUNCH();
   }
@@ -725,12 +783,12 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
   // fully coalesced rows write faster (ASPP fwd 2048 -> 19: 5.2 vs 9.5 us)
   if (!h3 && (forms_of(forms).pack_form == 0 || m <= 64)) {  // element-wise gather, then a separate split
     const int blocks = (int)std::min<long long>(cdiv(total, 256), 8192);
-    hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
+    MSL_LAUNCH(k_pack, dim3(blocks), dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad,
                        ncb, lda, taps, total, packed);
     MSL_CHECK_LAUNCH();
     if (m > 64) {
       const int ksteps = nbranch * ncb * taps;
-      hipLaunchKernelGGL(k_split_pack, dim3((int)std::min<long long>(cdiv(total, 256), 4096)), dim3(256),
+      MSL_LAUNCH(k_split_pack, dim3((int)std::min<long long>(cdiv(total, 256), 4096)), dim3(256),
                          0, st, packed, ksteps, lda, planes);
       MSL_CHECK_LAUNCH();
     }
@@ -742,17 +800,17 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
   const int split = m > 64 || h3;
   if (taps != 9 && taps != 1) return MSL_ERR_ARG;
   if (h3) {
-    hipLaunchKernelGGL(k_absmax, dim3(kNPart), dim3(256), 0, st, w, (long long)cout * cin * taps, branch_stride,
+    MSL_LAUNCH(k_absmax, dim3(kNPart), dim3(256), 0, st, w, (long long)cout * cin * taps, branch_stride,
                        nbranch, tail);
     MSL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_pack_scale, dim3(1), dim3(64), 0, st, tail);
+    MSL_LAUNCH(k_pack_scale, dim3(1), dim3(64), 0, st, tail);
     MSL_CHECK_LAUNCH();
   }
   if (taps == 9)
-    hipLaunchKernelGGL(k_pack_split<9>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
+    MSL_LAUNCH(k_pack_split<9>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
                        lda, split, packed, planes, tail);
   else
-    hipLaunchKernelGGL(k_pack_split<1>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
+    MSL_LAUNCH(k_pack_split<1>, grid, dim3(256), 0, st, w, branch_stride, cin, cout, for_dgrad, ncb,
                        lda, split, packed, planes, tail);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -871,41 +929,41 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
       a.anpart = an;
       a.bnpart = bn;
       a.rowscale = (an == cout && bn == cin) ? 1 : 0;
-      hipLaunchKernelGGL(k_split_rows<MT>, dim3(pl.lda / kSplitRowsR, cdiv(pl.KS, 16)), dim3(256), 0, st, dy, cout, P,
+      MSL_LAUNCH(k_split_rows<MT>, dim3(pl.lda / kSplitRowsR, cdiv(pl.KS, 16)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, ap, an, a.rowscale);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL((k_wgrad_x6<MT>), grid, block, 0, st, a);
+      MSL_LAUNCH((k_wgrad_x6<MT>), grid, block, 0, st, a);
     } else {
-      hipLaunchKernelGGL(k_split_rows<kMathX6>, dim3(pl.lda / kSplitRowsR, cdiv(pl.KS, 16)), dim3(256), 0, st, dy, cout, P,
+      MSL_LAUNCH(k_split_rows<kMathX6>, dim3(pl.lda / kSplitRowsR, cdiv(pl.KS, 16)), dim3(256), 0, st, dy, cout, P,
                          pl.KS, pl.lda, planes, (const float*)nullptr, 0);
       MSL_CHECK_LAUNCH();
-      hipLaunchKernelGGL(k_wgrad_x6<kMathX6>, grid, block, 0, st, a);
+      MSL_LAUNCH(k_wgrad_x6<kMathX6>, grid, block, 0, st, a);
     }
     MSL_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
+    MSL_LAUNCH((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
   } else if (pl.bm == 128) {
-    hipLaunchKernelGGL((k_wgrad_sk<128, 128, 2, 2, 2, MB>), grid, block, 0, st, a);
+    MSL_LAUNCH((k_wgrad_sk<128, 128, 2, 2, 2, MB>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
+    MSL_LAUNCH((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
   } else if (pl.bm == 64) {
-    hipLaunchKernelGGL((k_wgrad_sk<64, 64, 2, 2, 2, MS>), grid, block, 0, st, a);
+    MSL_LAUNCH((k_wgrad_sk<64, 64, 2, 2, 2, MS>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
     // few tiles with many pieces each (the 33k-px 1x1 gradients: 4 tiles x ~128 pieces): 8 threads
     // per output float4 (k_wsk_reduce_wide) instead of one serial chain of every piece
     const long long pieces = cdiv((long long)pl.nw, std::max(1LL, pl.T / pl.KS));  // per (tile, tap)
     if ((long long)rgrid.x * rgrid.y < 256 && pieces >= 16)
-      hipLaunchKernelGGL((k_wsk_reduce_wide<64, 64, 8>), dim3(cdiv((long long)64 * 64 / 4 * taps, 32), rgrid.y), rblock,
+      MSL_LAUNCH((k_wsk_reduce_wide<64, 64, 8>), dim3(cdiv((long long)64 * 64 / 4 * taps, 32), rgrid.y), rblock,
                          0, st, a);
     else
-      hipLaunchKernelGGL((k_wsk_reduce<64, 64>), rgrid, rblock, 0, st, a);
+      MSL_LAUNCH((k_wsk_reduce<64, 64>), rgrid, rblock, 0, st, a);
   } else {
-    hipLaunchKernelGGL((k_wgrad_sk<32, 128, 2, 1, 4, MS>), grid, block, 0, st, a);
+    MSL_LAUNCH((k_wgrad_sk<32, 128, 2, 1, 4, MS>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_wsk_reduce<32, 128>), rgrid, rblock, 0, st, a);
+    MSL_LAUNCH((k_wsk_reduce<32, 128>), rgrid, rblock, 0, st, a);
   }
   MSL_CHECK_LAUNCH();
   if (dbias) {
-    hipLaunchKernelGGL(k_bias_grad, dim3(cout), dim3(256), 0, st, dy, P, dbias, cout, nbranch,
+    MSL_LAUNCH(k_bias_grad, dim3(cout), dim3(256), 0, st, dy, P, dbias, cout, nbranch,
                        accumulate);
     MSL_CHECK_LAUNCH();
   }
@@ -945,12 +1003,20 @@ int msl_forms_default(msl_forms* out) {
 
 int msl_forms_check(const msl_forms* forms) { return forms_bad(forms) ? MSL_ERR_ARG : MSL_OK; }
 
+int msl_launch_guard_probe(int threads, float* out, msl_stream_t stream) {
+  if (threads < 1 || !out) return MSL_ERR_ARG;
+  MSL_LAUNCH(k_guard_probe, dim3(1), dim3(threads), 0, as_stream(stream), out);
+  MSL_CHECK_LAUNCH();
+  return MSL_OK;
+}
+
 const char* msl_status_string(int status) {
   switch (status) {
     case MSL_OK: return "ok";
     case MSL_ERR_SHAPE: return "invalid shape";
     case MSL_ERR_WORKSPACE: return "workspace too small";
     case MSL_ERR_ARG: return "invalid argument";
+    case MSL_ERR_LAUNCH: return "block exceeds the kernel's launch bounds";
     default: return status > 0 ? hipGetErrorString((hipError_t)status) : "unknown error";
   }
 }
@@ -983,21 +1049,21 @@ int msl_conv_pack_many(const msl_pack_job* jobs, const long long* block_start, i
   const int h3 = forms_of(forms).f32_form == kMathH3P;
   if (h3) {  // the weights' absmax partials first (jobs with M > 64: the split packs)
     if (taps == 9)
-      hipLaunchKernelGGL(k_absmax_jobs<9>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
+      MSL_LAUNCH(k_absmax_jobs<9>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
     else
-      hipLaunchKernelGGL(k_absmax_jobs<1>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
+      MSL_LAUNCH(k_absmax_jobs<1>, dim3(kNPart, (unsigned)njobs), dim3(256), 0, st, jobs);
     MSL_CHECK_LAUNCH();
     if (taps == 9)
-      hipLaunchKernelGGL(k_pack_scale_jobs<9>, dim3((unsigned)njobs), dim3(64), 0, st, jobs);
+      MSL_LAUNCH(k_pack_scale_jobs<9>, dim3((unsigned)njobs), dim3(64), 0, st, jobs);
     else
-      hipLaunchKernelGGL(k_pack_scale_jobs<1>, dim3((unsigned)njobs), dim3(64), 0, st, jobs);
+      MSL_LAUNCH(k_pack_scale_jobs<1>, dim3((unsigned)njobs), dim3(64), 0, st, jobs);
     MSL_CHECK_LAUNCH();
   }
   if (taps == 9)
-    hipLaunchKernelGGL(k_pack_split_many<9>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs,
+    MSL_LAUNCH(k_pack_split_many<9>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs,
                        h3);
   else
-    hipLaunchKernelGGL(k_pack_split_many<1>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs,
+    MSL_LAUNCH(k_pack_split_many<1>, dim3((unsigned)total_blocks), dim3(256), 0, st, jobs, block_start, njobs,
                        h3);
   MSL_CHECK_LAUNCH();
   return MSL_OK;

@@ -518,25 +518,32 @@ __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane,
   mid();
 }
 
-// The BD stage with the image operand pre-split (k_split_img): braw holds the lane's hi plane (floats
-// 0..3 as 16 B) and lo plane (4..7), already scaled; no split work in the loop.
-template <int TM, int BM, bool HI_ONLY, typename F>
-__device__ __forceinline__ void mfma_stage_hdp(const float* As, int wm, int lane, f32x16 (&acc)[TM][1],
-                                               F&& mid, const float (&braw)[8]) {
+// The BD stage with the image operand pre-split (k_split_img): braw[8 j ..] holds the lane's hi plane
+// (floats 0..3 as 16 B) and lo plane (4..7) of pixel column j, already scaled; no split work in the loop.
+// TN = 1: the 1 x 4 wave layout (128 rows x 32 pixels per wave); TN = 2: the 2 x 2 layout (r06, 64 rows x
+// 64 pixels per wave: half the A-fragment LDS reads per MFMA).
+template <int TM, int TN, int BM, bool HI_ONLY, typename F>
+__device__ __forceinline__ void mfma_stage_hdp(const float* As, int wm, int lane, f32x16 (&acc)[TM][TN],
+                                               F&& mid, const float (&braw)[8 * TN]) {
   const int l32 = lane & 31, h = lane >> 5;
   const f16x8* Ab = reinterpret_cast<const f16x8*>(As);
-  union { float f[4]; f16x8 h; } bh, bl;
+  union { float f[4]; f16x8 h; } bh[TN], bl[TN];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    bh.f[j] = braw[j];
-    bl.f[j] = braw[4 + j];
-  }
+  for (int t = 0; t < TN; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh[t].f[j] = braw[8 * t + j];
+      bl[t].f[j] = braw[8 * t + 4 + j];
+    }
   if constexpr (HI_ONLY) {
     f16x8 av[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bh.h, acc[i][0], 0, 0, 0);
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bh[t].h, acc[i][t], 0, 0, 0);
   } else {
     Split2h av[TM];
 #pragma unroll
@@ -544,11 +551,20 @@ __device__ __forceinline__ void mfma_stage_hdp(const float* As, int wm, int lane
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bh.h, acc[i][0], 0, 0, 0);
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bl.h, acc[i][0], 0, 0, 0);
+      for (int t = 0; t < TN; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bh[t].h, acc[i][t], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bh.h, acc[i][0], 0, 0, 0);
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bl[t].h, acc[i][t], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bh[t].h, acc[i][t], 0, 0, 0);
   }
   mid();
 }
@@ -906,13 +922,19 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   static_assert(BN % 64 == 0 && BM % 32 == 0, "tiles");
+  // r05: 256- and 384-row tiles of the LDS form computed wrong results from the first row on
+  // (profiles/r05_aspp_384_tile_attempt.txt); no such form may be instantiated until the cause is fixed
+  static_assert(BM <= 128, "fwd_sk_body: tiles over 128 rows are not a validated form");
   constexpr bool H1 = MT == kMathH1P;                                 // fp16: the hi plane only
   constexpr bool H3 = MT == kMathH3P || H1;                           // f16x3: two fp16 planes
   constexpr bool APRE = MT == kMathX6P || H3;  // A from pre-split planes
   constexpr int NQ = H3 ? 4 : 6;  // (plane, k half) blocks of one pre-split K-step in the pack
   constexpr int NQL = H1 ? 2 : NQ;  // of them staged (fp16 math: plane 0's two halves)
   static_assert(!APRE || BM % 64 == 0, "pre-split A: 64-row DMA pieces");
-  static_assert(!BD || (H3 && G == 1 && WM == 1 && WN == 4 && TN == 1 && STAGES == 4), "BD form");
+  // BD: 1 x 4 waves (128 rows x 32 pixels each); the pre-split image (BP) also in 2 x 2 waves (64 x 64, r06)
+  static_assert(!BD || (H3 && G == 1 && STAGES == 4 &&
+                        ((WM == 1 && WN == 4 && TN == 1) || (BP && WM == 2 && WN == 2 && TM == 2 && TN == 2))),
+                "BD form");
   constexpr int A_STAGE = APRE ? G * 4 * NQL * BM : BK * BM;
   constexpr int STAGE = A_STAGE + (BD ? 0 : BK * BN);
   constexpr int A_ROWS_PER_INST = 256 / BM;
@@ -925,7 +947,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   constexpr int BG_INST_W = PW ? kCB * BN / 256 / 4 : kCB * NH / 4;  // B DMAs per wave per K-step
   static_assert(!PW || BN == 128, "pointwise B rows: two rows of 128 pixels per dwordx4 instruction");
   static_assert(!BP || BD, "BP: the BD form with a pre-split image");
-  constexpr int INST_W = A_INST_W + G * (BP ? (H1 ? 1 : 2) : BD ? 8 : BG_INST_W);
+  constexpr int INST_W = A_INST_W + G * (BP ? (H1 ? 1 : 2) * TN : BD ? 8 : BG_INST_W);
   static_assert(AHALF || A_INST % 4 == 0, "A instructions split evenly over waves");
   static_assert(!AHALF || (G == 1 && BM == 64), "half-wave A pieces: one K-step of 64 rows per stage");
   static_assert((STAGES - 2) * INST_W < 64, "vmcnt range");
@@ -1033,10 +1055,17 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
     // offsets (OOB outside the image) are recomputed only when the tap changes.
     int c_cb, c_tap = -1;
     unsigned vrow[NH];
-    unsigned vbd = OOB;   // BD: this lane's shifted pixel byte offset (OOB outside the image)
-    unsigned vbdh = OOB;  // BD, full channel blocks: + the lane's channel half (8 * (lane >> 5) rows)
-    const int pbd = n0 + wn + (lane & 31);
-    const int pqd = pbd / a.W, pxd = pbd - pqd * a.W, pyd = pqd % a.H;
+    unsigned vbd[TN];     // BD: this lane's shifted pixel byte offset per column (OOB outside the image)
+    unsigned vbdh = OOB;  // BD (TN = 1), full channel blocks: + the lane's channel half (8 * (lane >> 5) rows)
+    int pbd[TN], pxd[TN], pyd[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      vbd[j] = OOB;
+      pbd[j] = n0 + wn + j * 32 + (lane & 31);
+      const int pqd = pbd[j] / a.W;
+      pxd[j] = pbd[j] - pqd * a.W;
+      pyd[j] = pqd % a.H;
+    }
     {
       // wave-uniform: the cursor lives in scalar registers (it feeds the scalar channel offsets)
       const int ks0 = __builtin_amdgcn_readfirstlane(k_a * G);
@@ -1051,9 +1080,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       const int dh = (tp / 3 - 1) * d, dw = (tp % 3 - 1) * d;
       const int shift = dh * a.W + dw;
       if constexpr (BD) {
-        const bool v = pbd < a.P && (unsigned)(pyd + dh) < (unsigned)a.H && (unsigned)(pxd + dw) < (unsigned)a.W;
-        vbd = v ? (unsigned)((pbd + shift) * (BP ? 16 : 4)) : OOB;
-        vbdh = v ? vbd + (unsigned)(8 * (lane >> 5)) * chan_bytes : OOB;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const bool v = pbd[j] < a.P && (unsigned)(pyd[j] + dh) < (unsigned)a.H &&
+                         (unsigned)(pxd[j] + dw) < (unsigned)a.W;
+          vbd[j] = v ? (unsigned)((pbd[j] + shift) * (BP ? 16 : 4)) : OOB;
+        }
+        vbdh = vbd[0] != OOB ? vbd[0] + (unsigned)(8 * (lane >> 5)) * chan_bytes : OOB;
       } else {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
@@ -1063,12 +1096,12 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       }
     };
     set_tap(c_tap);
-    float bdq[4][8];  // BD: the register ring of B values (K-step i in slot i % 4)
-    float bdv[4];     // PROF & 16: the ring's pixel validity (+inf / 0) and channel blocks
+    float bdq[4][8 * TN];  // BD: the register ring of B values (K-step i in slot i % 4; 8 per column)
+    float bdv[4];          // PROF & 16: the ring's pixel validity (+inf / 0) and channel blocks
     int bdc[4];
     // part 1: stage s's A pieces into LDS slot `slot`; part 2: its B operand (ring entry bq, or LDS),
     // advancing the cursor; 3: both
-    auto issue = [&](int s, int slot, float (&bq)[8], float& bv, int& bc, int part = 3) {
+    auto issue = [&](int s, int slot, float (&bq)[8 * TN], float& bv, int& bc, int part = 3) {
       float* As = smem + slot * STAGE;
       float* Bs = As + A_STAGE;
       if (!(part & 1)) {
@@ -1106,10 +1139,13 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
 #pragma unroll
           for (int q = 0; q < NPB; ++q) {
             const unsigned row = (unsigned)((c_cb * NPB + q) * 2 + (lane >> 5)) * pl_bytes;
-            union { u32x4 u; float f[4]; } c;
-            c.u = __builtin_amdgcn_raw_buffer_load_b128(rbx, vbd + row, 0, 0);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bq[4 * q + j] = c.f[j];
+            for (int t = 0; t < TN; ++t) {
+              union { u32x4 u; float f[4]; } c;
+              c.u = __builtin_amdgcn_raw_buffer_load_b128(rbx, vbd[t] + row, 0, 0);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) bq[8 * t + 4 * q + j] = c.f[j];
+            }
           }
         } else if constexpr (BD) {
           // channels cb16 + 8h + j of this lane's pixel.  The BD form runs only with every 16-channel
@@ -1190,7 +1226,8 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
       // vmcnt(2 * INST_W) - a wave now and then read a stage's A slot before another wave's DMA piece
       // had landed; scripts/dbg_det.py, profiles/r04_bd_wait_race.txt).  The B registers are waited
       // for by the compiler at their use.
-      auto step = [&](int i, float (&cur)[8], float (&nxt)[8], float& curv, float& nxtv, int& curc, int& nxtc) {
+      auto step = [&](int i, float (&cur)[8 * TN], float (&nxt)[8 * TN], float& curv, float& nxtv, int& curc,
+                      int& nxtc) {
         unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
         if constexpr (PROF & 1) t0 = sk_stamp();
         wait_vmcnt<2 * A_INST_W>();
@@ -1205,7 +1242,7 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         const float* As = lds_after_barrier(smem) + (i % STAGES) * STAGE;
         auto mid = [&] { issue(k_a + i + STAGES - 1, (i + STAGES - 1) % STAGES, nxt, nxtv, nxtc, 1); };
         if constexpr (BP) {
-          mfma_stage_hdp<TM, BM, H1>(As, wm, lane, acc, mid, cur);
+          mfma_stage_hdp<TM, TN, BM, H1>(As, wm, lane, acc, mid, cur);
         } else if constexpr ((PROF & 16) != 0) {
           const float4* tq = reinterpret_cast<const float4*>(tabp + (curc * 2 + (lane >> 5)) * 16);
           const float4 a0 = tq[0], a1 = tq[1], b0 = tq[2], b1 = tq[3];
@@ -1843,7 +1880,10 @@ template <int MT = kMathX6>
 __global__ void __launch_bounds__(256) k_split_rows(const float* __restrict__ src, int M, int P, int KS, int lda,
                                                      bf16x8* __restrict__ planes, const float* __restrict__ part,
                                                      int npart, int rowscale = 0) {
-  constexpr int R = kSplitRowsR, PX = 256, LDP = PX + 8;  // rows, pixels per block; LDS row stride (16-bit terms)
+  // LDS row stride (16-bit terms): 272 = 136 dwords, 8 mod 64, so the 16-B reads of a 16-lane group - rows r
+  // of one k half and rows of the other, 16 B further - land on distinct bank slots (2r + h mod 16); r05 had
+  // 264 (4 mod 64), where k half 1 of row r met row r + 1: 25 % of the kernel's LDS cycles were conflicts
+  constexpr int R = kSplitRowsR, PX = 256, LDP = PX + 16;  // rows, pixels per block
   constexpr int KB = PX / kWx6BK;                // K-steps per block
   constexpr bool F16 = MT == kMathH3P || MT == kMathH1P;
   constexpr int NP = MT == kMathH1P ? 1 : F16 ? 2 : 3;
@@ -1932,7 +1972,12 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
   constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
   constexpr int RB = 128 * 16 + 32;   // bytes per (plane, k half) block of 128 rows, padded
   constexpr int KVB = 2 * NP * RB;    // one K-step's B planes
-  constexpr int STAGEB = 2 * KVB;     // two K-steps
+  // the second K-step of a stage starts 64 B past a multiple of 128 B (r06): a 16-lane group of the 8-B
+  // plane stores holds both K-steps of two rows, and at f16x3's KVB (8320 B = 0 mod 128) the two K-steps
+  // hit the same 16 banks - 2-way conflicts on every store, 34 % of the kernel's LDS cycles
+  // (profiles/r05_wgrad_sq_final.txt); at 64 mod 128 they take the other 16
+  constexpr int KVS = KVB + (192 - KVB % 128) % 128;
+  constexpr int STAGEB = 2 * KVS;     // two K-steps
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   // + (r05) the segment's border-mask table: 16 bits per K-step, kWxMaskTab K-steps
@@ -1973,7 +2018,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
   // this thread's B chunks: c = tid + 256 i -> row c / 8, chunk c % 8 (4 pixels) of the stage's 32
   const int cc = tid & 7;
   const int ck = cc >> 2, chh = (cc >> 1) & 1, cq = cc & 1;  // K-step, k half, quarter
-  const int wofs = ck * KVB + chh * RB + (tid >> 3) * 16 + cq * 8;  // + q*2*RB + i*32*16
+  const int wofs = ck * KVS + chh * RB + (tid >> 3) * 16 + cq * 8;  // + q*2*RB + i*32*16
 
   f32x16 acc[TM][TN];
   for (int it = it_begin; it < it_end;) {
@@ -2265,7 +2310,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
       __builtin_amdgcn_sched_barrier(0);  // (left to itself the compiler sinks a B load past the MFMAs)
       compute(Bs, A0);
       loadA(A0, ks + 2);
-      compute(Bs + KVB, A1);
+      compute(Bs + KVS, A1);
       ks += 2;
       storeB((s + 1) & 1, rbv, rmb, rsh);
       __syncthreads();

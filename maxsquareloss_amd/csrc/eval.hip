@@ -49,7 +49,7 @@ int msl_confusion_accumulate(const float* pred, const long long* label, int c, l
                              unsigned long long* confusion, int* argmax_out, msl_stream_t stream) {
   if (!pred || !label || !confusion || c < 1 || c > kEvalMaxClasses || p < 1) return MSL_ERR_ARG;
   const int blocks = (int)std::min<long long>((p + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_confusion, dim3(blocks), dim3(256), 0, as_stream(stream), pred, label, c, p,
+  MSL_LAUNCH(k_confusion, dim3(blocks), dim3(256), 0, as_stream(stream), pred, label, c, p,
                      confusion, argmax_out);
   MSL_CHECK_LAUNCH();
   return MSL_OK;

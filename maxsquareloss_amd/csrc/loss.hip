@@ -673,10 +673,10 @@ static int loss_fwd(const float* L1, const float* L2, const int64_t* labels, int
   const int rec = rec_len(c);
   const int nblk = std::min(kFwdBlocks, cdiv((long long)ho * wo, 256));
   MSL_DISPATCH_C(c, CM,
-                 hipLaunchKernelGGL((k_loss_fwd<KIND, CM>), dim3(nblk), dim3(256), 0, st, L1, L2,
+                 MSL_LAUNCH((k_loss_fwd<KIND, CM>), dim3(nblk), dim3(256), 0, st, L1, L2,
                                     labels, g, thr, part, rec));
   MSL_CHECK_LAUNCH();
-  hipLaunchKernelGGL((k_loss_finalize<KIND>), dim3(1), dim3(256), 0, st, part, nblk, rec, c,
+  MSL_LAUNCH((k_loss_finalize<KIND>), dim3(1), dim3(256), 0, st, part, nblk, rec, c,
                      ho * wo, ratio, out, stats, hist, weights);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -696,12 +696,12 @@ static int loss_bwd(const float* L1, const float* L2, const int64_t* labels, con
   MSL_DISPATCH_C(c, CM, {
     auto kern = k_bwd_rows<KIND, CM>;
     if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(ho, rows_chunks(g)), dim3(256), lds, st, L1, L2, labels, gin_hi, g, thr,
+    MSL_LAUNCH(kern, dim3(ho, rows_chunks(g)), dim3(256), lds, st, L1, L2, labels, gin_hi, g, thr,
                        stats, gout, T, rows_wmax(g));
   });
   MSL_CHECK_LAUNCH();
   const int n = c * hi * wi;
-  hipLaunchKernelGGL(k_bwd_cols, dim3(std::min(cdiv(n, 256), 2048)), dim3(256), 0, st,
+  MSL_LAUNCH(k_bwd_cols, dim3(std::min(cdiv(n, 256), 2048)), dim3(256), 0, st,
                      (const float*)T, g, dlow);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -727,7 +727,7 @@ int msl_upsample_fwd(const float* in, float* out, int c, int hi, int wi, int ho,
   const Geo g = make_geo(c, hi, wi, ho, wo);
   const long long n = (long long)c * ho * ((wo + 3) / 4);
   const int blocks = (int)std::min<long long>(cdiv(n, 256), 8192);
-  hipLaunchKernelGGL(k_upsample_fwd, dim3(blocks), dim3(256), 0, as_stream(stream), in, g, out);
+  MSL_LAUNCH(k_upsample_fwd, dim3(blocks), dim3(256), 0, as_stream(stream), in, g, out);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
@@ -811,7 +811,7 @@ int msl_loss_labels_up(const float* logits1, const float* logits2, int c, int hi
   const Geo g = make_geo(c, hi, wi, ho, wo);
   const int nblk = std::min(4096, cdiv((long long)ho * wo, 256));
   MSL_DISPATCH_C(c, CM,
-                 hipLaunchKernelGGL((k_loss_labels<CM>), dim3(nblk), dim3(256), 0, as_stream(stream),
+                 MSL_LAUNCH((k_loss_labels<CM>), dim3(nblk), dim3(256), 0, as_stream(stream),
                                     logits1, logits2, g, thr, argmax1, label2));
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -826,12 +826,12 @@ int msl_maxsquare_prob_fwd(const float* prob, int c, int hw, float* out, void* w
   const int rec = rec_len(c);
   float* part = (float*)ws;
   MSL_DISPATCH_C(c, CM,
-                 hipLaunchKernelGGL((k_prob_fwd<0, CM>), dim3(nblk), dim3(256), 0, st, prob,
+                 MSL_LAUNCH((k_prob_fwd<0, CM>), dim3(nblk), dim3(256), 0, st, prob,
                                     (const int64_t*)nullptr, c, hw, part, rec));
   MSL_CHECK_LAUNCH();
   // MS finalize: -sum / (2*C*hw); stats scratch lives after the partials
   float* stats = part + (size_t)nblk * rec;
-  hipLaunchKernelGGL((k_loss_finalize<K_MS>), dim3(1), dim3(256), 0, st, (const float*)part, nblk,
+  MSL_LAUNCH((k_loss_finalize<K_MS>), dim3(1), dim3(256), 0, st, (const float*)part, nblk,
                      rec, c, hw, 0.f, out, stats, (int32_t*)nullptr, (float*)nullptr);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -841,7 +841,7 @@ int msl_maxsquare_prob_bwd(const float* prob, int c, int hw, const float* gout, 
                            msl_stream_t stream) {
   if (!prob || !gout || !dprob || c < 1 || c > kMaxC || hw < 1) return MSL_ERR_ARG;
   MSL_DISPATCH_C(c, CM,
-                 hipLaunchKernelGGL((k_prob_bwd<0, CM>), dim3(std::min(cdiv(hw, 256), 4096)),
+                 MSL_LAUNCH((k_prob_bwd<0, CM>), dim3(std::min(cdiv(hw, 256), 4096)),
                                     dim3(256), 0, as_stream(stream), prob, c, hw,
                                     (const float*)nullptr, gout, dprob));
   MSL_CHECK_LAUNCH();
@@ -858,11 +858,11 @@ int msl_iw_maxsquare_prob_fwd(const float* prob, const int64_t* label, int c, in
   const int rec = rec_len(c);
   float* part = (float*)ws;
   MSL_DISPATCH_C(c, CM,
-                 hipLaunchKernelGGL((k_prob_fwd<1, CM>), dim3(nblk), dim3(256), 0, st, prob, label,
+                 MSL_LAUNCH((k_prob_fwd<1, CM>), dim3(nblk), dim3(256), 0, st, prob, label,
                                     c, hw, part, rec));
   MSL_CHECK_LAUNCH();
   float* stats = part + (size_t)nblk * rec;
-  hipLaunchKernelGGL((k_loss_finalize<K_IW>), dim3(1), dim3(256), 0, st, (const float*)part, nblk,
+  MSL_LAUNCH((k_loss_finalize<K_IW>), dim3(1), dim3(256), 0, st, (const float*)part, nblk,
                      rec, c, hw, ratio, out, stats, hist, weights);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -872,7 +872,7 @@ int msl_iw_maxsquare_prob_bwd(const float* prob, int c, int hw, const float* wei
                               const float* gout, float* dprob, msl_stream_t stream) {
   if (!prob || !weights || !gout || !dprob || c < 1 || c > kMaxC || hw < 1) return MSL_ERR_ARG;
   MSL_DISPATCH_C(c, CM,
-                 hipLaunchKernelGGL((k_prob_bwd<1, CM>), dim3(std::min(cdiv(hw, 256), 4096)),
+                 MSL_LAUNCH((k_prob_bwd<1, CM>), dim3(std::min(cdiv(hw, 256), 4096)),
                                     dim3(256), 0, as_stream(stream), prob, c, hw, weights, gout,
                                     dprob));
   MSL_CHECK_LAUNCH();

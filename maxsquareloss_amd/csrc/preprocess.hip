@@ -109,10 +109,10 @@ int msl_image_transform(const uint8_t* rgb, int h, int w, int mirror, float mean
   const bool vec = (w % 4) == 0 && (reinterpret_cast<uintptr_t>(rgb) & 3) == 0 &&
                    (reinterpret_cast<uintptr_t>(out) & 15) == 0;
   if (vec)
-    hipLaunchKernelGGL(k_image_transform_x4, dim3(blocks_for(hw / 4)), dim3(256), 0, as_stream(stream), rgb, h,
+    MSL_LAUNCH(k_image_transform_x4, dim3(blocks_for(hw / 4)), dim3(256), 0, as_stream(stream), rgb, h,
                        w, mirror ? 1 : 0, mean_b, mean_g, mean_r, out);
   else
-    hipLaunchKernelGGL(k_image_transform, dim3(blocks_for(hw)), dim3(256), 0, as_stream(stream), rgb, h, w,
+    MSL_LAUNCH(k_image_transform, dim3(blocks_for(hw)), dim3(256), 0, as_stream(stream), rgb, h, w,
                        mirror ? 1 : 0, mean_b, mean_g, mean_r, out);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -125,10 +125,10 @@ int msl_label_transform(const uint8_t* ids, int h, int w, int mirror, const int3
   const bool vec = (w % 4) == 0 && (reinterpret_cast<uintptr_t>(ids) & 3) == 0 &&
                    (reinterpret_cast<uintptr_t>(out) & 15) == 0;
   if (vec)
-    hipLaunchKernelGGL(k_label_transform_x4, dim3(blocks_for(hw / 4)), dim3(256), 0, as_stream(stream), ids, h,
+    MSL_LAUNCH(k_label_transform_x4, dim3(blocks_for(hw / 4)), dim3(256), 0, as_stream(stream), ids, h,
                        w, mirror ? 1 : 0, lut256, out);
   else
-    hipLaunchKernelGGL(k_label_transform, dim3(blocks_for(hw)), dim3(256), 0, as_stream(stream), ids, h, w,
+    MSL_LAUNCH(k_label_transform, dim3(blocks_for(hw)), dim3(256), 0, as_stream(stream), ids, h, w,
                        mirror ? 1 : 0, lut256, out);
   MSL_CHECK_LAUNCH();
   return MSL_OK;

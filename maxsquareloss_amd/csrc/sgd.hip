@@ -82,7 +82,7 @@ int msl_sgd_step(const msl_sgd_entry* entries, const int32_t* block_entry,
   if (!entries || !block_entry || !block_offset || n_blocks < 0 || n_blocks > 0x7fffffff)
     return MSL_ERR_ARG;
   if (n_blocks == 0) return MSL_OK;
-  hipLaunchKernelGGL(k_sgd, dim3((unsigned)n_blocks), dim3(256), 0, as_stream(stream), entries,
+  MSL_LAUNCH(k_sgd, dim3((unsigned)n_blocks), dim3(256), 0, as_stream(stream), entries,
                      block_entry, block_offset, lr0, lr1, (const float*)nullptr, momentum, weight_decay,
                      grad_scale);
   MSL_CHECK_LAUNCH();
@@ -95,7 +95,7 @@ int msl_sgd_step_lr_dev(const msl_sgd_entry* entries, const int32_t* block_entry
   if (!entries || !block_entry || !block_offset || !lr_dev || n_blocks < 0 || n_blocks > 0x7fffffff)
     return MSL_ERR_ARG;
   if (n_blocks == 0) return MSL_OK;
-  hipLaunchKernelGGL(k_sgd, dim3((unsigned)n_blocks), dim3(256), 0, as_stream(stream), entries,
+  MSL_LAUNCH(k_sgd, dim3((unsigned)n_blocks), dim3(256), 0, as_stream(stream), entries,
                      block_entry, block_offset, 0.f, 0.f, lr_dev, momentum, weight_decay, grad_scale);
   MSL_CHECK_LAUNCH();
   return MSL_OK;

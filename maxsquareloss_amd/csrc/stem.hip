@@ -186,7 +186,7 @@ int msl_im2col(const float* x, int c, int h, int w, int nimg, int kh, int kw, in
     return MSL_ERR_ARG;
   const int K = c * kh * kw;
   const long long n = (long long)K * nimg * ho * ((wo + 3) / 4);
-  hipLaunchKernelGGL(k_im2col, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, nimg, kh, kw, stride, pad,
+  MSL_LAUNCH(k_im2col, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, nimg, kh, kw, stride, pad,
                      dil, ho, wo, K, col);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -198,7 +198,7 @@ int msl_col2im(const float* col, int c, int h, int w, int nimg, int kh, int kw, 
       kw < 1 || dil < 1 || (long long)nimg * ho * wo >= (1LL << 31))
     return MSL_ERR_ARG;
   const long long n = (long long)c * nimg * h * w;
-  hipLaunchKernelGGL(k_col2im, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), col, c, h, w, nimg, kh, kw, stride,
+  MSL_LAUNCH(k_col2im, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), col, c, h, w, nimg, kh, kw, stride,
                      pad, dil, ho, wo, x);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -210,7 +210,7 @@ int msl_maxpool_fwd(const float* x, int c, int h, int w, int k, int stride, int 
   // every window must start inside the image (torch: the last window starts before h + pad)
   if ((long long)(ho - 1) * stride - pad >= h || (long long)(wo - 1) * stride - pad >= w) return MSL_ERR_SHAPE;
   const long long n = (long long)c * ho * wo;
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, k, stride, pad, ho,
+  MSL_LAUNCH(k_maxpool_fwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, k, stride, pad, ho,
                      wo, n, y, idx);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -220,7 +220,7 @@ int msl_maxpool_bwd(const float* dy, const int32_t* idx, int c, int h, int w, in
                     int wo, float* dx, msl_stream_t stream) {
   if (!dy || !idx || !dx || bad_geom(c, h, w, k, stride, pad, ho, wo) || 2 * pad > k) return MSL_ERR_ARG;
   const long long n = (long long)c * h * w;
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, idx, h, w, k, stride,
+  MSL_LAUNCH(k_maxpool_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, idx, h, w, k, stride,
                      pad, ho, wo, n, dx);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -231,7 +231,7 @@ int msl_subsample(const float* x, int c, int h, int w, int stride, int ho, int w
       (long long)(wo - 1) * stride >= w)
     return MSL_ERR_ARG;
   const long long n = (long long)c * ho * wo;
-  hipLaunchKernelGGL(k_subsample, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, stride, ho, wo, n, y);
+  MSL_LAUNCH(k_subsample, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, stride, ho, wo, n, y);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
@@ -240,7 +240,7 @@ int msl_subsample_bwd(const float* dy, int c, int h, int w, int stride, int ho, 
                       msl_stream_t stream) {
   if (!dy || !dx || bad_geom(c, h, w, 1, stride, 0, ho, wo)) return MSL_ERR_ARG;
   const long long n = (long long)c * h * w;
-  hipLaunchKernelGGL(k_subsample_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, h, w, stride, ho, wo,
+  MSL_LAUNCH(k_subsample_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, h, w, stride, ho, wo,
                      n, dx);
   MSL_CHECK_LAUNCH();
   return MSL_OK;

@@ -107,6 +107,7 @@ SIGNATURES = {
     "msl_sgd_plan": (c_ll, [c_p, c_int, c_p, c_p, c_ll]),
     "msl_sgd_step": (c_int, [c_p, c_p, c_p, c_ll, c_f, c_f, c_f, c_f, c_f, c_p]),
     "msl_sgd_step_lr_dev": (c_int, [c_p, c_p, c_p, c_ll, c_p, c_f, c_f, c_f, c_p]),
+    "msl_launch_guard_probe": (c_int, [c_int, c_p, c_p]),
 }
 
 ABI_VERSION = 3

@@ -163,6 +163,76 @@ def conv_f16(wgrad_rounds):
     return conv
 
 
+def _split_gemm_rounds(m, n, ntap, p, row):
+    """Whether a weight-gradient GEMM dW[m][n][tap] = sum_p dY[m][p] X[n][p + shift] of the fp16 path runs on
+    the split kernel (both operands rounded to fp16, one power-of-two scale per row) rather than the exact
+    bf16x6 one.  The rule DESIGN.md §3.3 states for k_wgrad_x6: 128 x 128 tiles, so at least 128 rows on
+    both sides; 16-pixel K-steps whose image-border masks handle one row wrap, so image rows of at least 16
+    pixels (a pointwise call passes the whole pixel axis as one row); and either at least 256 channels on
+    both sides or chunked split-K items - (tile, pixel chunk) pairs of >= 8 K-steps, <= 4096 items - that
+    fill at least 75 % of the 512 resident workgroups in their last round."""
+    if m < 128 or n < 128 or row < 16:
+        return False
+    ntiles = -(-m // 128) * -(-n // 128) * ntap
+    ks = -(-p // 16)
+    best = 0.0
+    for c in range(1, ks + 1):
+        if ntiles * c > 4096:
+            break
+        length = -(-ks // c)
+        if length < 8:
+            break
+        items = ntiles * -(-ks // length)
+        fill = items / (-(-items // 512) * 512)
+        if fill > best + 0.01:
+            best = fill
+    return best >= 0.75 or (m >= 256 and n >= 256)
+
+
+def f16_wgrad_rounds(num_classes, nimg=2, aspp_shift=True):
+    """The fp16 emulation's weight-gradient predicate (cin, cout, k, h, w) -> bool for _ConvF16 at the
+    trainer's shapes (image pairs: nimg = 2; h x w = the gradient's map), restated from the design rule
+    (_split_gemm_rounds) instead of asked of the library (r06; tests/test_host.py holds it
+    equal to msl_conv_wgrad_split on every conv of the three config sizes):
+      - 3x3: M = cout, N = cin, 9 taps, rows of w pixels;
+      - 1x1: one flat row of nimg * h * w pixels; with more output than input channels the GEMM runs on
+        swapped operands (the narrower one pre-split), so M = cin, N = cout there - the rule then asks the
+        swapped shape first;
+      - the ASPP heads in the shift form: one pointwise GEMM of 18 * classes rows over the 2048 / 1024-channel
+        map (the 3x3 weight gradient is scattered from it)."""
+    def rounds(cin, cout, k, h, w):
+        p = nimg * h * w
+        if k == 3 and cout == num_classes and aspp_shift:
+            cout, k = 18 * num_classes, 1
+        if k == 1:
+            if cout > cin and _split_gemm_rounds(cin, cout, 1, p, p):
+                return True
+            return _split_gemm_rounds(cout, cin, 1, p, p)
+        return _split_gemm_rounds(cout, cin, 9, p, w)
+    return rounds
+
+
+def conv_calls(H, W, num_classes):
+    """(cin, cout, k, h_out, w_out) of every conv that forward_low runs through its `conv` argument (the stem
+    stays fp32 and is not one of them) for an H x W image, in call order - taken from the model's own forward
+    on the meta device, so the geometry (stride-2 1x1s, ceil-mode pooling) is the model's."""
+    calls = []
+
+    def rec(x, w, b=None, stride=1, padding=0, dilation=1):
+        y = F.conv2d(x, w, b, stride, padding, dilation)
+        calls.append((w.shape[1], w.shape[0], w.shape[2], y.shape[2], y.shape[3]))
+        return y
+    meta = torch.device("meta")
+    params = {n: torch.empty(s, device=meta) for n, s, _ in param_specs(num_classes)}
+    buffers = {}
+    for n in bn_names(num_classes):
+        c = params[n + ".weight"].shape[0]
+        buffers[n + ".running_mean"] = torch.zeros(c, device=meta)
+        buffers[n + ".running_var"] = torch.ones(c, device=meta)
+    forward_low(params, buffers, torch.empty(1, 3, H, W, device=meta), True, rec)
+    return calls
+
+
 # --------------------------------------------------------------------------- forward
 def _bn(x, params, buffers, name, training):
     return F.batch_norm(x, buffers[name + ".running_mean"], buffers[name + ".running_var"],

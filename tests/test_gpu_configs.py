@@ -52,19 +52,11 @@ CFG5 = dict(w=1280, h=760, C=16, mode="IW_maxsquare", multi=True, lt=0.1, math="
 
 def f16_wgrad_policy(num_classes, nimg=2):
     """The oracle's fp16 emulation predicate (oracle.Model f16_wgrad): whether the GPU's weight gradient
-    of a conv (cin, cout, k, h, w) rounds its operands - asked of the library's own plan
-    (msl_conv_wgrad_split) at the trainer's shapes: image pairs (nimg 2), the ASPP heads in the shift
-    form (one pointwise GEMM with 18 * C rows)."""
-    lib = hip.load(require_gpu=False)
-
-    def rounds(cin, cout, k, h, w):
-        if k == 3 and cout == num_classes and ops.ASPP_FORM == "shift":
-            r = lib.msl_conv_wgrad_split(1, 1, cin, 18 * num_classes, h, w, nimg)
-        else:
-            r = lib.msl_conv_wgrad_split(1, 9 if k == 3 else 1, cin, cout, h, w, nimg)
-        assert r in (0, 1), (cin, cout, k, h, w, r)
-        return bool(r)
-    return rounds
+    of a conv (cin, cout, k, h, w) rounds its operands - the oracle's own restatement of the design rule
+    (orc.f16_wgrad_rounds, r06; r05 asked the library's plan, msl_conv_wgrad_split, which the CPU test
+    tests/test_host.py::test_f16_wgrad_predicate_matches_library now holds it to) at the trainer's shapes:
+    image pairs (nimg 2), the ASPP heads in the shift form (one pointwise GEMM with 18 * C rows)."""
+    return orc.f16_wgrad_rounds(num_classes, nimg, aspp_shift=ops.ASPP_FORM == "shift")
 
 
 def _resync(tr, model, opt):

@@ -36,6 +36,22 @@ def _conv_ref(x, w, d, bias=None):
     return F.conv2d(x.double(), w.double(), None if bias is None else bias.double(), padding=d, dilation=d)
 
 
+def test_launch_guard_refuses_oversized_blocks():
+    """MSL_LAUNCH (r06): a block over the kernel's __launch_bounds__ returns MSL_ERR_LAUNCH (-4) and launches
+    nothing; within the bound the kernel runs (the probe kernel is bound to 256 threads)."""
+    from maxsquareloss_amd import hip
+    lib = hip.load()
+    out = torch.full((1024,), -1.0, device=DEV)
+    assert lib.msl_launch_guard_probe(512, out.data_ptr(), hip.stream_ptr()) == -4
+    assert lib.msl_launch_guard_probe(257, out.data_ptr(), hip.stream_ptr()) == -4
+    torch.cuda.synchronize()
+    assert (out == -1).all()
+    assert lib.msl_launch_guard_probe(256, out.data_ptr(), hip.stream_ptr()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out[:256].cpu(), torch.arange(256, dtype=torch.float32))
+    assert (out[256:] == -1).all()
+
+
 @pytest.mark.parametrize("cin,cout,h,w,d", [
     (256, 256, 17, 33, 2), (512, 512, 17, 33, 4), (64, 64, 33, 65, 1), (32, 48, 9, 13, 2),
     (256, 256, 65, 129, 2)])

@@ -37,6 +37,46 @@ def test_library_exports_every_declared_symbol():
     assert set(syms) <= exported
 
 
+def test_every_launch_is_guarded():
+    """every kernel launch in csrc/ goes through MSL_LAUNCH, which checks the block
+    against the kernel's __launch_bounds__ on the host and returns MSL_ERR_LAUNCH instead of launching
+    (tests/test_gpu_ops.py::test_launch_guard_refuses_oversized_blocks runs it on the GPU)."""
+    csrc = os.path.join(ROOT, "maxsquareloss_amd", "csrc")
+    n = 0
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith(".hip"):
+            src = open(os.path.join(csrc, f)).read()
+            assert "hipLaunchKernelGGL" not in src, f
+            n += src.count("MSL_LAUNCH(")
+    assert n >= 80
+    internal = open(os.path.join(csrc, "msl_internal.h")).read()
+    assert internal.count("hipLaunchKernelGGL") == 1 and "launch_guard" in internal
+
+
+@pytest.mark.parametrize("H,W,C", [(512, 1024, 19), (640, 1280, 19), (760, 1280, 16), (380, 640, 16)])
+def test_f16_wgrad_predicate_matches_library(H, W, C):
+    """the fp16 envelope's weight-gradient rounding predicate is the oracle's restatement
+    of the design rule (orc.f16_wgrad_rounds), and it equals the library's own plan (msl_conv_wgrad_split,
+    a pure-host query) on every conv of the model at the config sizes (configs[1..4], the fp16 loss-curve
+    size 640 x 380) - so a wrong plan in the library is caught instead of mirrored."""
+    from oracle import msl_oracle as orc
+    from maxsquareloss_amd import hip
+    lib = hip.load(require_gpu=False)
+    calls = orc.conv_calls(H, W, C)
+    assert len(calls) == 107  # 33 bottlenecks x 3 + 4 downsamples (the stem excluded) + 2 heads x 2 live branches
+    pred = orc.f16_wgrad_rounds(C)
+    n_round = 0
+    for cin, cout, k, h, w in sorted(set(calls)):
+        if k == 3 and cout == C:
+            lib_r = lib.msl_conv_wgrad_split(1, 1, cin, 18 * C, h, w, 2)
+        else:
+            lib_r = lib.msl_conv_wgrad_split(1, 9 if k == 3 else 1, cin, cout, h, w, 2)
+        assert lib_r in (0, 1)
+        assert pred(cin, cout, k, h, w) == bool(lib_r), (cin, cout, k, h, w)
+        n_round += lib_r
+    assert 10 <= n_round <= 21  # most wide convs round; layer1's 64-channel ones never do
+
+
 def test_library_is_gfx950_code_object():
     from maxsquareloss_amd import hip
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", hip.LIB_PATH],
@@ -49,6 +89,7 @@ def test_pure_host_entry_points():
     lib = hip.load(require_gpu=False)
     assert lib.msl_abi_version() == hip.ABI_VERSION
     assert lib.msl_status_string(-2) == b"workspace too small"
+    assert lib.msl_status_string(-4) == b"block exceeds the kernel's launch bounds"
     # packed-weight sizes: [nbranch][ceil(cimg/16)][9][16] rows x round_up(m, 128), x 2.5 for the
     # planes, + the 320-float tail (the f16x3 form's weight absmax partials and scale)
     assert lib.msl_dconv_packed_elems(1, 256, 256, 0) == 16 * 9 * 16 * 256 * 5 // 2 + 320
