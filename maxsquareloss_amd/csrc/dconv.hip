@@ -279,7 +279,17 @@ struct FwdPlan {
   bool sk;
   int G;  // stream-K: K-steps per stage
   int bm, bn, bk, tiles_m, tiles_n, ksteps, kps, S;
+  int bmx;  // r06: the f16x3 pointwise GEMM's wide-tile rows (256; 0 = none), its pieces sized for them
 };
+
+// r06: f16x3 pointwise GEMMs with M a multiple of 256 from kPw256MinM on 256 x 128 tiles, 1 x 4 waves (each 256 rows
+// x 32 pixels, its A fragments streamed row block by row block): the image operand read once per 256 rows.  Same box
+// (profiles/r06_wide_tiles_ab.txt): 512 -> 2048 fwd 109 vs 118 us, 2048 -> 512 dgrad 120 vs 128; at M = 1024 even,
+// at M <= 512 slower (fewer tiles than workers: 1024 -> 256 fwd 54 vs 48, 2048 -> 512 fwd 129 vs 107).  A 384-row
+// tile for the ASPP heads (M = 342: the operand read once instead of three times) needs 192 accumulator registers
+// per lane and spilled 96-188 VGPRs at one or two waves per SIMD: not built.
+constexpr int kPw256MinM = 2048;
+static int wide_rows(int taps, int M) { return taps == 1 && M % 256 == 0 && M >= kPw256MinM ? 256 : 0; }
 
 static int pad_to(int v, int a) { return (v + a - 1) / a * a; }
 
@@ -296,6 +306,7 @@ static FwdPlan plan_fwd(int nbranch, int taps, int cimg, int M, int P, bool has_
   const int groups = nbranch * cdiv(cimg, kCB) * taps;
   const int bm = M > 64 ? 128 : (M > 32 ? 64 : 32);
   pl.sk = groups % 2 == 0 || bm > 32;
+  pl.bmx = pl.sk ? wide_rows(taps, M) : 0;
   if (pl.sk) {
     pl.G = groups % 2 == 0 ? 2 : 1;
     pl.bm = bm;
@@ -413,8 +424,10 @@ static size_t wgrad_planes_bytes(const WgradPlan& pl) { return pl.rx6 ? (size_t)
 constexpr size_t kPartBytes = kNPart * sizeof(float);
 // stream-K pieces, then (the BP form) the image operand's fp16 planes, then the partials at the end
 static size_t fwd_piece_bytes(const FwdPlan& pl) {
-  // (the <= 64-row f16x3 / fp16 3x3 tiles run 64 rows: room for those pieces whatever the form)
-  return align_up((size_t)kSkNW * 2 * std::max(pl.bm, 64) * pl.bn * sizeof(float), 256);
+  // (the <= 64-row f16x3 / fp16 3x3 tiles run 64 rows: room for those pieces whatever the form; the 256-row
+  // pointwise tiles twice the 128-row pieces - r05's 256 / 384-row attempt kept the 128-row size, and its
+  // pieces ran past the workspace into the image partials behind them)
+  return align_up((size_t)kSkNW * 2 * std::max(pl.bmx, std::max(pl.bm, 64)) * pl.bn * sizeof(float), 256);
 }
 static size_t img_planes_bytes(int cimg, int P) { return align_up((size_t)cdiv(cimg, kCB) * kCB * P * 4, 256); }
 // The f16x3 / fp16 forward-form GEMMs that read their image operand pre-split (k_split_img, BP form):
@@ -685,6 +698,19 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
         // (profiles/r02_f16x3_waves.txt)
         if (small_f16) {
           MSL_TRY(launch_sk<64, 1, 4, 1, 4, MT>(accum, grid, block, st, a, sk, bp));
+        } else if (taps == 1 && dil0 == 0 && MT == kMathH3P && pl.bmx > 0) {
+          // wide tiles (r06): the plan, the grid and the reduce of that tile size
+          if constexpr (MT == kMathH3P) {
+            const int tm = cdiv(M, pl.bmx);
+            const SkArgs s2 = plan_sk(tm, pl.tiles_n, pl.kps, kSkNW, forms_of(forms).sk_hybrid, (float*)ws);
+            const dim3 g2(s2.tdp > 0 ? kSkNW : s2.NW);
+            const dim3 r2(pl.bmx * kSkBN / 1024, (unsigned)((long long)tm * pl.tiles_n - s2.tdp));
+            MSL_TRY(launch_sk<256, 1, 3, 1, 4, MT, true>(accum, g2, block, st, a, s2));
+            MSL_CHECK_LAUNCH();
+            if (s2.T > 0) MSL_LAUNCH((k_sk_reduce<256, kSkBN>), r2, block, 0, st, a, s2);
+            MSL_CHECK_LAUNCH();
+            return MSL_OK;
+          }
         } else if (taps == 1 && dil0 == 0) {
           if constexpr (MT == kMathH1P) {
             if (pw2)

@@ -408,6 +408,35 @@ __device__ __forceinline__ void mfma_stage_h3p(const float* As, const float* Bs,
 #pragma unroll
   for (int kk = 0; kk < G; ++kk) {
     const f16x8* Ab = reinterpret_cast<const f16x8*>(As + kk * 16 * BM);
+    if constexpr (TM * TN >= 8) {
+      // the 256-row pointwise tiles (r06: 128 accumulator registers per lane): B read and split first, then
+      // row block by row block, so only one A fragment's two planes are live at a time (all of them at once
+      // spilled 74 VGPRs)
+      Split2h bv[TN];
+      float braw[TN][8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int t = 0; t < TN; ++t) braw[t][j] = Bs[(kk * 16 + 8 * h + j) * LDB_S + wn + t * 32 + l32];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int t = 0; t < TN; ++t) split2h_set(bv[t], j, braw[t][j] * sB);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        Split2h av;
+        av.lo = Ab[(2 + h) * BM + wm + i * 32 + l32];
+        av.hi = Ab[h * BM + wm + i * 32 + l32];
+#pragma unroll
+        for (int t = 0; t < TN; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av.lo, bv[t].hi, acc[i][t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < TN; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av.hi, bv[t].lo, acc[i][t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < TN; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av.hi, bv[t].hi, acc[i][t], 0, 0, 0);
+      }
+      if (kk == 0) mid();
+      continue;
+    }
     Split2h av[TM], bv[TN];
     float braw[TN][8];
 #pragma unroll
@@ -923,8 +952,10 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   static_assert(BN % 64 == 0 && BM % 32 == 0, "tiles");
   // r05: 256- and 384-row tiles of the LDS form computed wrong results from the first row on
-  // (profiles/r05_aspp_384_tile_attempt.txt); no such form may be instantiated until the cause is fixed
-  static_assert(BM <= 128, "fwd_sk_body: tiles over 128 rows are not a validated form");
+  // (profiles/r05_aspp_384_tile_attempt.txt): the launch kept the workspace of 128-row pieces, and the larger
+  // pieces ran past it (r06: dconv.hip fwd_piece_bytes).  Only the form validated since may be instantiated
+  static_assert(BM <= 128 || (BM == 256 && PW && WM == 1 && WN == 4 && STAGES == 3),
+                "fwd_sk_body: tiles over 128 rows are validated only as the 256-row pointwise form (r06)");
   constexpr bool H1 = MT == kMathH1P;                                 // fp16: the hi plane only
   constexpr bool H3 = MT == kMathH3P || H1;                           // f16x3: two fp16 planes
   constexpr bool APRE = MT == kMathX6P || H3;  // A from pre-split planes
