@@ -491,192 +491,294 @@ __device__ __forceinline__ void bn_st(__amdgpu_buffer_rsrc_t r, unsigned voff, i
 }
 constexpr int kBnTwoBlockEpt = 16;  // forms built for two blocks per CU (64 VGPRs)
 
-template <int EPT>
-__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= kBnTwoBlockEpt ? 8 : 1))) k_bn_fwd_fused(BnArgs a) {
-  __shared__ double red[2 * kBnFusedThreads / 64];
-  const int c = blockIdx.x, t = threadIdx.x, P = a.P;
-  float am = 0.f;
-  for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
-  if (img) __syncthreads();               // red[] is reused
-  const int r = c * a.NI + img;
-  const long long base = (long long)r * P;
-  const float* xc = a.x + base;
-  const unsigned vo = (unsigned)t * 4u;
-  const __amdgpu_buffer_rsrc_t rx = bn_row(xc, P);
-  float xv[EPT];
+// N fp64 sums over the block, each in block_sum2_d16's order (wave xor-shuffle, then the 16 waves in order):
+// the joint two-image form below sums every value exactly as the one-image form does (red: N * 16 doubles)
+template <int N>
+__device__ __forceinline__ void block_sum_d16(double (&v)[N], double* red) {
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = j * kBnFusedThreads + t;
-    xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
-  }
-  const double shift = (double)xc[0];
-  double s1 = 0.0, s2 = 0.0;
+  for (int k = 0; k < N; ++k) v[k] = wave_sum_d(v[k]);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    if (j * kBnFusedThreads + t < P) {
-      const double d = (double)xv[j] - shift;
-      s1 = __dadd_rn(s1, d);  // explicit roundings: the single-image and pair forms agree bit for bit
-      s2 = __fma_rn(d, d, s2);
-    }
+    for (int k = 0; k < N; ++k) red[N * w + k] = v[k];
   }
-  block_sum2_d16(s1, s2, red);
-  const double n = (double)P;
-  const double dm = s1 / n;
-  double var = __fma_rn(-dm, dm, __ddiv_rn(s2, n));
-  if (var < 0.0) var = 0.0;
-  const float mean = (float)(shift + dm);
-  const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-  if (t == 0) {
-    if (a.update_running) {
-      const float m = a.momentum;
-      const float unbiased = (float)(P > 1 ? var * n / (n - 1.0) : var);
-      a.running_mean[c] = running_blend(a.running_mean[c], m, mean);
-      a.running_var[c] = running_blend(a.running_var[c], m, unbiased);
-      if (c == 0 && a.num_batches) a.num_batches[0] += 1;
-    }
-    a.save_mean[r] = mean;
-    a.save_invstd[r] = invstd;
-  }
-  const float alpha = invstd * (a.gamma ? a.gamma[c] : 1.f);
-  const float bsh = __fmaf_rn(-mean, alpha, a.beta ? a.beta[c] : 0.f);
-  const __amdgpu_buffer_rsrc_t ry = bn_row(a.y + base, P);
-  // the residual is loaded after the statistics: not live across the reduction, so the EPT <= 16
-  // forms fit 64 VGPRs (two 1024-thread blocks per CU)
-  float rv[EPT];
-  if (a.residual) {
-    const __amdgpu_buffer_rsrc_t rr = bn_row(a.residual + base, P);
+  __syncthreads();
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) rv[j] = j * kBnFusedThreads + t < P ? bn_ld(rr, vo, j) : 0.f;
-  } else {
+  for (int k = 0; k < N; ++k) v[k] = 0.0;
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) rv[j] = 0.f;
-  }
-  // r05: with a.mask, y > 0 of each wave's 64 consecutive pixels as one 64-bit word (a ballot): the
-  // residual BN's backward then reads 1 bit per pixel for its ReLU mask instead of the 4-byte y
-  // (lane j of the wave keeps block j's word, and the EPT words leave in one masked store after the loop)
-  unsigned long long* mrow = a.mask ? a.mask + (long long)r * cdiv(P, 64) : nullptr;
-  unsigned long long myword = 0;
+  for (int i = 0; i < kBnFusedThreads / 64; ++i) {  // fixed order: deterministic
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = j * kBnFusedThreads + t;
-    bool pos = false;
-    if (e < P) {
-      float v = __fmaf_rn(xv[j], alpha, bsh);
-      v += rv[j];
-      v = a.relu ? fmaxf(v, 0.f) : v;
-      bn_st(ry, vo, j, v);
-      am = fmaxf(am, fabsf(v));
-      pos = v > 0.f;
-    }
-    if (mrow) {
-      const unsigned long long bits = __ballot(pos);
-      if ((t & 63) == j) myword = bits;
-    }
-  }
-  static_assert(EPT <= 64, "one mask word per lane");
-  if (mrow && (t & 63) < EPT && (t & 63) * kBnFusedThreads + (t & ~63) < P)
-    mrow[(t & 63) * (kBnFusedThreads / 64) + (t >> 6)] = myword;
-  }  // images
-  if (a.absmax) {
-    __shared__ float redm[kBnFusedThreads / 64];
-    am = block_max16(am, redm);
-    if (t == 0) a.absmax[c] = am;
+    for (int k = 0; k < N; ++k) v[k] += red[N * i + k];
   }
 }
 
-template <int EPT>
-__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(EPT <= kBnTwoBlockEpt ? 8 : 1))) k_bn_bwd_fused(BnBwdArgs a) {
-  __shared__ double red[2 * kBnFusedThreads / 64];
-  const int c = blockIdx.x, t = threadIdx.x, P = a.P;
-  float am = 0.f;
-  float dg = 0.f, db = 0.f;  // the parameter gradients, image by image (thread 0)
-  for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
-  if (img) __syncthreads();               // red[] is reused
-  const int r = c * a.NI + img;
-  const long long base = (long long)r * P;
-  const float mean = a.save_mean[r], invstd = a.save_invstd[r];
+// NB images img0 .. img0 + NB - 1 of channel c, their loads, reductions and stores issued together (r06: with
+// NB = 1 per image, a 256-channel pair BN - 256 blocks, one per CU - loaded, reduced and stored image 0 before
+// image 1's loads: 12.2 us per forward at 2.8 TB/s, profiles/r06_bn_pair_ab.txt).  Every per-image value is
+// computed with the one-image operations in the same order, so NB = 2 and two NB = 1 passes agree bit for bit;
+// the running statistics and the batch counter are updated image by image, image 0 first, as before.
+template <int EPT, int NB>
+__device__ __forceinline__ void bn_fwd_rows(const BnArgs& a, int c, int img0, double* red, float& am) {
+  const int t = threadIdx.x, P = a.P;
   const unsigned vo = (unsigned)t * 4u;
-  const __amdgpu_buffer_rsrc_t rdy = bn_row(a.dy + base, P), rx = bn_row(a.x + base, P);
-  float g[EPT], xv[EPT];
+  float xv[NB][EPT];
+  double sh[NB];
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = j * kBnFusedThreads + t;
-    g[j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
-    xv[j] = e < P ? bn_ld(rx, vo, j) : 0.f;
-  }
-  const float w = invstd * (a.gamma ? a.gamma[c] : 1.f);
-  if (a.relu && a.mask) {  // the forward's y > 0 bits: one 8-byte word per wave and element block
-    const unsigned long long* mrow = a.mask + (long long)r * cdiv(P, 64);
+  for (int b = 0; b < NB; ++b) {
+    const long long base = (long long)(c * a.NI + img0 + b) * P;
+    const __amdgpu_buffer_rsrc_t rx = bn_row(a.x + base, P);
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const int e = j * kBnFusedThreads + t;
-      if (j * kBnFusedThreads + (t & ~63) < P) {  // wave-uniform: the word exists
-        const unsigned long long bits = mrow[j * (kBnFusedThreads / 64) + (t >> 6)];
-        if (e < P && !((bits >> (t & 63)) & 1ull)) g[j] = 0.f;
+      xv[b][j] = e < P ? bn_ld(rx, vo, j) : 0.f;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) sh[b] = (double)a.x[(long long)(c * a.NI + img0 + b) * P];
+  double s[2 * NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      if (j * kBnFusedThreads + t < P) {
+        const double d = (double)xv[b][j] - sh[b];
+        s1 = __dadd_rn(s1, d);  // explicit roundings: the single-image and pair forms agree bit for bit
+        s2 = __fma_rn(d, d, s2);
       }
     }
-  } else if (a.relu && a.y) {
-    const __amdgpu_buffer_rsrc_t ryy = bn_row(a.y + base, P);
+    s[2 * b] = s1;
+    s[2 * b + 1] = s2;
+  }
+  block_sum_d16<2 * NB>(s, red);
+  const double n = (double)P;
+  float alpha[NB], bsh[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int r = c * a.NI + img0 + b;
+    const double dm = s[2 * b] / n;
+    double var = __fma_rn(-dm, dm, __ddiv_rn(s[2 * b + 1], n));
+    if (var < 0.0) var = 0.0;
+    const float mean = (float)(sh[b] + dm);
+    const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+    if (t == 0) {
+      if (a.update_running) {
+        const float m = a.momentum;
+        const float unbiased = (float)(P > 1 ? var * n / (n - 1.0) : var);
+        a.running_mean[c] = running_blend(a.running_mean[c], m, mean);
+        a.running_var[c] = running_blend(a.running_var[c], m, unbiased);
+        if (c == 0 && a.num_batches) a.num_batches[0] += 1;
+      }
+      a.save_mean[r] = mean;
+      a.save_invstd[r] = invstd;
+    }
+    alpha[b] = invstd * (a.gamma ? a.gamma[c] : 1.f);
+    bsh[b] = __fmaf_rn(-mean, alpha[b], a.beta ? a.beta[c] : 0.f);
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int r = c * a.NI + img0 + b;
+    const long long base = (long long)r * P;
+    const __amdgpu_buffer_rsrc_t ry = bn_row(a.y + base, P);
+    // the residual is loaded after the statistics: not live across the reduction, so the EPT <= 16
+    // forms fit 64 VGPRs (two 1024-thread blocks per CU)
+    float rv[EPT];
+    if (a.residual) {
+      const __amdgpu_buffer_rsrc_t rr = bn_row(a.residual + base, P);
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) rv[j] = j * kBnFusedThreads + t < P ? bn_ld(rr, vo, j) : 0.f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) rv[j] = 0.f;
+    }
+    // r05: with a.mask, y > 0 of each wave's 64 consecutive pixels as one 64-bit word (a ballot): the
+    // residual BN's backward then reads 1 bit per pixel for its ReLU mask instead of the 4-byte y
+    // (lane j of the wave keeps block j's word, and the EPT words leave in one masked store after the loop)
+    unsigned long long* mrow = a.mask ? a.mask + (long long)r * cdiv(P, 64) : nullptr;
+    unsigned long long myword = 0;
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const int e = j * kBnFusedThreads + t;
-      if (e < P && !(bn_ld(ryy, vo, j) > 0.f)) g[j] = 0.f;
+      bool pos = false;
+      if (e < P) {
+        float v = __fmaf_rn(xv[b][j], alpha[b], bsh[b]);
+        v += rv[j];
+        v = a.relu ? fmaxf(v, 0.f) : v;
+        bn_st(ry, vo, j, v);
+        am = fmaxf(am, fabsf(v));
+        pos = v > 0.f;
+      }
+      if (mrow) {
+        const unsigned long long bits = __ballot(pos);
+        if ((t & 63) == j) myword = bits;
+      }
     }
-  } else if (a.relu) {  // y > 0 recomputed with k_bn_fwd_fused's operations (its alpha, bsh)
-    if constexpr (EPT <= kBnRemaskMaxEpt) {  // (the 33-element form spills twice as much with it)
-      const float bsh = __fmaf_rn(-mean, w, a.beta ? a.beta[c] : 0.f);
+    static_assert(EPT <= 64, "one mask word per lane");
+    if (mrow && (t & 63) < EPT && (t & 63) * kBnFusedThreads + (t & ~63) < P)
+      mrow[(t & 63) * (kBnFusedThreads / 64) + (t >> 6)] = myword;
+  }
+}
+
+// JOINT: the two images of a pair together (launched for NI = 2, EPT <= 9) at one 1024-thread block per CU
+// (128 VGPRs: the pair's registers); else image by image, two blocks per CU for EPT <= 16 (64 VGPRs)
+template <int EPT, bool JOINT>
+constexpr int bn_waves_per_eu() { return JOINT ? 4 : EPT <= kBnTwoBlockEpt ? 8 : 1; }
+
+template <int EPT, bool JOINT = false>
+__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(bn_waves_per_eu<EPT, JOINT>()))) k_bn_fwd_fused(BnArgs a) {
+  __shared__ double red[4 * kBnFusedThreads / 64];
+  const int c = blockIdx.x;
+  float am = 0.f;
+  if constexpr (JOINT) {
+    bn_fwd_rows<EPT, 2>(a, c, 0, red, am);
+  } else {
+    for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
+      if (img) __syncthreads();               // red[] is reused
+      bn_fwd_rows<EPT, 1>(a, c, img, red, am);
+    }
+  }
+  if (a.absmax) {
+    __shared__ float redm[kBnFusedThreads / 64];
+    am = block_max16(am, redm);
+    if (threadIdx.x == 0) a.absmax[c] = am;
+  }
+}
+
+// the backward's NB images of channel c (as bn_fwd_rows: joint loads and reductions, per-image arithmetic and
+// the parameter gradients image by image, image 0 first)
+template <int EPT, int NB>
+__device__ __forceinline__ void bn_bwd_rows(const BnBwdArgs& a, int c, int img0, double* red, float& am, float& dg,
+                                            float& db) {
+  const int t = threadIdx.x, P = a.P;
+  const unsigned vo = (unsigned)t * 4u;
+  float g[NB][EPT], xv[NB][EPT];
+  float mean[NB], invstd[NB];
 #pragma unroll
-      for (int j = 0; j < EPT; ++j)
-        if (!(__fmaf_rn(xv[j], w, bsh) > 0.f)) g[j] = 0.f;
-    }
-  }
-  double sg = 0.0, sgx = 0.0;
+  for (int b = 0; b < NB; ++b) {
+    const int r = c * a.NI + img0 + b;
+    const long long base = (long long)r * P;
+    mean[b] = a.save_mean[r];
+    invstd[b] = a.save_invstd[r];
+    const __amdgpu_buffer_rsrc_t rdy = bn_row(a.dy + base, P), rx = bn_row(a.x + base, P);
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const float xh = (xv[j] - mean) * invstd;
-    sg = __dadd_rn(sg, (double)g[j]);  // g = 0 past P
-    sgx = __fma_rn((double)g[j], (double)xh, sgx);
-  }
-  block_sum2_d16(sg, sgx, red);
-  if (t == 0) {
-    if (img == 0) {
-      dg = (a.accumulate && a.dgamma) ? a.dgamma[c] + (float)sgx : (float)sgx;
-      db = (a.accumulate && a.dbeta) ? a.dbeta[c] + (float)sg : (float)sg;
-    } else {
-      dg += (float)sgx;
-      db += (float)sg;
+    for (int j = 0; j < EPT; ++j) {
+      const int e = j * kBnFusedThreads + t;
+      g[b][j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
+      xv[b][j] = e < P ? bn_ld(rx, vo, j) : 0.f;
     }
   }
-  const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
-  const __amdgpu_buffer_rsrc_t rdres = bn_row(a.dres ? a.dres + base : nullptr, P);
-  const __amdgpu_buffer_rsrc_t rdx = bn_row(a.dx ? a.dx + base : nullptr, P);
+  const float gm = a.gamma ? a.gamma[c] : 1.f;
+  double s[2 * NB];
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = j * kBnFusedThreads + t;
-    if (e < P) {
-      const float xh = (xv[j] - mean) * invstd;
-      if (a.dres) bn_st(rdres, vo, j, g[j]);
-      const float d = __fmul_rn(__fmaf_rn(-xh, m2, __fsub_rn(g[j], m1)), w);
-      if (a.dx) bn_st(rdx, vo, j, d);
-      am = fmaxf(am, fabsf(d));
+  for (int b = 0; b < NB; ++b) {
+    const int r = c * a.NI + img0 + b;
+    const float w = invstd[b] * gm;
+    if (a.relu && a.mask) {  // the forward's y > 0 bits: one 8-byte word per wave and element block
+      const unsigned long long* mrow = a.mask + (long long)r * cdiv(P, 64);
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        const int e = j * kBnFusedThreads + t;
+        if (j * kBnFusedThreads + (t & ~63) < P) {  // wave-uniform: the word exists
+          const unsigned long long bits = mrow[j * (kBnFusedThreads / 64) + (t >> 6)];
+          if (e < P && !((bits >> (t & 63)) & 1ull)) g[b][j] = 0.f;
+        }
+      }
+    } else if (a.relu && a.y) {
+      const __amdgpu_buffer_rsrc_t ryy = bn_row(a.y + (long long)r * P, P);
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        const int e = j * kBnFusedThreads + t;
+        if (e < P && !(bn_ld(ryy, vo, j) > 0.f)) g[b][j] = 0.f;
+      }
+    } else if (a.relu) {  // y > 0 recomputed with k_bn_fwd_fused's operations (its alpha, bsh)
+      if constexpr (EPT <= kBnRemaskMaxEpt) {  // (the 33-element form spills twice as much with it)
+        const float bsh = __fmaf_rn(-mean[b], w, a.beta ? a.beta[c] : 0.f);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j)
+          if (!(__fmaf_rn(xv[b][j], w, bsh) > 0.f)) g[b][j] = 0.f;
+      }
+    }
+    double sg = 0.0, sgx = 0.0;
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const float xh = (xv[b][j] - mean[b]) * invstd[b];
+      sg = __dadd_rn(sg, (double)g[b][j]);  // g = 0 past P
+      sgx = __fma_rn((double)g[b][j], (double)xh, sgx);
+    }
+    s[2 * b] = sg;
+    s[2 * b + 1] = sgx;
+  }
+  block_sum_d16<2 * NB>(s, red);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const double sg = s[2 * b], sgx = s[2 * b + 1];
+    if (t == 0) {
+      if (img0 + b == 0) {
+        dg = (a.accumulate && a.dgamma) ? a.dgamma[c] + (float)sgx : (float)sgx;
+        db = (a.accumulate && a.dbeta) ? a.dbeta[c] + (float)sg : (float)sg;
+      } else {
+        dg += (float)sgx;
+        db += (float)sg;
+      }
+    }
+    const float w = invstd[b] * gm;
+    const float m1 = (float)(sg / (double)P), m2 = (float)(sgx / (double)P);
+    const long long base = (long long)(c * a.NI + img0 + b) * P;
+    const __amdgpu_buffer_rsrc_t rdres = bn_row(a.dres ? a.dres + base : nullptr, P);
+    const __amdgpu_buffer_rsrc_t rdx = bn_row(a.dx ? a.dx + base : nullptr, P);
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = j * kBnFusedThreads + t;
+      if (e < P) {
+        const float xh = (xv[b][j] - mean[b]) * invstd[b];
+        if (a.dres) bn_st(rdres, vo, j, g[b][j]);
+        const float d = __fmul_rn(__fmaf_rn(-xh, m2, __fsub_rn(g[b][j], m1)), w);
+        if (a.dx) bn_st(rdx, vo, j, d);
+        am = fmaxf(am, fabsf(d));
+      }
     }
   }
-  }  // images
-  if (t == 0) {
+}
+
+template <int EPT, bool JOINT = false>
+__global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_per_eu(bn_waves_per_eu<EPT, JOINT>()))) k_bn_bwd_fused(BnBwdArgs a) {
+  __shared__ double red[4 * kBnFusedThreads / 64];
+  const int c = blockIdx.x;
+  float am = 0.f;
+  float dg = 0.f, db = 0.f;  // the parameter gradients, image by image (thread 0)
+  if constexpr (JOINT) {
+    bn_bwd_rows<EPT, 2>(a, c, 0, red, am, dg, db);
+  } else {
+    for (int img = 0; img < a.NI; ++img) {  // the channel's images one after the other
+      if (img) __syncthreads();               // red[] is reused
+      bn_bwd_rows<EPT, 1>(a, c, img, red, am, dg, db);
+    }
+  }
+  if (threadIdx.x == 0) {
     if (a.dgamma) a.dgamma[c] = dg;
     if (a.dbeta) a.dbeta[c] = db;
   }
   if (a.absmax) {
     __shared__ float redm[kBnFusedThreads / 64];
     am = block_max16(am, redm);
-    if (t == 0) a.absmax[c] = am;
+    if (threadIdx.x == 0) a.absmax[c] = am;
   }
 }
 
 
+// r06: the pair (NI = 2) of <= kBnJointMaxC channels at EPT <= 9 runs the joint two-image kernels: there one round
+// of <= 256 blocks leaves half of the CUs' block slots empty anyway, and the joint loads double what is in flight
+// (256 ch fwd 11.7 vs 12.2 us, bwd 17.5 vs 19.0, bwd with the mask recomputed 12.1 vs 13.8).  From 512 channels the
+// image-by-image kernel's two blocks per CU win (512 ch fwd 18.1 vs 23.3 us, 1024 ch + residual 37.5 vs 46.0;
+// profiles/r06_bn_pair_ab.txt); at 16 elements the pair's registers spill.
+constexpr int kBnJointPair = 1;
+constexpr int kBnJointMaxC = 256;
 template <typename K, typename A>
-static int bn_launch_fused(K k4, K k9, K k16, K k33, int c, int p, hipStream_t st, const A& a) {
-  K k = p <= 4 * kBnFusedThreads ? k4 : p <= 9 * kBnFusedThreads ? k9 : p <= 16 * kBnFusedThreads ? k16 : k33;
+static int bn_launch_fused(K k4, K k9, K k16, K k33, K j4, K j9, K j16, int c, int p, hipStream_t st, const A& a) {
+  const bool joint = kBnJointPair && a.NI == 2 && c <= kBnJointMaxC;
+  K k = p <= 4 * kBnFusedThreads ? (joint ? j4 : k4)
+        : p <= 9 * kBnFusedThreads ? (joint ? j9 : k9)
+        : p <= 16 * kBnFusedThreads ? (joint ? j16 : k16) : k33;
   MSL_LAUNCH(k, dim3(c), dim3(kBnFusedThreads), 0, st, a);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
@@ -775,7 +877,9 @@ int msl_bn_fwd_mask(const float* x, const float* gamma, const float* beta, const
   a.momentum = momentum;
   a.absmax = absmax;
   a.mask = reinterpret_cast<unsigned long long*>(relu_mask);
-  if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>, c, p, st, a);
+  if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>,
+                                        k_bn_fwd_fused<4, true>, k_bn_fwd_fused<9, true>, k_bn_fwd_fused<16>, c, p, st,
+                                        a);
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec)
     MSL_LAUNCH(k_bn_apply<true>, dim3(blocks), dim3(256), 0, st, a);
@@ -842,7 +946,8 @@ static int bn_bwd(const float* dy, const float* x, const float* y, const uint64_
   a.absmax = absmax_dx;
   a.mask = reinterpret_cast<const unsigned long long*>(relu_mask);
   if (fused)
-    return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>, c, p, st, a);
+    return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>,
+                           k_bn_bwd_fused<4, true>, k_bn_bwd_fused<9, true>, k_bn_bwd_fused<16>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec) {

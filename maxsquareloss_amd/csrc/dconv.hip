@@ -465,7 +465,10 @@ static bool bp_form(int taps, int M, bool small_f16, bool h1 = false) {
          (M >= 512 || (h1 && M >= 128) || bq_form(taps, M, small_f16) || w1_form(taps, M, small_f16));
 }
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P, int cimg, int taps) {
-  // the planes only where the BP form can run (the stem / pointwise calls reserved them too)
+  // the planes only where the BP form can run (the stem / pointwise calls reserved them too).  The
+  // query is form-independent (the forms come with the call, not with the query), so a 3x3 GEMM with
+  // 128 <= M < 512 reserves the image planes that only the fp16 math's BP form reads (cimg x P x 4 bytes, e.g.
+  // ~17 MB at layer2's pair shape) in every form: conservative, accepted
   if (pl.sk) return fwd_piece_bytes(pl) + (bp_form(taps, M, false, true) ? img_planes_bytes(cimg, P) : 0) + kPartBytes;
   return (pl.S > 1 ? (size_t)pl.S * M * P * sizeof(float) : 0) + kPartBytes;
 }

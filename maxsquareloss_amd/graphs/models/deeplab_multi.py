@@ -207,12 +207,18 @@ class ResNetMulti(nn.Module):
         output: layer4 and both heads."""
         return [p for m in (self.layer4, self.layer5, self.layer6) for p in m.parameters() if p.requires_grad]
 
+    def valid_cuts(self):
+        """split_cuts that lie inside this layer3 (a cut after block c needs blocks after it: 0 <= c <
+        len(layer3) - 1), distinct, descending - the cuts _heads and split_segments use (the
+        23-block defaults indexed past a shallower layer3)."""
+        return sorted({int(c) for c in self.split_cuts if 0 <= int(c) < len(self.layer3) - 1}, reverse=True)
+
     def split_segments(self):
         """The trainable parameters each segment of the split backward finishes, in backward order:
         [layer4 + heads, layer3 blocks after the last cut, ..., after the first cut]; the last segment
         (layer3 up to the first cut, layer2, layer1, the stem) finishes the rest."""
         groups, hi = [self.split_params()], len(self.layer3)
-        for c in sorted(self.split_cuts, reverse=True):
+        for c in self.valid_cuts():
             groups.append([p for b in range(c + 1, hi) for p in self.layer3[b].parameters() if p.requires_grad])
             hi = c + 1
         return groups
@@ -234,9 +240,10 @@ class ResNetMulti(nn.Module):
         x = self.layer2(x)
         if self.keep_split:
             self.split_out = []
+            cuts = set(self.valid_cuts())
             for i, blk in enumerate(self.layer3):
                 x = blk(x)
-                if i in self.split_cuts or i == len(self.layer3) - 1:
+                if i in cuts or i == len(self.layer3) - 1:
                     x = self._cut(x)
         else:
             x = self.layer3(x)

@@ -111,6 +111,7 @@ SIGNATURES = {
 }
 
 ABI_VERSION = 3
+_DIAGNOSTIC = {"msl_launch_guard_probe"}  # r06 diagnostics, not on any compute path
 _lib = None
 
 
@@ -135,6 +136,8 @@ def load(require_gpu=True):
                        "(make -C maxsquareloss_amd/csrc)")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if name in _DIAGNOSTIC and not hasattr(lib, name):
+            continue  # an older build (MSL_LIB_PATH, a same-box A/B) without the diagnostics entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -172,6 +175,13 @@ def forms():
     """The const msl_forms* of every conv / pack / BN call: FORMS, read by the library on the host when
     the call launches (a captured graph keeps the forms of its capture)."""
     return ctypes.addressof(FORMS)
+
+
+def snapshot_forms():
+    """A copy of FORMS: an autograd function keeps the forms of its forward and passes them to
+    its backward's calls, so a form switched between the two (the tests toggle them) cannot hand a
+    backward kernel a state its forward did not leave (the fused BN's mask bits, a pack's form)."""
+    return Forms(*(getattr(FORMS, f) for f, _ in Forms._fields_))
 
 
 def set_form(name, value):

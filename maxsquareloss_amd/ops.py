@@ -9,6 +9,7 @@ out [C][2][H][W], each image convolved, pooled and batch-normalised on its own (
 own bs=1 statistics) while every conv GEMM runs once over both (pair_join /
 pair_split; the trunk ops take either form, the losses one image).
 """
+import ctypes
 from contextlib import nullcontext as _nullctx
 
 import torch
@@ -372,6 +373,7 @@ class _DConv3x3(Function):
 
     @staticmethod
     def forward(ctx, x, w0, w1, b0, b1, dil0, dil1, cache):
+        ctx.fm = hip.snapshot_forms()  # the backward runs the forms of its forward
         x = _check_act(x, "dconv3x3", images=True)
         n = _nimg(x)
         weights = [w0] if w1 is None else [w0, w1]
@@ -425,7 +427,7 @@ class _DConv3x3(Function):
             ws = hip.workspace(wsb, x.device)
             hip.check(_conv_call(lib, "msl_dconv_dgrad", math,
                                  (gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), nb, cin, cout, h, w, n, dil0, d1,
-                                  hip.forms(), ws.data_ptr(), wsb, s), (gpart,)),
+                                  ctypes.addressof(ctx.fm), ws.data_ptr(), wsb, s), (gpart,)),
                       "msl_dconv_dgrad")
         sink = grad_sink(weights[0]) if (nb == 1 and not has_bias and ctx.needs_input_grad[1]) else None
         wsb = lib.msl_dconv_wgrad_workspace(nb, cin, cout, h, w, n)
@@ -436,7 +438,7 @@ class _DConv3x3(Function):
                 ws = hip.workspace(wsb, x.device)
                 hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
                                      (x.data_ptr(), gy.data_ptr(), g.data_ptr(), None, 1, cin, cout, h, w, n, dil0, 0, 1,
-                                      hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr()), (xpart, gpart)), "msl_dconv_wgrad")
+                                      ctypes.addressof(ctx.fm), ws.data_ptr(), wsb, hip.stream_ptr()), (xpart, gpart)), "msl_dconv_wgrad")
             if side is not None:
                 _keep(side, x, gy, *(q[0] for q in (xpart, gpart) if q is not None))
             fg.notify(i)
@@ -446,7 +448,7 @@ class _DConv3x3(Function):
         db_all = torch.empty((nb, cout), dtype=_f32, device=x.device) if has_bias else None
         hip.check(_conv_call(lib, "msl_dconv_wgrad", math,
                              (x.data_ptr(), gy.data_ptr(), dw_all.data_ptr(), hip.ptr(db_all), nb, cin, cout, h, w,
-                              n, dil0, d1, 0, hip.forms(), ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
+                              n, dil0, d1, 0, ctypes.addressof(ctx.fm), ws.data_ptr(), wsb, s), (xpart, gpart)), "msl_dconv_wgrad")
         dw0 = dw_all[0]
         dw1 = dw_all[1] if nb > 1 else None
         db0 = db_all[0] if has_bias else None
@@ -507,6 +509,7 @@ class _ASPPShift(Function):
 
     @staticmethod
     def forward(ctx, x, w0, w1, b0, b1, dil0, dil1, cache):
+        ctx.fm = hip.snapshot_forms()  # the backward runs the forms of its forward
         x = _check_act(x, "aspp2", images=True)
         n = _nimg(x)
         weights = [w0] if w1 is None else [w0, w1]
@@ -559,7 +562,7 @@ class _ASPPShift(Function):
             dx = torch.empty_like(x)
             wsb = lib.msl_pconv_dgrad_workspace(cin, m, p)
             ws = hip.workspace(wsb, x.device)
-            cnt = hip.forms()
+            cnt = ctypes.addressof(ctx.fm)
             if math == "bf16":
                 st = lib.msl_pconv_dgrad_bf16(g.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, m, p, cnt,
                                               ws.data_ptr(), wsb, s)
@@ -574,7 +577,7 @@ class _ASPPShift(Function):
             wsb = lib.msl_pconv_wgrad_workspace(cin, m, p)
             ws = hip.workspace(wsb, x.device)
             hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
-                                 (x.data_ptr(), g.data_ptr(), dwp.data_ptr(), cin, m, p, 0, hip.forms(), ws.data_ptr(), wsb, s),
+                                 (x.data_ptr(), g.data_ptr(), dwp.data_ptr(), cin, m, p, 0, ctypes.addressof(ctx.fm), ws.data_ptr(), wsb, s),
                                  (ctx.xpart, gpart)), "msl_pconv_wgrad")
             dw_all = torch.empty((nb, c, cin, 3, 3), dtype=_f32, device=x.device)
             hip.check(lib.msl_aspp_weight_grad(dwp.data_ptr(), nb, c, cin, dw_all.data_ptr(), s), "msl_aspp_weight_grad")
@@ -604,6 +607,7 @@ class _PConv(Function):
 
     @staticmethod
     def forward(ctx, x, weight, cache, hold=None, grad_to=None):
+        ctx.fm = hip.snapshot_forms()  # the backward runs the forms of its forward
         x = _check_act(x, "pconv", images=True)
         cout, cin = weight.shape[0], weight.shape[1]
         if weight.shape[2:] != (1, 1) or x.size(1) != cin:
@@ -652,7 +656,7 @@ class _PConv(Function):
             packed_d = cache.get([weight], cin, cout, 1)
             wsb = lib.msl_pconv_dgrad_workspace(cin, cout, p)
             ws = hip.workspace(wsb, x.device)
-            cnt = hip.forms()
+            cnt = ctypes.addressof(ctx.fm)
             if math == "bf16":
                 tgt = torch.empty_like(x) if acc else dx
                 hip.check(lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), tgt.data_ptr(), cin, cout, p,
@@ -678,7 +682,7 @@ class _PConv(Function):
             ws = hip.workspace(wsb, x.device)
             hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
                                  (x.data_ptr(), gy.data_ptr(), dst.data_ptr(), cin, cout, p, int(sink is not None),
-                                  hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.xpart, gpart)), "msl_pconv_wgrad")
+                                  ctypes.addressof(ctx.fm), ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.xpart, gpart)), "msl_pconv_wgrad")
         if side is not None:
             _keep(side, x, gy, *(q[0] for q in (ctx.xpart, gpart) if q is not None))
         if sink is None:
@@ -729,6 +733,7 @@ class _StemConv(Function):
 
     @staticmethod
     def forward(ctx, x, weight, stride, pad, cache):
+        ctx.fm = hip.snapshot_forms()  # the backward runs the forms of its forward
         x = _check_act(x, "stem_conv", images=True)
         cout, cin, kh, kw = weight.shape
         if x.size(1) != cin:
@@ -780,7 +785,7 @@ class _StemConv(Function):
             dcol = torch.empty_like(col)
             wsb = lib.msl_pconv_dgrad_workspace(kk, cout, p)
             ws = hip.workspace(wsb, gy.device)
-            cnt = hip.forms()
+            cnt = ctypes.addressof(ctx.fm)
             if math == "bf16":
                 st = lib.msl_pconv_dgrad_bf16(gy.data_ptr(), packed_d.data_ptr(), dcol.data_ptr(), kk, cout, p, cnt,
                                               ws.data_ptr(), wsb, s)
@@ -802,7 +807,7 @@ class _StemConv(Function):
             ws = hip.workspace(wsb, gy.device)
             hip.check(_conv_call(lib, "msl_pconv_wgrad", math,
                                  (col.data_ptr(), gy.data_ptr(), dst.data_ptr(), kk, cout, p, int(sink is not None),
-                                  hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.cpart, gpart)), "msl_pconv_wgrad")
+                                  ctypes.addressof(ctx.fm), ws.data_ptr(), wsb, hip.stream_ptr()), (ctx.cpart, gpart)), "msl_pconv_wgrad")
         if side is not None:
             _keep(side, col, gy, *(q[0] for q in (ctx.cpart, gpart) if q is not None))
         if sink is None:
@@ -1192,6 +1197,7 @@ class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, training, momentum,
                 eps, relu, hold=None):
+        ctx.fm = hip.snapshot_forms()  # the backward runs the forms of its forward
         x = _check_act(x, "bn_act", images=True)
         n = _nimg(x)
         c, p = x.size(1), x.size(-2) * x.size(-1)  # p: pixels of one image
@@ -1260,12 +1266,12 @@ class _BNAct(Function):
             st = lib.msl_bn_bwd_mask(gy.data_ptr(), x.data_ptr(), ctx.bits.data_ptr(), hip.ptr(weight),
                                      hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(), hip.ptr(dx),
                                      hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n, int(training), int(relu),
-                                     int(direct), hip.forms(), ws.data_ptr(), wsb, hip.stream_ptr(), hip.ptr(am))
+                                     int(direct), ctypes.addressof(ctx.fm), ws.data_ptr(), wsb, hip.stream_ptr(), hip.ptr(am))
         else:
             st = lib.msl_bn_bwd_am_beta(gy.data_ptr(), x.data_ptr(), hip.ptr(y), hip.ptr(weight),
                                         hip.ptr(ctx.bias), save_mean.data_ptr(), save_invstd.data_ptr(),
                                         hip.ptr(dx), hip.ptr(dres), hip.ptr(dgamma), hip.ptr(dbeta), c, p, n,
-                                        int(training), int(relu), int(direct), hip.forms(), ws.data_ptr(), wsb,
+                                        int(training), int(relu), int(direct), ctypes.addressof(ctx.fm), ws.data_ptr(), wsb,
                                         hip.stream_ptr(), hip.ptr(am))
         hip.check(st, "msl_bn_bwd")
         if am is not None:

@@ -126,10 +126,12 @@ class UDATrainer(Trainer):
             if self._graphed is None:
                 if self.reducer is None:
                     self._graphed = GraphedStep(self, self._uda_body)
-                elif self.pair and x_s.shape == x_t.shape and self._split_ok():
+                elif self._split_ok():
                     # the backward captured in segments split at layer3's output and inside layer3 (the
                     # model's split_cuts): the gradients each segment finished are exchanged while the
-                    # next segments replay
+                    # next segments replay.  Pair mode: the pair's one backward is cut; two-pass mode (r06,
+                    # the reference's order): the source pass runs whole in the first segment (it only
+                    # accumulates), and the target backward - the one that finishes the gradients - is cut
                     ends = list(np.cumsum([len(g) for g in self.model.split_segments()]))
                     self.reducer.set_breaks(ends)
                     red = self.reducer
@@ -200,10 +202,17 @@ class UDATrainer(Trainer):
     def _split_ok(self):
         """Whether the parameters each backward segment finishes (model.split_segments) lead the flat
         gradient buffer (its backward order) in segment order, so the buckets launched after a segment
-        hold final gradients only."""
+        hold final gradients only (False for a model without the split, or a cut list that leaves a
+        segment empty)."""
+        if not hasattr(self.model, "split_segments"):
+            return False
         order = [id(p) for p in self.optimizer.grads.params]
         k = 0
-        for grp in self.model.split_segments():
+        try:
+            segments = self.model.split_segments()
+        except (IndexError, AttributeError):
+            return False
+        for grp in segments:
             ids = {id(p) for p in grp}
             if not ids or set(order[k:k + len(ids)]) != ids:
                 return False
@@ -213,8 +222,25 @@ class UDATrainer(Trainer):
     def _uda_grads_head(self, x_s, y_s, x_t):
         """The pair's forward and the backward through the heads and layer4, stopping at layer3's
         output (the cuts kept for _uda_grads_trunk): the first segment of a captured data-parallel step
-        (utils/graph.py).  The segments run exactly the kernels of _uda_grads, in its order."""
+        (utils/graph.py).  The segments run exactly the kernels of _uda_grads, in its order.
+        Two-pass mode (r06): the source forward and backward whole (they only accumulate), then the target
+        forward with the cuts kept and its backward through the heads and layer4 - _uda_grads' order with
+        the target backward cut (without the side-stream overlap of the target forward: one stream)."""
         m = self.model
+        if not (self.pair and x_s.shape == x_t.shape):
+            self.train_source(m(x_s), y_s)
+            m.keep_split = True
+            try:
+                pred_t = m(x_t)
+            finally:
+                m.keep_split = False
+            split, m.split_out = m.split_out, None
+            loss_t = self.target_loss_total(pred_t)
+            self.reducer.prepare_for_backward()
+            loss_t.backward()  # ends at the heads' detached input (its .grad)
+            ops.wgrad_join(self.device)
+            self._split = split
+            return
         m.keep_split = True
         try:
             pred_s, pred_t = m.forward_pair(x_s, x_t)

@@ -54,6 +54,14 @@ def dist_env():
     return rank, world, local
 
 
+def _free_port():
+    """A TCP port free on 127.0.0.1 now (the one-rank group's rendezvous)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 class Trainer:
     def __init__(self, args, cuda=None, train_id="None", logger=None):
         self.args = args
@@ -65,6 +73,12 @@ class Trainer:
         self.device = torch.device("cuda", self.local_rank)
         dp = self.world > 1 or bool(getattr(args, "dp_exchange", False))
         if dp and not dist.is_initialized():
+            if self.world == 1:
+                # --dp_exchange on a plain single-process launch: a one-rank group on this host
+                # instead of env:// failing on the variables torchrun would have set
+                for k, v in (("MASTER_ADDR", "127.0.0.1"), ("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0")):
+                    os.environ.setdefault(k, v)
+                os.environ.setdefault("MASTER_PORT", str(_free_port()))
             dist.init_process_group("nccl", device_id=self.device)
         self.train_id = train_id
         self.logger = logger or logging.getLogger(__name__)

@@ -113,13 +113,16 @@ def main():
     ap.add_argument("--hw", type=int, nargs=2, default=[H, W], help="map size (default the step's 65 x 129)")
     ap.add_argument("--nimg", type=int, default=1, help="images per call ([C][nimg][h][w]; 2 = the trainer's pair)")
     ap.add_argument("--which", default="fwd,dgrad,wgrad", help="the ops to time (a profiler pass over one of them)")
+    ap.add_argument("--form", default=None, help="the fp32 form (mfma_f32, bf16x6, f16x3; default: the library's)")
     a = ap.parse_args()
+    if a.form:
+        ops.set_f32_form(a.form)
     which = a.which.split(",")
     lib = hip.load()
     ops_list = [conv_ops(*s, h=a.hw[0], w=a.hw[1], nimg=a.nimg) for s in SHAPES if a.only is None or a.only in s[0]]
     for name, fwd, dgr, wgr, flops, check in ops_list:
         t = [timed(f, a.reps) if n in which else float("nan") for n, f in (("fwd", fwd), ("dgrad", dgr), ("wgrad", wgr))]
-        rec = {"hw": a.hw, "nimg": a.nimg, "op": name, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
+        rec = {"hw": a.hw, "nimg": a.nimg, "form": ops.f32_form(), "op": name, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
                "wgrad_us": round(t[2], 1), "fwd_tf": round(flops / t[0] / 1e6, 1),
                "wgrad_tf": round(flops / t[2] / 1e6, 1)}
         if a.check:

@@ -183,7 +183,7 @@ def test_grad_reducer_real_model_two_ranks(tmp_path):
                                       "other rank", other[sl][k]))
 
 
-def _graph_worker(rank, world, port, q):
+def _graph_worker(rank, world, port, q, pair=True):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                           WORLD_SIZE=str(world), LOCAL_RANK="0")
@@ -196,7 +196,7 @@ def _graph_worker(rank, world, port, q):
         for graph in (False, True):
             argv = ["--crop_size", f"{W},{H}", "--target_crop_size", f"{W},{H}", "--imagenet_pretrained", "False",
                     "--save_dir", "", "--target_mode", "IW_maxsquare", "--multi", "True", "--lambda_target", "0.09",
-                    "--iter_max", "1000", "--graph", str(graph)]
+                    "--iter_max", "1000", "--graph", str(graph), "--pair", str(pair)]
             args, _, _ = init_args(build_parser().parse_args(argv))
             tr = UDATrainer(args, cuda=True)
             tr.optimizer.zero_grad()
@@ -242,18 +242,20 @@ def _graph_worker(rank, world, port, q):
         raise
 
 
-def test_graphed_dp_step_matches_eager_dp():
+@pytest.mark.parametrize("pair", [True, False])
+def test_graphed_dp_step_matches_eager_dp(pair):
     """The captured data-parallel step (utils/graph.py: the forward/backward passes as graphs split at
     layer3's output and inside layer3, the exchange of each segment's gradients launched after its
     replay, the rest of the exchange after the last, then the graph of the SGD step) against the eager DP
     step with the overlapped bucket countdown, 2 ranks (gloo) x 4 UDA iterations: every loss and
     every parameter bit-identical (the step has no library kernel and the 2-rank sum is exact in
     either order), and the two replicas' parameters identical after every run (one exchange per
-    iteration keeps data-parallel replicas in lock step)."""
+    iteration keeps data-parallel replicas in lock step).  r06: also in two-pass mode (--pair False, the
+    reference's source-then-target order), whose captured step now cuts the target backward the same way."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, q, pair)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}

@@ -392,11 +392,13 @@ def test_loss_bwd_chunk_lds_bound(hi, wi, ho, wo):
         assert hi_ - lo <= wmax, (j, hi_ - lo, wmax)
 
 
-def _split_worker(rank, world, port, q):
+def _split_worker(rank, world, port, q, two_pass=False):
     """The split exchange of a captured DP step (utils/graph.py segments; solve_gta5.uda_step): bucket
     bounds end at each segment's end (set_breaks); after the first backward segment reduce_early launches
     only the buckets made of the parameters that segment finished, after the second reduce_more the next
-    ones, reduce_rest the others after the last segment."""
+    ones, reduce_rest the others after the last segment.  two_pass (r06, the reference's order): a source
+    backward that only accumulates runs first, unarmed, inside the first segment; the exchanged buffer is
+    then the rank-sum of both backwards' gradients."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
@@ -419,6 +421,10 @@ def _split_worker(rank, world, port, q):
     red._launch = lambda b: (log.append(("launch", b)), real(b))[1]
     opt.zero_grad()
     red.deferred = True                           # as under a graph capture: no hooks armed
+    if two_pass:
+        xs = torch.randn(4, 8, generator=g)
+        (2.0 * net(xs)).sum().backward()          # the source pass: accumulates, exchanges nothing
+        log.append(("source", 0))
     red.prepare_for_backward()
     net(x).sum().backward()
     log.append(("segment", 1))
@@ -433,11 +439,15 @@ def _split_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_dp_bucket_launches_interleave_gloo():
+@pytest.mark.parametrize("two_pass", [False, True])
+def test_dp_bucket_launches_interleave_gloo(two_pass):
+    """Pair mode and (r06) two-pass mode: nothing launched before the first segment ends (in two-pass mode
+    not during the source pass either), each bucket after the segment that finished it, every live bucket
+    once, both ranks holding the same reduced buffer."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q, two_pass)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(world)))
@@ -446,6 +456,9 @@ def test_dp_bucket_launches_interleave_gloo():
         assert p.exitcode == 0
     log, bounds, has_live, flat0, ends = got[0]
     assert all(any(hi == e for _, hi in bounds) for e in ends), (bounds, ends)  # buckets end at segment ends
+    if two_pass:
+        assert log[0] == ("source", 0)                    # nothing launched during the source pass
+        log = log[1:]
     assert log[0] == ("segment", 1)                       # nothing launched inside the backward
     cuts = [log.index(("segment", i)) for i in (1, 2, 3)] + [len(log)]
     limits = [0] + ends + [max(hi for _, hi in bounds)]
