@@ -138,6 +138,81 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const float* __restrict__ d
   }
 }
 
+// r06: the ResNet stem's pools (K = 3, S = 2: at most 2 x 2 windows cover an input pixel, and a window has at most
+// 3 x 3 taps) with every candidate loaded unconditionally from a clamped, valid address and masked afterwards, so
+// all of a thread's loads are in flight together; the same scan orders as k_maxpool_fwd / k_maxpool_bwd (the
+// same bits).  The generic kernels' loop bounds per thread left one or two dependent load chains per element:
+// 105 us backward, 38 us forward for the 1024x512 pair (profiles/r06_step_breakdown.txt).
+__global__ void __launch_bounds__(256) k_maxpool_fwd3(const float* __restrict__ x, int H, int W, int S, int PAD, int HO,
+                                                      int WO, long long total, float* __restrict__ y,
+                                                      int32_t* __restrict__ idx) {
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < (unsigned)total; e += gridDim.x * 256u) {
+    const int ox = (int)(e % (unsigned)WO);
+    const unsigned r = e / (unsigned)WO;
+    const int oy = (int)(r % (unsigned)HO);
+    const long long c = r / (unsigned)HO;
+    const int y0 = oy * S - PAD, x0 = ox * S - PAD;
+    const float* src = x + c * H * W;
+    float v[9];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const int yy = min(max(y0 + a, 0), H - 1), xx = min(max(x0 + b, 0), W - 1);
+        v[3 * a + b] = src[yy * W + xx];
+      }
+    const int ya = max(y0, 0), xa = max(x0, 0);
+    float best = -INFINITY;
+    int bi = ya * W + xa;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const int yy = y0 + a, xx = x0 + b;
+        const float t = v[3 * a + b];
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W && (t > best || t != t)) {
+          best = t;
+          bi = yy * W + xx;
+        }
+      }
+    y[e] = best;
+    idx[e] = bi;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_maxpool_bwd22(const float* __restrict__ dy, const int32_t* __restrict__ idx,
+                                                       int H, int W, int K, int S, int PAD, int HO, int WO,
+                                                       long long total, float* __restrict__ dx) {
+  for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < (unsigned)total; e += gridDim.x * 256u) {
+    const int xx = (int)(e % (unsigned)W);
+    const unsigned r = e / (unsigned)W;
+    const int y = (int)(r % (unsigned)H);
+    const long long c = r / (unsigned)H;
+    const int me = y * W + xx;
+    const int ly = y + PAD - (K - 1), lx = xx + PAD - (K - 1);
+    const int oy0 = ly <= 0 ? 0 : (ly + S - 1) / S, oy1 = min((y + PAD) / S, HO - 1);
+    const int ox0 = lx <= 0 ? 0 : (lx + S - 1) / S, ox1 = min((xx + PAD) / S, WO - 1);
+    const long long base = c * HO * WO;
+    int iv[4];
+    float dv[4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const long long o = base + (long long)min(oy0 + a, HO - 1) * WO + min(ox0 + b, WO - 1);
+        iv[2 * a + b] = idx[o];
+        dv[2 * a + b] = dy[o];
+      }
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        if (oy0 + a <= oy1 && ox0 + b <= ox1 && iv[2 * a + b] == me) s += dv[2 * a + b];
+    dx[e] = s;
+  }
+}
+
 // y[c][oy][ox] = x[c][oy*S][ox*S]   (fwd)      x[c][y][xx] = (y % S || xx % S) ? 0 : y'[..]  (bwd)
 __global__ void __launch_bounds__(256) k_subsample(const float* __restrict__ x, int H, int W, int S, int HO, int WO,
                                                    long long total, float* __restrict__ y) {
@@ -210,8 +285,12 @@ int msl_maxpool_fwd(const float* x, int c, int h, int w, int k, int stride, int 
   // every window must start inside the image (torch: the last window starts before h + pad)
   if ((long long)(ho - 1) * stride - pad >= h || (long long)(wo - 1) * stride - pad >= w) return MSL_ERR_SHAPE;
   const long long n = (long long)c * ho * wo;
-  MSL_LAUNCH(k_maxpool_fwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, k, stride, pad, ho,
-                     wo, n, y, idx);
+  if (k == 3)
+    MSL_LAUNCH(k_maxpool_fwd3, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, stride, pad, ho, wo, n, y,
+               idx);
+  else
+    MSL_LAUNCH(k_maxpool_fwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, h, w, k, stride, pad, ho,
+               wo, n, y, idx);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
@@ -220,8 +299,12 @@ int msl_maxpool_bwd(const float* dy, const int32_t* idx, int c, int h, int w, in
                     int wo, float* dx, msl_stream_t stream) {
   if (!dy || !idx || !dx || bad_geom(c, h, w, k, stride, pad, ho, wo) || 2 * pad > k) return MSL_ERR_ARG;
   const long long n = (long long)c * h * w;
-  MSL_LAUNCH(k_maxpool_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, idx, h, w, k, stride,
-                     pad, ho, wo, n, dx);
+  if (k <= 2 * stride)  // at most 2 x 2 windows per input pixel
+    MSL_LAUNCH(k_maxpool_bwd22, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, idx, h, w, k, stride, pad, ho,
+               wo, n, dx);
+  else
+    MSL_LAUNCH(k_maxpool_bwd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, idx, h, w, k, stride,
+               pad, ho, wo, n, dx);
   MSL_CHECK_LAUNCH();
   return MSL_OK;
 }
