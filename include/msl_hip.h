@@ -164,6 +164,19 @@ int msl_pconv_dgrad(const float* dy, const float* packed_dgrad, float* dx, int c
  * (Bottleneck.forward, deeplab_multi.py:31-48: conv1(x) and the identity residual both read x). */
 int msl_pconv_dgrad_acc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
                         int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream);
+/* msl_pconv_dgrad_acc's sum with the identity residual's gradient formed in the epilogue (r06):
+ * dx = mask(res) + W^T dy, mask(res)[c][n] = res[c][n] where the forward's y > 0 bit of that element is set
+ * (res_mask: msl_bn_fwd_mask's bits, rows c * nimg + image, cdiv(p / nimg, 64) words each), else 0.  dx is
+ * written, not read.  The bottleneck's bn3 backward (msl_bn_bwd_mask with dres = NULL) then need not write
+ * that gradient; replaces autograd's residual accumulation at deeplab_multi.py:31-48 (x feeds conv1 and
+ * the identity residual).  Workspace: msl_pconv_dgrad_workspace.  _sc: the dy partials as in the _sc
+ * entry points; _f16: the fp16 math as msl_pconv_dgrad_f16. */
+int msl_pconv_dgrad_resmask_sc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                               const float* res, const unsigned long long* res_mask, int nimg, const msl_forms* forms,
+                               void* ws, size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart);
+int msl_pconv_dgrad_resmask_f16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                                const float* res, const unsigned long long* res_mask, int nimg, const msl_forms* forms,
+                                void* ws, size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart);
 
 /* dw[cout][cin] (= or += when accumulate) = sum_p dy[cout][p] x[cin][p] */
 size_t msl_pconv_wgrad_workspace(int cin, int cout, int p);

@@ -543,7 +543,8 @@ template <int MT>
 static int launch_fwd_form(const float* img, int cimg, const float* packed, int M, const float* bias,
                            int nbias, float* out, int nbranch, int taps, int h, int w, int nimg, int dil0,
                            int dil1, const msl_forms* forms, void* ws, size_t ws_bytes, hipStream_t st,
-                           int accum = 0, const float* img_part = nullptr, int img_npart = 0) {
+                           int accum = 0, const float* img_part = nullptr, int img_npart = 0,
+                           const float* accres = nullptr, const unsigned long long* accmask = nullptr, int accni = 1) {
   if (forms_bad(forms)) return MSL_ERR_ARG;
   const int P = nimg * h * w;  // nimg images of h x w stacked along the pixel axis
   FwdPlan pl = plan_fwd(nbranch, taps, cimg, M, P, bias != nullptr);
@@ -590,6 +591,10 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
   a.bpart = nullptr;
   a.bnpart = 0;
   a.accum = accum;
+  a.accres = accres;  // (r06: the masked residual gradient of msl_pconv_dgrad_resmask*; needs accum)
+  a.accmask = accmask;
+  a.accni = accni;
+  if (accres && (!accum || !accmask || accni < 1 || P % accni != 0)) return MSL_ERR_ARG;
   a.A = packed;
   a.B = img;
   a.C = pl.S > 1 ? (float*)ws : out;
@@ -1261,6 +1266,16 @@ int msl_pconv_dgrad_acc_sc(const float* dy, const float* packed_dgrad, float* dx
                  as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart);
 }
 
+int msl_pconv_dgrad_resmask_sc(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                               const float* res, const unsigned long long* res_mask, int nimg, const msl_forms* forms,
+                               void* ws, size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart) {
+  if (bad_parts(dy_part, dy_npart)) return MSL_ERR_ARG;
+  if (bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx || !res || !res_mask || nimg < 1 || p % nimg)
+    return MSL_ERR_ARG;
+  return fwd_f32(forms, dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms, ws, ws_bytes,
+                 as_stream(stream), 1, dy_part, dy_npart, res, res_mask, nimg);
+}
+
 int msl_pconv_wgrad_sc(const float* x, const float* dy, float* dw, int cin, int cout, int p,
                        int accumulate, const msl_forms* forms, void* ws, size_t ws_bytes, msl_stream_t stream, const float* x_part,
                        int x_npart, const float* dy_part, int dy_npart) {
@@ -1391,6 +1406,16 @@ int msl_pconv_dgrad_f16(const float* dy, const float* packed_dgrad, float* dx, i
     return MSL_ERR_ARG;
   return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms, ws,
                                    ws_bytes, as_stream(stream), accumulate ? 1 : 0, dy_part, dy_npart);
+}
+
+int msl_pconv_dgrad_resmask_f16(const float* dy, const float* packed_dgrad, float* dx, int cin, int cout, int p,
+                                const float* res, const unsigned long long* res_mask, int nimg, const msl_forms* forms,
+                                void* ws, size_t ws_bytes, msl_stream_t stream, const float* dy_part, int dy_npart) {
+  if (!f16_ready(forms) || bad_parts(dy_part, dy_npart) || bad_dims(1, cin, cout, 1, p) || !dy || !packed_dgrad || !dx ||
+      !res || !res_mask || nimg < 1 || p % nimg)
+    return MSL_ERR_ARG;
+  return launch_fwd_form<kMathH1P>(dy, cout, packed_dgrad, cin, nullptr, 0, dx, 1, 1, 1, p, 1, 0, 0, forms, ws,
+                                   ws_bytes, as_stream(stream), 1, dy_part, dy_npart, res, res_mask, nimg);
 }
 
 int msl_pconv_wgrad_f16(const float* x, const float* dy, float* dw, int cin, int cout, int p, int accumulate, const msl_forms* forms,

@@ -29,12 +29,27 @@ struct FwdArgs {
   const void* Ax6;    // kMathX6P/PP: A split into bf16 planes [ks][plane][k half][lda][8] (k_split_pack)
   const void* Bx6;    // the BP form: the image operand's fp16 planes (k_split_img)
   int accum;          // stream-K forms: C = C_old + result (the fused residual-gradient sum)
+  // r06, accum with accres != null: C = mask(accres) + result instead, mask(accres)[m][n] = accres[m][n] where bit
+  // (n % hw) of row m * accni + n / hw of accmask is set, else 0 (hw = P / accni): the identity residual's
+  // gradient of a bottleneck - its bn3 backward's ReLU-masked dy - formed in this epilogue from dy and the
+  // forward's y > 0 bits, so the BN backward need not write it (msl_pconv_dgrad_resmask*)
+  const float* accres;
+  const unsigned long long* accmask;
+  int accni;
   // kMathH3P: Ax6 holds A * sA as two fp16 planes [ks][plane][k half][lda][8]; ascale = {sA,
   // 1/sA} (written by the pack); bpart = the kNPart absmax partials of B (k_absmax)
   const float* ascale;
   const float* bpart;
   int bnpart;  // partials in bpart
 };
+
+// mask(accres)[m][n] of FwdArgs (r06): accres[m * P + n] if the forward's y > 0 bit of that element is set
+__device__ __forceinline__ float acc_masked(const FwdArgs& a, int m, int n) {
+  const int hw = a.P / a.accni;
+  const int img = n / hw, px = n - img * hw;
+  const unsigned long long w = a.accmask[(long long)(m * a.accni + img) * ((hw + 63) >> 6) + (px >> 6)];
+  return ((w >> (px & 63)) & 1ull) ? a.accres[(long long)m * a.P + n] : 0.f;
+}
 
 struct WgradArgs {
   const float* dy;  // [M][P]
@@ -1387,11 +1402,36 @@ __device__ __forceinline__ void fwd_sk_body(FwdArgs a, SkArgs sk) {
         // previous element's store: +30 us on a 2048 x 8385 output)
         float old[16];
         if constexpr (ACC) {
+          if (a.accres) {  // r06: the masked residual gradient (acc_masked) instead of C's old values
+            // the lane's column fixes the image, the mask word (32-bit half) and the bit once per
+            // fragment; the 16 rows then differ by constant strides (buffer loads, OOB -> 0)
+            const int hw = a.P / a.accni;
+            const int img = n / hw, px = n - img * hw;
+            const int w32 = ((hw + 63) >> 6) * 2;  // 32-bit mask words per (row, image)
+            const unsigned mstride = (unsigned)(a.accni * w32 * 4);
+            const unsigned moff = n < a.P ? (unsigned)(((mrow * a.accni + img) * w32 + (px >> 5)) * 4) : OOB;
+            const int sh = px & 31;
+            const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)a.accres, (short)0, (int)min(0x7fffffffLL, (long long)a.M * a.P * 4), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rmk = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)a.accmask, (short)0, (int)min(0x7fffffffLL, (long long)a.M * mstride), 0x00020000);
+            unsigned mw[16];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ro = (r & 3) + 8 * (r >> 2);
-            const unsigned off = full_m ? voff + ro * a.P * 4 : (mrow + ro < a.M ? voff + ro * a.P * 4 : OOB);
-            old[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, off, 0, 0));
+            for (int r = 0; r < 16; ++r) {
+              const int ro = (r & 3) + 8 * (r >> 2);
+              const bool in = full_m || mrow + ro < a.M;
+              old[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, in ? voff + ro * a.P * 4 : OOB, 0, 0));
+              mw[r] = __builtin_amdgcn_raw_buffer_load_b32(rmk, in && n < a.P ? moff + ro * mstride : OOB, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) old[r] = ((mw[r] >> sh) & 1u) ? old[r] : 0.f;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int ro = (r & 3) + 8 * (r >> 2);
+              const unsigned off = full_m ? voff + ro * a.P * 4 : (mrow + ro < a.M ? voff + ro * a.P * 4 : OOB);
+              old[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, off, 0, 0));
+            }
           }
         }
 #pragma unroll
@@ -1489,8 +1529,13 @@ __global__ void __launch_bounds__(256) k_sk_reduce(FwdArgs a, SkArgs sk) {
     }
     if (a.accum) {  // all four old values loaded before the first store
       float old[4];
+      if (a.accres) {  // r06: the masked residual gradient (acc_masked)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) old[c] = n + c < a.P ? dst[c] : 0.f;
+        for (int c = 0; c < 4; ++c) old[c] = n + c < a.P ? acc_masked(a, m, n + c) : 0.f;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) old[c] = n + c < a.P ? dst[c] : 0.f;
+      }
 #pragma unroll
       for (int c = 0; c < 4; ++c) vals[c] = old[c] + vals[c];
     }

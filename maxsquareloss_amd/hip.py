@@ -108,10 +108,16 @@ SIGNATURES = {
     "msl_sgd_step": (c_int, [c_p, c_p, c_p, c_ll, c_f, c_f, c_f, c_f, c_f, c_p]),
     "msl_sgd_step_lr_dev": (c_int, [c_p, c_p, c_p, c_ll, c_p, c_f, c_f, c_f, c_p]),
     "msl_launch_guard_probe": (c_int, [c_int, c_p, c_p]),
+    "msl_pconv_dgrad_resmask_sc": (c_int, [c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_int, c_p, c_p, c_sz, c_p, c_p,
+                                           c_int]),
+    "msl_pconv_dgrad_resmask_f16": (c_int, [c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_int, c_p, c_p, c_sz, c_p,
+                                            c_p, c_int]),
 }
 
 ABI_VERSION = 3
-_DIAGNOSTIC = {"msl_launch_guard_probe"}  # r06 diagnostics, not on any compute path
+# r06 entry points an older build (MSL_LIB_PATH, a same-box A/B) may lack: the diagnostics probe and the masked
+# residual dgrad (ops.py falls back to the materialised residual gradient without it)
+_DIAGNOSTIC = {"msl_launch_guard_probe", "msl_pconv_dgrad_resmask_sc", "msl_pconv_dgrad_resmask_f16"}
 _lib = None
 
 

@@ -648,9 +648,17 @@ class _PConv(Function):
             acc = 0
             if hold is not None:
                 hold.consumed = True
+            res = None
             if hold is not None and hold.g is not None:
-                dx, hold.g = hold.g, None
-                acc = 1
+                if isinstance(hold.g, MaskedResidual):
+                    res, hold.g = hold.g, None
+                    if math == "bf16":  # the bf16 form has no epilogue of either kind
+                        dx, res, acc = res.materialize(), None, 1
+                    else:
+                        dx = torch.empty_like(x)
+                else:
+                    dx, hold.g = hold.g, None
+                    acc = 1
             else:
                 dx = torch.empty_like(x)
             packed_d = cache.get([weight], cin, cout, 1)
@@ -663,6 +671,11 @@ class _PConv(Function):
                                                    cnt, ws.data_ptr(), wsb, s), "msl_pconv_dgrad")
                 if acc:  # the bf16 form has no accumulate epilogue
                     dx.add_(tgt)
+            elif res is not None:  # r06: dx = mask(dy of bn3) + W^T dy, the mask applied in the epilogue
+                fn = lib.msl_pconv_dgrad_resmask_f16 if math == "fp16" else lib.msl_pconv_dgrad_resmask_sc
+                hip.check(fn(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, res.dy.data_ptr(),
+                             res.bits.data_ptr(), res.nimg, cnt, ws.data_ptr(), wsb, s, *_pp(gpart)),
+                          "msl_pconv_dgrad_resmask")
             else:
                 fn = lib.msl_pconv_dgrad_f16 if math == "fp16" else lib.msl_pconv_dgrad_acc_sc
                 hip.check(fn(gy.data_ptr(), packed_d.data_ptr(), dx.data_ptr(), cin, cout, p, acc, cnt,
@@ -715,6 +728,27 @@ class ResidualGrad:
     def __init__(self):
         self.g = None
         self.consumed = False  # the summing conv's backward ran (a later producer hands to autograd)
+
+
+class MaskedResidual:
+    """r06: the identity residual's gradient left unmaterialised - relu'(y) * dy of the block's bn3, as
+    bn3's output gradient `dy` and its forward's ReLU mask bits (msl_bn_fwd_mask).  conv1's data-gradient
+    GEMM applies the mask in its epilogue (msl_pconv_dgrad_resmask), so bn3's backward skips writing the
+    masked copy (one activation-sized write and read per identity block)."""
+
+    __slots__ = ("dy", "bits", "nimg")
+
+    def __init__(self, dy, bits, nimg):
+        self.dy, self.bits, self.nimg = dy, bits, nimg
+
+    def materialize(self):
+        """The masked gradient as a tensor (the bf16 data-gradient form, which has no epilogue for it)."""
+        c, hw = self.dy.size(1), self.dy.size(-2) * self.dy.size(-1)
+        words = self.bits.view(c * self.nimg, (hw + 63) // 64)  # [channel][image][word] (msl_bn_relu_mask_bytes)
+        idx = torch.arange(hw, device=self.dy.device)
+        on = ((words[:, idx // 64] >> (idx % 64)) & 1).bool()  # [channel * image][pixel]
+        g = self.dy.reshape(c * self.nimg, hw)  # (1,C[,N],H,W): channel-major, images inside
+        return torch.where(on, g, torch.zeros((), dtype=g.dtype, device=g.device)).reshape(self.dy.shape)
 
 
 # --------------------------------------------------------------------------- stem, maxpool, stride-2 glue
@@ -1191,6 +1225,7 @@ def iw_maxsquare_prob(prob, label, ratio):
 # for the backward (msl_bn_fwd_mask / msl_bn_bwd_mask) instead of re-reading the block output; the same
 # mask bit for bit (tests/test_gpu_ops.py test_bn_relu_mask_bits).  False: the backward reads y.
 BN_MASK_BITS = True
+RESMASK_DGRAD = True  # r06: MaskedResidual instead of bn3 writing the residual gradient
 
 
 class _BNAct(Function):
@@ -1249,7 +1284,11 @@ class _BNAct(Function):
         nig = ctx.needs_input_grad
         dx = torch.empty_like(x) if nig[0] else None
         hold = ctx.hold
-        dres = torch.empty_like(x) if (nig[3] or hold is not None) else None
+        # r06: an identity block's residual gradient stays unmaterialised (MaskedResidual) when conv1's
+        # data-gradient form has the masked epilogue
+        lazy = (hold is not None and not nig[3] and ctx.bits is not None and RESMASK_DGRAD and
+                CONV_MATH != "bf16" and hasattr(lib, "msl_pconv_dgrad_resmask_sc"))
+        dres = torch.empty_like(x) if (nig[3] or (hold is not None and not lazy)) else None
         sw = grad_sink(weight) if nig[1] else None
         sb = grad_sink(ctx.bias) if nig[2] else None
         direct = sw is not None and sb is not None
@@ -1281,7 +1320,7 @@ class _BNAct(Function):
             sb[1].notify(sb[2])
             dgamma = dbeta = None
         if hold is not None:  # handed to the block's conv1 backward (ResidualGrad)
-            hold.g = dres
+            hold.g = MaskedResidual(gy, ctx.bits, n) if lazy else dres
             dres = None
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 

@@ -35,7 +35,7 @@ def timed(fn, reps):
     return e0.elapsed_time(e1) / reps * 1e3  # us
 
 
-def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W, nimg=1):
+def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W, nimg=1, dgrad_mode="plain"):
     """(label, fwd, dgrad, wgrad callables, flops, reference checker) for one conv shape."""
     g = torch.Generator().manual_seed(cin + cout)
     x = torch.relu(torch.randn(1, cin, nimg, h, w, generator=g)).to(DEV)  # [C][nimg][h][w]
@@ -59,7 +59,14 @@ def conv_ops(name, cin, cout, k, d, nb=1, h=H, w=W, nimg=1):
         fwd = lambda: hip.check(lib.msl_pconv_fwd_sc(x.data_ptr(), pf.data_ptr(), y.data_ptr(), cin, cout, p, cnt,  # noqa: E731
                                                      wsf.data_ptr(), wsf.numel(), s, *ops._pp(xpart)), "fwd")
         dgr = lambda: hip.check(lib.msl_pconv_dgrad_acc_sc(gy.data_ptr(), pd.data_ptr(), dx.data_ptr(), cin, cout, p,  # noqa: E731
-                                                           0, cnt, wsd.data_ptr(), wsd.numel(), s, *ops._pp(gpart)), "dgrad")
+                                                           int(dgrad_mode == "acc"), cnt, wsd.data_ptr(), wsd.numel(), s,
+                                                           *ops._pp(gpart)), "dgrad")
+        if dgrad_mode == "resmask":  # r06: the masked residual gradient added in the epilogue (timing only)
+            res = torch.randn(1, cin, nimg, h, w, generator=g).to(DEV)
+            bits = torch.randint(-2**62, 2**62, (cin * nimg * ((h * w + 63) // 64),), generator=g).to(DEV)
+            dgr = lambda: hip.check(lib.msl_pconv_dgrad_resmask_sc(  # noqa: E731
+                gy.data_ptr(), pd.data_ptr(), dx.data_ptr(), cin, cout, p, res.data_ptr(), bits.data_ptr(), nimg, cnt,
+                wsd.data_ptr(), wsd.numel(), s, *ops._pp(gpart)), "dgrad")
         wgr = lambda: hip.check(lib.msl_pconv_wgrad_sc(x.data_ptr(), gy.data_ptr(), dw.data_ptr(), cin, cout, p, 0,  # noqa: E731
                                                        cnt, wsw.data_ptr(), wsw.numel(), s, *ops._pp(xpart),
                                                        *ops._pp(gpart)), "wgrad")
@@ -114,15 +121,17 @@ def main():
     ap.add_argument("--nimg", type=int, default=1, help="images per call ([C][nimg][h][w]; 2 = the trainer's pair)")
     ap.add_argument("--which", default="fwd,dgrad,wgrad", help="the ops to time (a profiler pass over one of them)")
     ap.add_argument("--form", default=None, help="the fp32 form (mfma_f32, bf16x6, f16x3; default: the library's)")
+    ap.add_argument("--dgrad-mode", default="plain", choices=["plain", "acc", "resmask"],
+                    help="1x1 data gradient: dx =, dx +=, or dx = masked residual + (msl_pconv_dgrad_resmask)")
     a = ap.parse_args()
     if a.form:
         ops.set_f32_form(a.form)
     which = a.which.split(",")
     lib = hip.load()
-    ops_list = [conv_ops(*s, h=a.hw[0], w=a.hw[1], nimg=a.nimg) for s in SHAPES if a.only is None or a.only in s[0]]
+    ops_list = [conv_ops(*s, h=a.hw[0], w=a.hw[1], nimg=a.nimg, dgrad_mode=a.dgrad_mode) for s in SHAPES if a.only is None or a.only in s[0]]
     for name, fwd, dgr, wgr, flops, check in ops_list:
         t = [timed(f, a.reps) if n in which else float("nan") for n, f in (("fwd", fwd), ("dgrad", dgr), ("wgrad", wgr))]
-        rec = {"hw": a.hw, "nimg": a.nimg, "form": ops.f32_form(), "op": name, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
+        rec = {"hw": a.hw, "nimg": a.nimg, "form": ops.f32_form(), "op": name, "dgrad_mode": a.dgrad_mode, "fwd_us": round(t[0], 1), "dgrad_us": round(t[1], 1),
                "wgrad_us": round(t[2], 1), "fwd_tf": round(flops / t[0] / 1e6, 1),
                "wgrad_tf": round(flops / t[2] / 1e6, 1)}
         if a.check:

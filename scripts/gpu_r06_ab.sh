@@ -11,7 +11,7 @@ if [ "$1" = "--skip-checks" ]; then
 else
   timeout -k 10 300 python -u scripts/bench_ops.py --nimg 2 --check --reps 5 > gpurun_out/${TAG}_check.log 2>&1 || exit $?
   timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ops.py \
-    -k "dconv_fwd_bwd or f16x3 or conv_fp16_math or wgrad or aspp or launch_guard" > gpurun_out/${TAG}_tests.log 2>&1 || exit $?
+    -k "dconv_fwd_bwd or f16x3 or conv_fp16_math or wgrad or aspp or launch_guard or pconv or conv1x1 or sk_hybrid or bottleneck or masked_residual" > gpurun_out/${TAG}_tests.log 2>&1 || exit $?
   timeout -k 10 300 python -u scripts/dbg_det.py > gpurun_out/${TAG}_det.log 2>&1 || exit $?
 fi
 scripts/gpu_ab.sh "$TAG" "$@"

@@ -725,6 +725,67 @@ def test_bottleneck_fused_residual_grad(f32_form, monkeypatch, kind):
         assert _rel(a, b.double()) < 1e-6
 
 
+@pytest.mark.parametrize("nimg", [1, 2])
+@pytest.mark.parametrize("math", ["fp32", "fp16", "bf16"])
+def test_masked_residual_grad(monkeypatch, math, nimg):
+    """r06: an identity block's residual gradient left unmaterialised (ops.MaskedResidual, the ReLU mask
+    applied in conv1's data-gradient epilogue, msl_pconv_dgrad_resmask) gives bit-identical gradients to
+    bn3 writing it (RESMASK_DGRAD off); bf16, whose form has no epilogue, materialises it."""
+    from maxsquareloss_amd.graphs.models import deeplab_multi as dm
+    made = []
+
+    class Counted(ops.MaskedResidual):
+        __slots__ = ()
+
+        def __init__(self, *a):
+            super().__init__(*a)
+            made.append(1)
+
+    monkeypatch.setattr(ops, "MaskedResidual", Counted)
+    torch.manual_seed(5 + nimg)
+    blk = dm.Bottleneck(1024, 256, dilation=2).to(DEV).train()
+    shape = (1, 1024, nimg, 17, 33) if nimg > 1 else (1, 1024, 17, 33)
+    x = (torch.randn(*shape) * 2).to(DEV)
+    gy = torch.randn(*shape).to(DEV)
+    out = {}
+    prev = ops.CONV_MATH
+    try:
+        ops.set_conv_math(math)
+        for lazy in (True, False):
+            monkeypatch.setattr(ops, "RESMASK_DGRAD", lazy)
+            xg = x.clone().requires_grad_()
+            for prm in blk.parameters():
+                prm.grad = None
+            y = blk(xg)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            out[lazy] = (y.detach().clone(), xg.grad.clone(), [prm.grad.clone() for prm in blk.parameters()])
+    finally:
+        ops.set_conv_math(prev)
+    assert len(made) == (1 if math != "bf16" else 0)
+    assert torch.equal(out[True][0], out[False][0])
+    assert torch.equal(out[True][1], out[False][1])
+    for a, b in zip(out[True][2], out[False][2]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("nimg", [1, 2])
+def test_masked_residual_materialize(nimg):
+    """MaskedResidual.materialize (the bf16 path) equals dy * (y > 0) of the BN's own forward."""
+    torch.manual_seed(9)
+    bn = torch.nn.BatchNorm2d(256).to(DEV).train()
+    shape = (1, 256, nimg, 17, 33) if nimg > 1 else (1, 256, 17, 33)
+    x = torch.randn(*shape).to(DEV).requires_grad_()
+    res = torch.randn(*shape).to(DEV)
+    hold = ops.ResidualGrad()
+    y = ops.bn_act(bn, x, residual=res, relu=True, residual_grad=hold)
+    gy = torch.randn(*shape).to(DEV)
+    y.backward(gy)
+    torch.cuda.synchronize()
+    assert isinstance(hold.g, ops.MaskedResidual)
+    assert torch.equal(hold.g.materialize(), torch.where(y > 0, gy, torch.zeros_like(gy)))
+
+
 @pytest.mark.parametrize("cin,cout,h,w", [(256, 1024, 65, 129), (512, 2048, 64, 128), (2048, 512, 65, 129),
                                            (1024, 2048, 17, 33)])
 def test_sk_hybrid_schedule(cin, cout, h, w, f32_form):
