@@ -489,6 +489,26 @@ __device__ __forceinline__ float bn_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, 
 __device__ __forceinline__ void bn_st(__amdgpu_buffer_rsrc_t r, unsigned voff, int j, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, j * kBnFusedThreads * 4, 0);
 }
+// r06: element block j's offset in the lane's VGPR offset (v + j * 4 KB), not in the scalar offset: the buffer range
+// check covers the VGPR and immediate offsets only, so with the block offset there a lane past the row reads 0 and
+// its store is dropped by the hardware - no per-element range test (and no branch) around the access
+// (the add is an opaque asm statement, so each access computes its offset next to itself: as a plain add the
+// compiler kept the EPT offsets live from the loads to the stores - 16 more VGPRs at EPT 16).  The backward's
+// forms from kBnVoffMinEpt elements on (EPT 16: 14 -> 8 spilled VGPRs, 43 -> 8 SGPRs; EPT 33: 46 SGPRs -> none);
+// the smaller ones keep the scalar block offset and explicit range tests, which they hold without spilling
+__device__ __forceinline__ unsigned bn_voff(unsigned voff, int j) {
+  if (j == 0) return voff;
+  unsigned r;
+  asm volatile("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "i"(j * kBnFusedThreads * 4), "v"(voff));
+  return r;
+}
+__device__ __forceinline__ float bn_ldv(__amdgpu_buffer_rsrc_t r, unsigned voff, int j) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, bn_voff(voff, j), 0, 0));
+}
+__device__ __forceinline__ void bn_stv(__amdgpu_buffer_rsrc_t r, unsigned voff, int j, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, bn_voff(voff, j), 0, 0);
+}
+constexpr int kBnVoffMinEpt = 16;
 constexpr int kBnTwoBlockEpt = 16;  // forms built for two blocks per CU (64 VGPRs)
 
 // N fp64 sums over the block, each in block_sum2_d16's order (wave xor-shuffle, then the 16 waves in order):
@@ -649,8 +669,13 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
 template <int EPT, int NB>
 __device__ __forceinline__ void bn_bwd_rows(const BnBwdArgs& a, int c, int img0, double* red, float& am, float& dg,
                                             float& db) {
-  const int t = threadIdx.x, P = a.P;
+  // t through an opaque register copy (r06): the image loop of the one-image form cannot hoist the EPT per-element
+  // range tests out of the loop, where they were held across it (EPT = 16: 43 spilled SGPRs, 14 spilled VGPRs)
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  const int P = a.P;
   const unsigned vo = (unsigned)t * 4u;
+  constexpr bool VF = EPT >= kBnVoffMinEpt;
   float g[NB][EPT], xv[NB][EPT];
   float mean[NB], invstd[NB];
 #pragma unroll
@@ -661,10 +686,15 @@ __device__ __forceinline__ void bn_bwd_rows(const BnBwdArgs& a, int c, int img0,
     invstd[b] = a.save_invstd[r];
     const __amdgpu_buffer_rsrc_t rdy = bn_row(a.dy + base, P), rx = bn_row(a.x + base, P);
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      const int e = j * kBnFusedThreads + t;
-      g[b][j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
-      xv[b][j] = e < P ? bn_ld(rx, vo, j) : 0.f;
+    for (int j = 0; j < EPT; ++j) {  // 0 past P
+      if constexpr (VF) {
+        g[b][j] = bn_ldv(rdy, vo, j);
+        xv[b][j] = bn_ldv(rx, vo, j);
+      } else {
+        const int e = j * kBnFusedThreads + t;
+        g[b][j] = e < P ? bn_ld(rdy, vo, j) : 0.f;
+        xv[b][j] = e < P ? bn_ld(rx, vo, j) : 0.f;
+      }
     }
   }
   const float gm = a.gamma ? a.gamma[c] : 1.f;
@@ -674,21 +704,28 @@ __device__ __forceinline__ void bn_bwd_rows(const BnBwdArgs& a, int c, int img0,
     const int r = c * a.NI + img0 + b;
     const float w = invstd[b] * gm;
     if (a.relu && a.mask) {  // the forward's y > 0 bits: one 8-byte word per wave and element block
+      // r06: lane j of each wave loads element block j's word (the forward's store layout) and block j reads it
+      // back with readlane (wave-uniform, scalar registers): one load per lane instead of EPT 64-bit vector
+      // loads, which the compiler hoisted next to the row loads - 32 more VGPRs at EPT 16, 15 of them spilled
       const unsigned long long* mrow = a.mask + (long long)r * cdiv(P, 64);
+      const int l = t & 63;
+      unsigned long long mw = 0;
+      if (l < EPT && l * kBnFusedThreads + (t & ~63) < P) mw = mrow[l * (kBnFusedThreads / 64) + (t >> 6)];
+      const unsigned mlo = (unsigned)mw, mhi = (unsigned)(mw >> 32);
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        const int e = j * kBnFusedThreads + t;
-        if (j * kBnFusedThreads + (t & ~63) < P) {  // wave-uniform: the word exists
-          const unsigned long long bits = mrow[j * (kBnFusedThreads / 64) + (t >> 6)];
-          if (e < P && !((bits >> (t & 63)) & 1ull)) g[b][j] = 0.f;
-        }
+      for (int j = 0; j < EPT; ++j) {  // (g = 0 past P already)
+        const unsigned half = l < 32 ? __builtin_amdgcn_readlane(mlo, j) : __builtin_amdgcn_readlane(mhi, j);
+        if (!((half >> (l & 31)) & 1u)) g[b][j] = 0.f;
       }
     } else if (a.relu && a.y) {
       const __amdgpu_buffer_rsrc_t ryy = bn_row(a.y + (long long)r * P, P);
 #pragma unroll
       for (int j = 0; j < EPT; ++j) {
-        const int e = j * kBnFusedThreads + t;
-        if (e < P && !(bn_ld(ryy, vo, j) > 0.f)) g[b][j] = 0.f;
+        if constexpr (VF) {
+          if (!(bn_ldv(ryy, vo, j) > 0.f)) g[b][j] = 0.f;
+        } else {
+          if (j * kBnFusedThreads + t < P && !(bn_ld(ryy, vo, j) > 0.f)) g[b][j] = 0.f;
+        }
       }
     } else if (a.relu) {  // y > 0 recomputed with k_bn_fwd_fused's operations (its alpha, bsh)
       if constexpr (EPT <= kBnRemaskMaxEpt) {  // (the 33-element form spills twice as much with it)
@@ -729,10 +766,14 @@ __device__ __forceinline__ void bn_bwd_rows(const BnBwdArgs& a, int c, int img0,
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const int e = j * kBnFusedThreads + t;
-      if (e < P) {
-        const float xh = (xv[b][j] - mean[b]) * invstd[b];
+      const float xh = (xv[b][j] - mean[b]) * invstd[b];
+      const float d = __fmul_rn(__fmaf_rn(-xh, m2, __fsub_rn(g[b][j], m1)), w);
+      if constexpr (VF) {  // (stores past P dropped by bn_stv)
+        if (a.dres) bn_stv(rdres, vo, j, g[b][j]);
+        if (a.dx) bn_stv(rdx, vo, j, d);
+        if (e < P) am = fmaxf(am, fabsf(d));
+      } else if (e < P) {
         if (a.dres) bn_st(rdres, vo, j, g[b][j]);
-        const float d = __fmul_rn(__fmaf_rn(-xh, m2, __fsub_rn(g[b][j], m1)), w);
         if (a.dx) bn_st(rdx, vo, j, d);
         am = fmaxf(am, fabsf(d));
       }

@@ -98,8 +98,17 @@ def main():
                                               beta.data_ptr(), sm.data_ptr(), si.data_ptr(), dx.data_ptr(),
                                               hip.ptr(dres), dg.data_ptr(), db.data_ptr(), c, p, n, 1, int(relu), 0,
                                               hip.forms(), ws.data_ptr(), wsb, s, ba.data_ptr()), "bwd_mask")
+            def bwdm_nodres():  # r06: the identity block's backward (ops.MaskedResidual: no residual gradient)
+                hip.check(lib.msl_bn_bwd_mask(gy.data_ptr(), x.data_ptr(), bits.data_ptr(), gamma.data_ptr(),
+                                              beta.data_ptr(), sm.data_ptr(), si.data_ptr(), dx.data_ptr(),
+                                              None, dg.data_ptr(), db.data_ptr(), c, p, n, 1, int(relu), 0,
+                                              hip.forms(), ws.data_ptr(), wsb, s, ba.data_ptr()), "bwd_mask")
             rec["fwd_mask_us"] = round(timed(fwdm, args.reps), 2)
+            rec["fwd_mask_TBps"] = round(mb * 3 / rec["fwd_mask_us"], 3)
             rec["bwd_mask_us"] = round(timed(bwdm, args.reps), 2)
+            rec["bwd_mask_TBps"] = round(mb * 4 / rec["bwd_mask_us"], 3)
+            rec["bwd_mask_nodres_us"] = round(timed(bwdm_nodres, args.reps), 2)
+            rec["bwd_mask_nodres_TBps"] = round(mb * 3 / rec["bwd_mask_nodres_us"], 3)
         if relu and not res and not args.unfused:
             t = timed(bwd(False), args.reps)
             rec["bwd_remask_us"] = round(t, 2)
