@@ -509,6 +509,7 @@ __device__ __forceinline__ void bn_stv(__amdgpu_buffer_rsrc_t r, unsigned voff, 
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, bn_voff(voff, j), 0, 0);
 }
 constexpr int kBnVoffMinEpt = 16;
+constexpr bool kBnOpaqueAll = false;  // the opaque thread index in the smaller forms too
 constexpr int kBnTwoBlockEpt = 16;  // forms built for two blocks per CU (64 VGPRs)
 
 // N fp64 sums over the block, each in block_sum2_d16's order (wave xor-shuffle, then the 16 waves in order):
@@ -539,7 +540,10 @@ __device__ __forceinline__ void block_sum_d16(double (&v)[N], double* red) {
 // the running statistics and the batch counter are updated image by image, image 0 first, as before.
 template <int EPT, int NB>
 __device__ __forceinline__ void bn_fwd_rows(const BnArgs& a, int c, int img0, double* red, float& am) {
-  const int t = threadIdx.x, P = a.P;
+  constexpr bool VF = EPT >= kBnVoffMinEpt;  // (as bn_bwd_rows)
+  int t = threadIdx.x;
+  if constexpr (VF || kBnOpaqueAll) asm volatile("" : "+v"(t));
+  const int P = a.P;
   const unsigned vo = (unsigned)t * 4u;
   float xv[NB][EPT];
   double sh[NB];
@@ -549,8 +553,12 @@ __device__ __forceinline__ void bn_fwd_rows(const BnArgs& a, int c, int img0, do
     const __amdgpu_buffer_rsrc_t rx = bn_row(a.x + base, P);
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int e = j * kBnFusedThreads + t;
-      xv[b][j] = e < P ? bn_ld(rx, vo, j) : 0.f;
+      if constexpr (VF) {
+        xv[b][j] = bn_ldv(rx, vo, j);
+      } else {
+        const int e = j * kBnFusedThreads + t;
+        xv[b][j] = e < P ? bn_ld(rx, vo, j) : 0.f;
+      }
     }
   }
 #pragma unroll
@@ -606,7 +614,12 @@ __device__ __forceinline__ void bn_fwd_rows(const BnArgs& a, int c, int img0, do
     if (a.residual) {
       const __amdgpu_buffer_rsrc_t rr = bn_row(a.residual + base, P);
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) rv[j] = j * kBnFusedThreads + t < P ? bn_ld(rr, vo, j) : 0.f;
+      for (int j = 0; j < EPT; ++j) {
+        if constexpr (VF)
+          rv[j] = bn_ldv(rr, vo, j);
+        else
+          rv[j] = j * kBnFusedThreads + t < P ? bn_ld(rr, vo, j) : 0.f;
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < EPT; ++j) rv[j] = 0.f;
@@ -620,7 +633,16 @@ __device__ __forceinline__ void bn_fwd_rows(const BnArgs& a, int c, int img0, do
     for (int j = 0; j < EPT; ++j) {
       const int e = j * kBnFusedThreads + t;
       bool pos = false;
-      if (e < P) {
+      if constexpr (VF) {  // (stores past P dropped by bn_stv)
+        float v = __fmaf_rn(xv[b][j], alpha[b], bsh[b]);
+        v += rv[j];
+        v = a.relu ? fmaxf(v, 0.f) : v;
+        bn_stv(ry, vo, j, v);
+        if (e < P) {
+          am = fmaxf(am, fabsf(v));
+          pos = v > 0.f;
+        }
+      } else if (e < P) {
         float v = __fmaf_rn(xv[b][j], alpha[b], bsh[b]);
         v += rv[j];
         v = a.relu ? fmaxf(v, 0.f) : v;
@@ -671,11 +693,11 @@ __device__ __forceinline__ void bn_bwd_rows(const BnBwdArgs& a, int c, int img0,
                                             float& db) {
   // t through an opaque register copy (r06): the image loop of the one-image form cannot hoist the EPT per-element
   // range tests out of the loop, where they were held across it (EPT = 16: 43 spilled SGPRs, 14 spilled VGPRs)
+  constexpr bool VF = EPT >= kBnVoffMinEpt;
   int t = threadIdx.x;
-  asm volatile("" : "+v"(t));
+  if constexpr (VF || kBnOpaqueAll) asm volatile("" : "+v"(t));
   const int P = a.P;
   const unsigned vo = (unsigned)t * 4u;
-  constexpr bool VF = EPT >= kBnVoffMinEpt;
   float g[NB][EPT], xv[NB][EPT];
   float mean[NB], invstd[NB];
 #pragma unroll
