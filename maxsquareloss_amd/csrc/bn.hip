@@ -835,6 +835,10 @@ __global__ void __launch_bounds__(kBnFusedThreads) __attribute__((amdgpu_waves_p
 // image-by-image kernel's two blocks per CU win (512 ch fwd 18.1 vs 23.3 us, 1024 ch + residual 37.5 vs 46.0;
 // profiles/r06_bn_pair_ab.txt); at 16 elements the pair's registers spill.
 constexpr int kBnJointPair = 1;
+// r06: the joint forward at 16 elements too (128 VGPRs, one block per CU, no spill: config-5 256-channel maps 15.4 vs
+// 17.1 us); the joint backward spills 33 VGPRs there and is slower (remask 28.6 vs 21.8 us; profiles/r06_bn_joint16_ab.txt)
+constexpr bool kBnJoint16Fwd = true;
+constexpr bool kBnJoint16Bwd = false;
 constexpr int kBnJointMaxC = 256;
 template <typename K, typename A>
 static int bn_launch_fused(K k4, K k9, K k16, K k33, K j4, K j9, K j16, int c, int p, hipStream_t st, const A& a) {
@@ -941,7 +945,7 @@ int msl_bn_fwd_mask(const float* x, const float* gamma, const float* beta, const
   a.absmax = absmax;
   a.mask = reinterpret_cast<unsigned long long*>(relu_mask);
   if (fused) return bn_launch_fused(k_bn_fwd_fused<4>, k_bn_fwd_fused<9>, k_bn_fwd_fused<16>, k_bn_fwd_fused<33>,
-                                        k_bn_fwd_fused<4, true>, k_bn_fwd_fused<9, true>, k_bn_fwd_fused<16>, c, p, st,
+                                        k_bn_fwd_fused<4, true>, k_bn_fwd_fused<9, true>, k_bn_fwd_fused<16, kBnJoint16Fwd>, c, p, st,
                                         a);
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec)
@@ -1010,7 +1014,7 @@ static int bn_bwd(const float* dy, const float* x, const float* y, const uint64_
   a.mask = reinterpret_cast<const unsigned long long*>(relu_mask);
   if (fused)
     return bn_launch_fused(k_bn_bwd_fused<4>, k_bn_bwd_fused<9>, k_bn_bwd_fused<16>, k_bn_bwd_fused<33>,
-                           k_bn_bwd_fused<4, true>, k_bn_bwd_fused<9, true>, k_bn_bwd_fused<16>, c, p, st, a);
+                           k_bn_bwd_fused<4, true>, k_bn_bwd_fused<9, true>, k_bn_bwd_fused<16, kBnJoint16Bwd>, c, p, st, a);
   const bool vec = al16(dy) && al16(x) && (!relu || al16(y)) && (!dx || al16(dx)) && (!dres || al16(dres));
   const unsigned blocks = (unsigned)cdiv((long long)R * p, (long long)a.chunk);
   if (vec) {

@@ -155,7 +155,8 @@ def test_fp16_math_pair(kind, cin, cout, h, w, d):
 
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("c,h,w,res,relu", [(256, 65, 129, True, True), (64, 129, 257, False, True),
-                                            (1024, 33, 65, False, False), (64, 256, 512, False, True)])
+                                            (1024, 33, 65, False, False), (64, 256, 512, False, True),
+                                            (256, 96, 161, False, True), (128, 96, 161, True, True)])
 def test_bn_pair_bit_identical(c, h, w, res, relu, fused):
     prev = ops.set_bn_fused(fused)
     try:
