@@ -23,7 +23,6 @@
 // buffered, one barrier per K-step.  Small GEMMs are split along K into fp32
 // slabs that a reduce kernel sums deterministically (fixed order).
 #include "dconv_kernels.h"
-#include "dconv_w1.h"
 
 namespace msl {
 
@@ -437,9 +436,6 @@ static size_t img_planes_bytes(int cimg, int P) { return align_up((size_t)cdiv(c
 // pixels per wave, half the A-fragment LDS reads per MFMA of the 1 x 4 layout, no split in the loop)
 constexpr int kBqMinM = 1 << 30;
 static bool bq_form(int taps, int M, bool small_f16) { return taps == 9 && !small_f16 && M >= kBqMinM; }
-// r06: the 3x3 f16x3 / fp16 GEMMs with 128-row tiles run the W1 form (dconv_w1.h)
-constexpr int kW1MinM = 1 << 30;
-static bool w1_form(int taps, int M, bool small_f16) { return taps == 9 && !small_f16 && M >= kW1MinM; }
 
 // The stream-K schedule of a forward-form launch over at most nw_max workers (see launch_fwd_form)
 static SkArgs plan_sk(int tiles_m, int tiles_n, int KS, int nw_max, int hybrid, float* part) {
@@ -458,11 +454,8 @@ static SkArgs plan_sk(int tiles_m, int tiles_n, int KS, int nw_max, int hybrid, 
   sk.T = (int)T;
   return sk;
 }
-static bool w1_form(int taps, int M, bool small_f16);
 static bool bp_form(int taps, int M, bool small_f16, bool h1 = false) {
-  // (the W1 form reads only the pre-split planes)
-  return taps == 9 && !small_f16 &&
-         (M >= 512 || (h1 && M >= 128) || bq_form(taps, M, small_f16) || w1_form(taps, M, small_f16));
+  return taps == 9 && !small_f16 && (M >= 512 || (h1 && M >= 128) || bq_form(taps, M, small_f16));
 }
 static size_t fwd_ws_bytes(const FwdPlan& pl, int M, int P, int cimg, int taps) {
   // the planes only where the BP form can run (the stem / pointwise calls reserved them too).  The
@@ -682,21 +675,6 @@ static int launch_fwd_form(const float* img, int cimg, const float* packed, int 
             MSL_LAUNCH(k_split_img<2>, sgrid, block, 0, st, img, cimg, a.ncb, P, a.bpart, a.bnpart, planes);
           MSL_CHECK_LAUNCH();
           a.Bx6 = planes;
-        }
-        if (w1_form(taps, M, small_f16) && !accum) {
-          // the W1 form (r06, dconv_w1.h): 128 x 256 tiles at one wave per SIMD, 256 stream-K workers
-          const long long tiles1 = (long long)pl.tiles_m * cdiv(P, kW1BN);
-          if (tiles1 * sk.KS * kW1NW >= (1LL << 31)) return MSL_ERR_SHAPE;
-          const SkArgs s1 = plan_sk(pl.tiles_m, cdiv(P, kW1BN), sk.KS, kW1NW, forms_of(forms).sk_hybrid, (float*)ws);
-          static_assert((size_t)kW1NW * 2 * kW1BM * kW1BN <= (size_t)kSkNW * 2 * 128 * kSkBN, "W1 pieces fit");
-          const dim3 g1(s1.tdp > 0 ? kW1NW : s1.NW);
-          MSL_LAUNCH((k_igemm_fwd_w1<MT>), g1, block, 0, st, a, s1);
-          MSL_CHECK_LAUNCH();
-          if (s1.T > 0)
-            MSL_LAUNCH((k_sk_reduce<kW1BM, kW1BN>), dim3(kW1BM * kW1BN / 1024, (unsigned)(tiles1 - s1.tdp)), block, 0,
-                       st, a, s1);
-          MSL_CHECK_LAUNCH();
-          return MSL_OK;
         }
         // pointwise: B rows are unshifted, so they move as dwordx4 (4 pixels per lane: 2 DMAs per
         // wave and K-step instead of 8 dword ones): 1-4 us per call on the wide 1x1 GEMMs
