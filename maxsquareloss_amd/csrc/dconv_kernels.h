@@ -413,6 +413,19 @@ __device__ __forceinline__ void mfma_stage_x6p(const float* As, const float* Bs,
   }
 }
 
+// r06: s_setprio(1) around a wave's MFMA cluster (cdna_hip_programming.md T5): of a SIMD's two waves (two
+// workgroups) the one in its MFMA phase wins the issue arbitration over the one reading fragments / splitting,
+// so its cluster issues back to back.  BD f16x3 stages (kMfmaPrio): layer3 forward 83.0 -> 76.6 us, step
+// -0.14 ms; the weight gradient's clusters too (kMfmaPrioWg, neutral to -0.05 ms); the LDS-form and fp16 stages
+// (kMfmaPrioLds) measured neutral on configs 2 and 5 and stay off (profiles/r06_mfma_prio_ab.txt).
+constexpr bool kMfmaPrio = true;
+constexpr bool kMfmaPrioLds = false;
+constexpr bool kMfmaPrioWg = true;
+template <bool ON, int P>
+__device__ __forceinline__ void mfma_prio() {
+  if constexpr (ON) __builtin_amdgcn_s_setprio(P);
+}
+
 // f16x3 stage: A fragments from the pre-split fp16 planes (one LDS stage = G K-steps of
 // [plane][half][BM][8] fp16, 16*BM floats each), B fragments scaled by sB and split as they are read.
 template <int G, int TM, int TN, int BM, int LDB_S, typename F>
@@ -442,12 +455,14 @@ __device__ __forceinline__ void mfma_stage_h3p(const float* As, const float* Bs,
         Split2h av;
         av.lo = Ab[(2 + h) * BM + wm + i * 32 + l32];
         av.hi = Ab[h * BM + wm + i * 32 + l32];
+        mfma_prio<kMfmaPrioLds, 1>();
 #pragma unroll
         for (int t = 0; t < TN; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av.lo, bv[t].hi, acc[i][t], 0, 0, 0);
 #pragma unroll
         for (int t = 0; t < TN; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av.hi, bv[t].lo, acc[i][t], 0, 0, 0);
 #pragma unroll
         for (int t = 0; t < TN; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av.hi, bv[t].hi, acc[i][t], 0, 0, 0);
+        mfma_prio<kMfmaPrioLds, 0>();
       }
       if (kk == 0) mid();
       continue;
@@ -471,6 +486,7 @@ __device__ __forceinline__ void mfma_stage_h3p(const float* As, const float* Bs,
       for (int t = 0; t < TN; ++t) split2h_set(bv[t], j, braw[t][j] * sB);
     // product-major order: the TM*TN accumulators of one product are independent, so its MFMAs
     // issue back to back, and every A fragment is in registers before the first one
+    mfma_prio<kMfmaPrioLds, 1>();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -486,6 +502,7 @@ __device__ __forceinline__ void mfma_stage_h3p(const float* As, const float* Bs,
 #pragma unroll
       for (int t = 0; t < TN; ++t)
         acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv[t].hi, acc[i][t], 0, 0, 0);
+    mfma_prio<kMfmaPrioLds, 0>();
     if (kk == 0) mid();
   }
 }
@@ -513,10 +530,12 @@ __device__ __forceinline__ void mfma_stage_h1p(const float* As, const float* Bs,
     for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int t = 0; t < TN; ++t) bv[t][j] = (_Float16)(braw[t][j] * sB);
+    mfma_prio<kMfmaPrioLds, 1>();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int t = 0; t < TN; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bv[t], acc[i][t], 0, 0, 0);
+    mfma_prio<kMfmaPrioLds, 0>();
     if (kk == 0) mid();
   }
 }
@@ -537,8 +556,10 @@ __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane,
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) bv[j] = (_Float16)xf(j, braw[j]);
+    mfma_prio<kMfmaPrioLds, 1>();
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bv, acc[i][0], 0, 0, 0);
+    mfma_prio<kMfmaPrioLds, 0>();
   } else {
     Split2h av[TM], bv;
 #pragma unroll
@@ -552,12 +573,14 @@ __device__ __forceinline__ void mfma_stage_hd(const float* As, int wm, int lane,
 #pragma unroll
       for (int j = 0; j < 8; ++j) split2h_set(bv, j, xf(j, braw[j]));
     }
+    mfma_prio<kMfmaPrio, 1>();
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].lo, bv.hi, acc[i][0], 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv.lo, acc[i][0], 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bv.hi, acc[i][0], 0, 0, 0);
+    mfma_prio<kMfmaPrio, 0>();
   }
   mid();
 }
@@ -583,17 +606,20 @@ __device__ __forceinline__ void mfma_stage_hdp(const float* As, int wm, int lane
     f16x8 av[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[i] = Ab[h * BM + wm + i * 32 + l32];
+    mfma_prio<kMfmaPrioLds, 1>();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int t = 0; t < TN; ++t)
         acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bh[t].h, acc[i][t], 0, 0, 0);
+    mfma_prio<kMfmaPrioLds, 0>();
   } else {
     Split2h av[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[i].lo = Ab[(2 + h) * BM + wm + i * 32 + l32];
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[i].hi = Ab[h * BM + wm + i * 32 + l32];
+    mfma_prio<kMfmaPrio, 1>();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -609,6 +635,7 @@ __device__ __forceinline__ void mfma_stage_hdp(const float* As, int wm, int lane
 #pragma unroll
       for (int t = 0; t < TN; ++t)
         acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i].hi, bh[t].h, acc[i][t], 0, 0, 0);
+    mfma_prio<kMfmaPrio, 0>();
   }
   mid();
 }
@@ -2288,6 +2315,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
         for (int jj = 0; jj < TN; ++jj)
           bv[jj] = *reinterpret_cast<const f16x8*>(Bs + kh * RB + (wn + jj * 32 + l32) * 16);
+        mfma_prio<kMfmaPrioWg, 1>();
 #pragma unroll
         for (int ii = 0; ii < TM; ++ii) {
           union { u32x4 u; f16x8 h; } c0;
@@ -2296,6 +2324,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
           for (int jj = 0; jj < TN; ++jj)
             acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(c0.h, bv[jj], acc[ii][jj], 0, 0, 0);
         }
+        mfma_prio<kMfmaPrioWg, 0>();
         return;
       } else if constexpr (H3) {
         Split2h bv[TN];
@@ -2305,6 +2334,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
           bv[jj].hi = *reinterpret_cast<const f16x8*>(src);
           bv[jj].lo = *reinterpret_cast<const f16x8*>(src + 2 * RB);
         }
+        mfma_prio<kMfmaPrioWg, 1>();
 #pragma unroll
         for (int ii = 0; ii < TM; ++ii) {
           union { u32x4 u; f16x8 h; } c0, c1;
@@ -2314,6 +2344,7 @@ __global__ void __launch_bounds__(256, 2) k_wgrad_x6(WskArgs a) {
 #pragma unroll
           for (int jj = 0; jj < TN; ++jj) acc[ii][jj] = mfma_h3(av, bv[jj], acc[ii][jj]);
         }
+        mfma_prio<kMfmaPrioWg, 0>();
         return;
       }
       Split3 bv[TN];
