@@ -235,7 +235,7 @@ def test_source_step_cfg0_matches_goldens():
     The bs=1 random-init network is chaotic from the second iteration on: fp32 rounding of the
     first update (a few % of the stem's gradient) changes the second update by 30-90 % in every
     fp32 implementation (the CPU oracle vs an fp64 oracle on the same host, measured on the GPU
-    box: scripts/diag_src_updates.py), so the reference's own fp32 runs on two hosts disagree on
+    box in r02 with a diagnostic script since deleted, commit b6a08cc), so the reference's own fp32 runs on two hosts disagree on
     src_param_sum by far more than rounding.  The bars are therefore:
       it0: loss within 1e-3 of the golden and the oracle; the update per tensor within 3x the fp32
            oracle's own distance to the fp64 oracle;
