@@ -833,6 +833,8 @@ static int pack(const float* w, long long branch_stride, int nbranch, int taps, 
 // (256 -> 1024: a 256-row split instead of a 1024-row one, ~10 vs ~20 us) - and the reduce writes
 // the dW^T tiles transposed.
 static bool wgrad_swaps(int nbranch, int taps, int cin, int cout) { return nbranch == 1 && taps == 1 && cout > cin; }
+// k_wgrad_x6's piece reduce in the [m][n] orientation: waves per 64 outputs (1 = k_wsk_reduce's single chain)
+constexpr int kWskSplit = 4, kWskSplitMinPieces = 16;
 
 static size_t wgrad_core_bytes(int nbranch, int taps, int cin, int cout, int P, int w) {
   // large enough for either fp32 form and orientation: pieces, then (k_wgrad_x6) the split planes
@@ -952,7 +954,14 @@ static int launch_wgrad(const float* x, const float* dy, float* dw, float* dbias
       MSL_LAUNCH(k_wgrad_x6<kMathX6>, grid, block, 0, st, a);
     }
     MSL_CHECK_LAUNCH();
-    MSL_LAUNCH((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
+    // r06: S waves per 64 outputs, each summing every S-th piece (k_wsk_reduce_split), where a tile has >= 16 pieces
+    // (the 16- and 9-tile layer3 1x1 / layer2 3x3 gradients: 32-56 chunks; at 8 pieces, 512 -> 2048, it lost 4 us)
+    const long long tile_pieces = pl.nchunk > 0 ? pl.nchunk : cdiv((long long)pl.nw, (long long)a.ntiles);
+    if (kWskSplit > 1 && tile_pieces >= kWskSplitMinPieces)
+      MSL_LAUNCH((k_wsk_reduce_split<128, 128, kWskSplit>), dim3(cdiv(128LL * 128 / 4 * taps, 64), rgrid.y),
+                 dim3(64 * kWskSplit), 0, st, a);
+    else
+      MSL_LAUNCH((k_wsk_reduce<128, 128>), rgrid, rblock, 0, st, a);
   } else if (pl.bm == 128) {
     MSL_LAUNCH((k_wgrad_sk<128, 128, 2, 2, 2, MB>), grid, block, 0, st, a);
     MSL_CHECK_LAUNCH();

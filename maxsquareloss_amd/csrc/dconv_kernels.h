@@ -1947,6 +1947,121 @@ __global__ void __launch_bounds__(256) k_wsk_reduce_wide(WskArgs a) {
     if (c < nn) dst[c * a.taps] = vals[c];
 }
 
+// r06: k_wsk_reduce's [m][n] (not transposed) form with S waves per block summing disjoint, interleaved subsets of
+// a tile's pieces: wave s adds pieces w_lo + s, w_lo + s + S, ... in order for 64 consecutive float4 outputs
+// (each load a coalesced 1-KB run of one piece), and wave 0 adds the S partial sums in s order (deterministic;
+// a different, fixed association than k_wsk_reduce's single chain).  One chain per output put 8 loads in flight
+// per thread at one 256-thread block per (tile, 64 outputs): the 1 x 1 1024 -> 256 reduce read its 32 MB of
+// pieces at ~2.7 TB/s.  grid = (ceil(BM*BN/4 * taps / 64), tiles_m * tiles_n * nbranch), block 64 * S.
+template <int BM, int BN, int S>
+__global__ void __launch_bounds__(64 * S) k_wsk_reduce_split(WskArgs a) {
+  static_assert(S >= 4, "the transposed form writes 256 values per block");
+  constexpr int PSZ = BM * BN, P4 = PSZ / 4;
+  __shared__ float4 red[64 * S];
+  const int gsz = a.tiles_m * a.tiles_n;
+  const int br = blockIdx.y / gsz;
+  const int rem = blockIdx.y - br * gsz;
+  const int tn = rem / a.tiles_m, tm = rem - tn * a.tiles_m;
+  const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  // trans (pointwise, operands swapped; taps = 1): block = an 8-row x 32-column sub-tile (64 float4), transposed
+  // through LDS below; else 64 consecutive float4 of the [tap][m][n] piece layout
+  const int sr = blockIdx.x >> 2, sc = blockIdx.x & 3;
+  const int e = a.trans ? ((sr * 8 + (o >> 3)) * BN + sc * 32 + (o & 7) * 4) / 4 : blockIdx.x * 64 + o;
+  const int tap = e / P4, g4 = e - tap * P4;
+  const bool live = tap < a.taps;
+  const int t = ((br * a.taps + (live ? tap : 0)) * a.tiles_n + tn) * a.tiles_m + tm;
+  const float4* __restrict__ part = reinterpret_cast<const float4*>(a.part);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    const int w_lo = a.nchunk > 0 ? 0 : sk_worker_of(t * a.KS, a.T, a.NW);
+    const int w_hi = a.nchunk > 0 ? a.nchunk - 1 : sk_worker_of((t + 1) * a.KS - 1, a.T, a.NW);
+    auto piece = [&](int wc) {
+      if (a.nchunk > 0) return part[(long long)(wc * a.ntiles + t) * a.slots * P4 + g4];
+      return part[(long long)(wc * a.slots + t - sk_start(wc, a.T, a.NW) / a.KS) * P4 + g4];
+    };
+    for (int wc = w_lo + sl; wc <= w_hi; wc += 4 * S) {  // four loads in flight, added in order
+      float4 p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (wc + u * S <= w_hi) p[u] = piece(wc + u * S);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (wc + u * S <= w_hi) {
+          acc.x += p[u].x;
+          acc.y += p[u].y;
+          acc.z += p[u].z;
+          acc.w += p[u].w;
+        }
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  float4 v = red[o];
+  if (sl == 0) {
+#pragma unroll
+    for (int q = 1; q < S; ++q) {
+      const float4 u = red[q * 64 + o];
+      v.x += u.x;
+      v.y += u.y;
+      v.z += u.z;
+      v.w += u.w;
+    }
+  }
+  const int m = tm * BM + (g4 * 4) / BN, n = tn * BN + (g4 * 4) % BN;
+  if (a.trans) {  // dW^T: wave 0's sums (rowscaled) to LDS, then every thread writes one of 32 dW rows x 8 columns
+    __shared__ float tt[8][33];
+    if (sl == 0) {
+      float sv[4] = {v.x, v.y, v.z, v.w};
+      if (a.rowscale) {  // tile element (m, n): 1 / (s_m t_n), exact
+        float ia, ib;
+        pow2_scale(a.apart[min(a.M - 1, m)], ia);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pow2_scale(a.bpart[min(a.N - 1, n + q)], ib);
+          sv[q] = sv[q] * ia * ib;
+        }
+      }
+      const int r = o >> 3, c4 = (o & 7) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tt[r][c4 + q] = sv[q];
+    }
+    __syncthreads();
+    if (threadIdx.x >= 256) return;
+    const int j = threadIdx.x >> 3, i = threadIdx.x & 7;  // dW row n0 + j (a cout), column m0 + i
+    const int nr = tn * BN + sc * 32 + j, mc = tm * BM + sr * 8 + i;
+    if (nr >= a.N || mc >= a.M) return;
+    float* dst = a.dw + (long long)nr * a.M + mc;
+    float val = tt[i][j];
+    if (a.accumulate) val = *dst + val;
+    *dst = val;
+    return;
+  }
+  if (sl != 0 || !live) return;
+  if (m >= a.M || n >= a.N) return;
+  float* dst = a.dw + br * a.cbranch + ((long long)m * a.N + n) * a.taps + tap;
+  float vals[4] = {v.x, v.y, v.z, v.w};
+  const int nn = min(4, a.N - n);
+  if (a.rowscale) {  // per-row f16x3 scales (k_wgrad_x6): dW[m][n] / (s_m t_n), exact
+    float ia, ib;
+    pow2_scale(a.apart[m], ia);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      pow2_scale(a.bpart[min(a.N - 1, n + c)], ib);
+      vals[c] = vals[c] * ia * ib;
+    }
+  }
+  if (a.accumulate) {  // all old values loaded before the first store
+    float old[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) old[c] = c < nn ? dst[c * a.taps] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) vals[c] = old[c] + vals[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (c < nn) dst[c * a.taps] = vals[c];
+}
+
 // ---------------------------------------------------------------------------------------------
 // bf16x6 weight gradient, register-staged (the layer2-4 and ASPP-free x6 path).
 //
