@@ -78,9 +78,14 @@ def test_f16_wgrad_predicate_matches_library(H, W, C):
 
 
 def test_library_is_gfx950_code_object():
+    import shutil
+    import tempfile
     from maxsquareloss_amd import hip
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", hip.LIB_PATH],
-                         capture_output=True, text=True, cwd="/tmp")
+    # (llvm-objdump --offloading extracts the bundles next to its input: work on a copy outside the tree)
+    with tempfile.TemporaryDirectory() as d:
+        lib = shutil.copy(hip.LIB_PATH, d)
+        out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
+                             capture_output=True, text=True, cwd=d)
     assert "gfx950" in (out.stdout + out.stderr)
 
 
